@@ -1,0 +1,45 @@
+/* kinet_amd C-ABI: shared types.
+ *
+ * Every entry point takes raw device pointers + sizes + a hipStream_t, launches
+ * asynchronously on that stream (the caller's current stream, as the reference
+ * launcher does with at::cuda::getCurrentCUDAStream(), ms_deform_attn_cuda.cu:70),
+ * never allocates, never synchronises, and returns a status code.  A non-zero
+ * status leaves a message readable through kinet_last_error() (thread-local); the
+ * Python shim raises it as RuntimeError, mirroring AT_ASSERTM -> c10::Error in the
+ * reference (ms_deform_attn_cuda.cu:29-34, :48).
+ */
+#ifndef KINET_COMMON_H_
+#define KINET_COMMON_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* kinet_stream_t; /* == hipStream_t */
+
+enum kinet_dtype {
+    KINET_F32 = 0,
+    KINET_BF16 = 1,
+    KINET_F16 = 2,
+    KINET_F64 = 3,
+};
+
+enum kinet_status {
+    KINET_OK = 0,
+    KINET_ERR_ARG = 1,   /* invalid argument / unsupported shape or dtype */
+    KINET_ERR_HIP = 2,   /* HIP runtime error at launch */
+};
+
+/* Text of the last error raised on this host thread ("" if none). */
+const char* kinet_last_error(void);
+
+/* Library build identifier (gfx target + git-free build stamp). */
+const char* kinet_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KINET_COMMON_H_ */

@@ -1,0 +1,51 @@
+/* kinet_amd C-ABI: MFMA GEMM and implicit-GEMM NHWC convolution with fused epilogues.
+ *
+ * Replaces, on the detection hot path, the cuBLAS/cuDNN work the reference delegates
+ * to PyTorch ("Dense ops on the hot path"):
+ *   nn.Linear in MSDeformAttn          (ms_deform_attn.py:27-30)
+ *   FFN linear1/linear2                (deformable_transformer.py:273-276, 350-353)
+ *   nn.MultiheadAttention in/out proj  (deformable_transformer.py:345, :371)
+ *   class / bbox MLP heads             (deformable_detr.py:98-108, detr.py:937-951)
+ *   ResNet convs + FrozenBatchNorm2d   (backbone.py:22-58, :102)  -- BN folded into scale/bias
+ *   input_proj 1x1 / 3x3-s2 convs      (deformable_detr.py:63-71)
+ *
+ *   C[m, n] = epi( sum_k A[m, k] * B[n, k] )
+ *   epi(v)  = relu?( v * scale[n] + bias[n] + R[m, n] ),  rows with row_mask[m] != 0 -> 0
+ *
+ * A, B, C, R row-major with leading dims lda, ldb, ldc, ldr (elements).  B is the
+ * PyTorch weight layout (out_features, in_features), i.e. K-contiguous.  scale/bias
+ * are f32 (NULL = 1 / 0).  in_dtype in {F32, BF16, F16} for A and B; out_dtype for C
+ * and R in {F32, BF16, F16}.  bf16/f16 run v_mfma_f32_16x16x32_{bf16,f16}; f32 runs the
+ * exact-f32 v_mfma_f32_16x16x4_f32 (parity mode).  Requirements: K % 8 == 0, lda/ldb
+ * multiples of 8, 16-byte aligned A/B.
+ */
+#ifndef KINET_GEMM_H_
+#define KINET_GEMM_H_
+
+#include "kinet_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int kinet_gemm(const void* A, const void* B, void* C, int M, int N, int K,
+               int lda, int ldb, int ldc, int in_dtype,
+               const float* scale, const float* bias, const void* R, int ldr,
+               int relu, int out_dtype, const uint8_t* row_mask, int reserved,
+               kinet_stream_t stream);
+
+/* Convolution, NHWC activations, weights (Cout, KH, KW, Cin) = PyTorch OIHW permuted.
+ *   X (batch, Hin, Win, Cin) with Cin % 8 == 0 (pad channels with zeros otherwise)
+ *   Y (batch, Hout, Wout, Cout) written with row stride ldy (>= Cout) so outputs can land
+ *   directly inside a larger flattened buffer; R residual with the same layout (ldr).
+ *   Hout = (Hin + 2*pad - KH) / stride + 1 (dilation 1). */
+int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin,
+                 int Hout, int Wout, int Cout, int KH, int KW, int stride, int pad,
+                 int in_dtype, const float* scale, const float* bias, const void* R, int ldr,
+                 int relu, int ldy, kinet_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KINET_GEMM_H_ */

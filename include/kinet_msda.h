@@ -1,0 +1,84 @@
+/* kinet_amd C-ABI: multi-scale deformable attention (MSDeformAttn) sampling.
+ *
+ * Drop-in for the reference extension module `MultiScaleDeformableAttention`
+ * (src/trackformer/models/ops/src/vision.cpp:4-7), whose two pybind functions
+ *   ms_deform_attn_forward  -> ms_deform_attn.h:10-28  -> ms_deform_attn_cuda.cu:19-86
+ *   ms_deform_attn_backward -> ms_deform_attn.h:30-49  -> ms_deform_attn_cuda.cu:89-168
+ * are re-exposed by kinet_amd/MultiScaleDeformableAttention.py on top of these symbols.
+ *
+ * Layouts (all contiguous, row-major, as in ms_deform_attn_cuda.cu:25-27):
+ *   value          (N, S, M, D)            value_dtype
+ *   spatial_shapes (L, 2) int64 (H, W)     DEVICE memory (as the reference passes it)
+ *   sampling_loc   (N, Lq, M, L, P, 2)     loc_dtype, [x, y] in [0,1] (cuh:220-221)
+ *   attn_weight    (N, Lq, M, L, P)        loc_dtype
+ *   output         (N, Lq, M*D)            value_dtype, channel = m*D + d (cu:83)
+ * level_start_index is derived on the device from spatial_shapes (the reference
+ * builds it with per-level ATen ops, cu:52-58); a level whose start + H*W exceeds S
+ * contributes zero instead of reading out of bounds.
+ *
+ * dtypes: value in {F32, F64, BF16, F16}; loc_dtype == value_dtype for F32/F64 (the
+ * reference's AT_DISPATCH_FLOATING_TYPES, cu:69), loc_dtype == F32 for BF16/F16 (perf
+ * mode).  Accumulation is f32 (f64 for F64).
+ *
+ * im2col_step is accepted for signature parity and validated exactly like the
+ * reference (step = min(N, im2col_step); N % step == 0, cu:46-48), but does not
+ * change the launch: there is no `columns` staging buffer here.
+ */
+#ifndef KINET_MSDA_H_
+#define KINET_MSDA_H_
+
+#include "kinet_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* replaces ms_deform_attn_cuda_forward (ms_deform_attn_cuda.cu:19-86) */
+int kinet_msda_forward(const void* value, const int64_t* spatial_shapes,
+                       const void* sampling_loc, const void* attn_weight, void* output,
+                       int batch, int spatial_size, int num_heads, int channels,
+                       int num_levels, int num_query, int num_point, int im2col_step,
+                       int value_dtype, int loc_dtype, kinet_stream_t stream);
+
+/* replaces ms_deform_attn_cuda_backward (ms_deform_attn_cuda.cu:89-168).
+ * grad_value (N,S,M,D) value_dtype, grad_loc (N,Lq,M,L,P,2) and grad_attw (N,Lq,M,L,P)
+ * loc_dtype; all three are fully overwritten (the reference zero-fills, cu:119-121).
+ * For BF16/F16 value, `workspace` must hold N*S*M*D floats (f32 accumulation of
+ * grad_value); it may be NULL for F32/F64.  kinet_msda_backward_workspace_bytes()
+ * returns the required size. */
+int kinet_msda_backward(const void* value, const int64_t* spatial_shapes,
+                        const void* sampling_loc, const void* attn_weight,
+                        const void* grad_output, void* grad_value, void* grad_loc,
+                        void* grad_attw, void* workspace,
+                        int batch, int spatial_size, int num_heads, int channels,
+                        int num_levels, int num_query, int num_point, int im2col_step,
+                        int value_dtype, int loc_dtype, kinet_stream_t stream);
+
+int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num_heads,
+                                            int channels, int value_dtype);
+
+/* Fused module path (MSDeformAttn.forward, ms_deform_attn.py:49-88): computes
+ *   attw = softmax over L*P of logits            (ms_deform_attn.py:70-71)
+ *   attw = 0 where query_attn_mask               (:73-74, optional, uint8 (N,Lq))
+ *   loc  = ref + off / shapes[(H,W)]   (2-d refs, x divided by H: reference quirk :77-79)
+ *   loc  = ref_xy + off / P * ref_wh * 0.5       (4-d refs, :80-82)
+ * and samples, without materialising loc/attw in HBM.
+ *   offsets_logits  (N, Lq, ld_off) f32 rows holding [M*L*P*2 offsets | M*L*P logits]
+ *                   (the concatenated sampling_offsets/attention_weights projection)
+ *   ref_points      (N, Lq, L, ref_dim) f32, ref_dim in {2, 4}
+ * Writes output (N, Lq, M*D) and, when loc_out/attw_out are non-NULL, the f32
+ * sampling_loc / attn_weight tensors (needed to run kinet_msda_backward). */
+int kinet_msda_fused_forward(const void* value, const int64_t* spatial_shapes,
+                             const void* offsets_logits, int ld_off,
+                             const float* ref_points, int ref_dim,
+                             const uint8_t* query_attn_mask,
+                             void* output, float* loc_out, float* attw_out,
+                             int batch, int spatial_size, int num_heads, int channels,
+                             int num_levels, int num_query, int num_point,
+                             int value_dtype, kinet_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KINET_MSDA_H_ */

@@ -1,0 +1,59 @@
+/* kinet_amd C-ABI: normalisation / pooling / attention kernels on the detection path.
+ * dtype codes: include/kinet_common.h.  All tensors contiguous unless a stride is given.
+ */
+#ifndef KINET_OPS_H_
+#define KINET_OPS_H_
+
+#include "kinet_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* y = LayerNorm(x (+ r)) over the last dim d (nn.LayerNorm, eps) -- the post-norm of every
+ * encoder/decoder sub-layer (deformable_transformer.py:287, :294, :374, :380, :364).
+ * x, r, y: (rows, d) in `dtype`; gamma/beta f32; r may be NULL. */
+int kinet_layernorm(const void* x, const void* r, const float* gamma, const float* beta, void* y,
+                    int rows, int d, float eps, int dtype, int reserved, kinet_stream_t stream);
+
+/* nn.GroupNorm(groups, C) on NHWC input (deformable_detr.py:64, :70):
+ * x (N, HW, C) contiguous; y written at y + n*y_batch_stride + p*C + c (so a level can land
+ * inside the flattened multi-level src buffer, deformable_transformer.py:145-153).
+ * `stats`: caller-provided scratch of 2*N*groups floats (zeroed by the call). */
+int kinet_groupnorm(const void* x, const float* gamma, const float* beta, void* y,
+                    int N, int HW, int C, int groups, int y_batch_stride, float eps, int dtype,
+                    float* stats, kinet_stream_t stream);
+
+/* ResNet stem max-pool 3x3/2 pad 1 (torchvision), NHWC. */
+int kinet_maxpool2d_3x3s2(const void* x, void* y, int N, int H, int W, int C, int dtype,
+                          kinet_stream_t stream);
+
+/* (N, 3, H, W) f32 NCHW image -> (N, H, W, Cpad) NHWC in dtype, channels >= 3 zero. */
+int kinet_pack_image_nhwc(const float* x, void* y, int N, int H, int W, int Cpad, int dtype,
+                          kinet_stream_t stream);
+
+/* y = a + b, n elements. */
+int kinet_add(const void* a, const void* b, void* y, int64_t n_lo, int dtype, kinet_stream_t stream);
+
+/* Scaled-dot-product core of nn.MultiheadAttention (deformable_transformer.py:371):
+ *   O[b, i, h*D:(h+1)*D] = softmax_j( Q_bh[i] . K_bh[j] * scale  (-inf where key_mask[b,j]) ) V_bh[j]
+ * Q/K/V/O row-major with row strides ldq/ldk/ldv/ldo (elements), batch strides = rows*ld. */
+int kinet_mha_core(const void* Q, int ldq, const void* Kt, int ldk, const void* V, int ldv,
+                   void* O, int ldo, int batch, int Lq, int Lk, int heads, int head_dim,
+                   float scale, int dtype, const uint8_t* key_mask, kinet_stream_t stream);
+
+/* Iterative box refinement (deformable_transformer.py:414-425) fused with the next
+ * layer's reference input (:406-411):
+ *   new_ref = sigmoid(tmp + inverse_sigmoid(ref))        (ref_dim 4)
+ *   new_ref = sigmoid([tmp[:2] + inverse_sigmoid(ref), tmp[2:]])   (ref_dim 2)
+ *   ref_input[b,q,l,:] = new_ref * [vr_l, vr_l]
+ * tmp (N*Q, 4) f32, ref (N*Q, ref_dim) f32, valid_ratios (N, L, 2) f32;
+ * new_ref (N*Q, 4) f32, ref_input (N*Q, L, 4) f32. */
+int kinet_box_refine(const float* tmp, const float* ref, int ref_dim, const float* valid_ratios,
+                     float* new_ref, float* ref_input, int N, int Q, int L, kinet_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KINET_OPS_H_ */

@@ -1,0 +1,103 @@
+"""ctypes binding of the kinet_amd C-ABI (include/*.h) -> kinet_amd/_lib/libkinet_amd.so.
+
+There is deliberately NO fallback: if the library is missing or fails to load, every
+op raises.  (The reference behaves the same way -- MultiScaleDeformableAttention is
+imported at module import time, ms_deform_attn_func.py:11, and its CPU branch is an
+AT_ERROR, ms_deform_attn.h:27.)
+"""
+import ctypes
+import os
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libkinet_amd.so')
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+F = ctypes.c_float
+
+# symbol -> argtypes (restype int unless listed in _RESTYPES)
+_SIGS = {
+    'kinet_msda_forward': [P, P, P, P, P] + [I] * 10 + [P],
+    'kinet_msda_backward': [P] * 9 + [I] * 10 + [P],
+    'kinet_msda_backward_workspace_bytes': [I] * 5,
+    'kinet_msda_fused_forward': [P, P, P, I, P, I, P, P, P, P] + [I] * 8 + [P],
+    'kinet_gemm': [P, P, P] + [I] * 7 + [P, P, P, I, I, I, P, I, P],
+    'kinet_conv2d': [P, P, P] + [I] * 12 + [P, P, P, I, I, I, P],
+    'kinet_layernorm': [P] * 5 + [I, I, F, I, I, P],
+    'kinet_groupnorm': [P] * 4 + [I] * 5 + [F, I, P, P],
+    'kinet_maxpool2d_3x3s2': [P, P] + [I] * 5 + [P],
+    'kinet_pack_image_nhwc': [P, P] + [I] * 5 + [P],
+    'kinet_mha_core': [P, I, P, I, P, I, P, I] + [I] * 5 + [F, I, P, P],
+    'kinet_add': [P, P, P, I64, I, P],
+    'kinet_box_refine': [P, P, I, P, P, P, I, I, I, P],
+    'kinet_last_error': [],
+    'kinet_version': [],
+}
+_RESTYPES = {'kinet_last_error': ctypes.c_char_p, 'kinet_version': ctypes.c_char_p,
+             'kinet_msda_backward_workspace_bytes': ctypes.c_int64}
+
+DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
+
+_lib = None
+_load_error = None
+
+
+def lib():
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise RuntimeError(f'kinet_amd native library not built: {_LIB_PATH} missing '
+                           f'(run `python -m kinet_amd.build`)')
+    try:
+        L = ctypes.CDLL(_LIB_PATH)
+    except OSError as e:   # pragma: no cover
+        _load_error = e
+        raise RuntimeError(f'failed to load {_LIB_PATH}: {e}') from e
+    for name, args in _SIGS.items():
+        fn = getattr(L, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    _lib = L
+    return L
+
+
+def exported(name):
+    return hasattr(lib(), name)
+
+
+def call(name, *args):
+    """Invoke a C-ABI entry point and raise RuntimeError on a non-zero status."""
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if rc != 0:
+        msg = lib().kinet_last_error().decode(errors='replace')
+        raise RuntimeError(f'{name}: {msg}')
+    return rc
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def dtype_code(dt):
+    try:
+        return DT[dt]
+    except KeyError:
+        raise RuntimeError(f'kinet_amd: unsupported dtype {dt}') from None
+
+
+def require_gpu(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            # reference: AT_ASSERTM(value.type().is_cuda(), ...) (ms_deform_attn_cuda.cu:31-34)
+            raise RuntimeError('kinet_amd ops run on the GPU only: got a CPU tensor '
+                               '(the reference CPU branch is AT_ERROR too, ms_deform_attn.h:27)')

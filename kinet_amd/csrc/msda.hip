@@ -1,0 +1,593 @@
+// Multi-scale deformable attention sampling for gfx950 (CDNA4).
+//
+// Replaces the reference's three CUDA kernels (ms_deform_im2col_cuda.cuh:165-378) and
+// their launcher (ms_deform_attn_cuda.cu:19-168).  Design (DESIGN.md "MSDA kernels"):
+//
+//  * one workgroup = QT consecutive queries x all M heads of one batch image;
+//  * phase 1 ("setup"): one thread per sample (q, m, l, p) reads its location and
+//    attention weight with coalesced loads (or computes them from the raw projection in
+//    the fused module path), and stages the 4 bilinear tap row-offsets + tap weights in
+//    LDS -- the bilinear arithmetic happens once per sample, not once per channel as in
+//    the reference (which recomputes it for each of the D channel threads, cuh:227-231);
+//  * phase 2 ("gather"): LPQ lanes per (q, m) pair, each owning VEC contiguous channels,
+//    read the staged taps (LDS broadcast) and issue 16-byte vector loads of the value
+//    rows; accumulation in f32 registers; the output is written once.  No (L*P)x larger
+//    `columns` buffer and no separate at::sum reduction (cu:68, :80).
+//  * backward: the same setup; each lane computes the three channel-partial sums
+//    (attention-weight grad, d/dx, d/dy) in one pass over the taps (the reference walks
+//    the taps twice per coordinate and per channel, cuh:356-372) and scatters
+//    grad_value with f32 atomics over its contiguous channels (cuh:301 scans a 5x5
+//    neighbourhood per channel to find the same 4 taps).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include <type_traits>
+
+#include "../../include/kinet_msda.h"
+#include "common.h"
+
+namespace kinet {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxLevels = 16;
+
+template <typename T, int VEC>
+struct alignas(sizeof(T) * VEC) VecT {
+    T v[VEC];
+};
+
+struct LevelInfo {
+    int start[kMaxLevels];
+    int H[kMaxLevels];
+    int W[kMaxLevels];
+    int ok[kMaxLevels];
+};
+
+// level_start_index from spatial_shapes (cu:52-58), computed per block in LDS; a level
+// that would run past S is disabled instead of reading out of bounds.
+__device__ __forceinline__ void load_levels(LevelInfo& li, const int64_t* shapes, int L, int S) {
+    if (threadIdx.x == 0) {
+        long long acc = 0;
+        for (int l = 0; l < L; ++l) {
+            const long long H = shapes[2 * l], W = shapes[2 * l + 1];
+            li.start[l] = (int)acc;
+            li.H[l] = (int)H;
+            li.W[l] = (int)W;
+            li.ok[l] = (H > 0 && W > 0 && acc + H * W <= S) ? 1 : 0;
+            acc += H * W;
+        }
+    }
+}
+
+template <typename TL> __device__ __forceinline__ float ldf(const TL* p) { return (float)*p; }
+
+// ---------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------
+// Per-sample setup record in LDS: tap element offsets (within one batch image) and the
+// four tap weights already multiplied by the attention weight (0 for taps/samples
+// outside the image, with a safe offset so phase 2 needs no branch).
+struct Tap4 {
+    int off[4];
+    float w[4];
+};
+
+template <typename T, typename TL>
+__device__ __forceinline__ void setup_sample(Tap4& t, float x, float y, float a, const LevelInfo& li,
+                                             int l, int MD, int m, int D) {
+    const int H = li.H[l], W = li.W[l];
+    const float h = y * (float)H - 0.5f;   // cuh:227
+    const float w = x * (float)W - 0.5f;   // cuh:228
+    const int base = m * D;
+    int o0 = base, o1 = base, o2 = base, o3 = base;
+    float w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
+    if (li.ok[l] && h > -1.f && w > -1.f && h < (float)H && w < (float)W) {   // cuh:229
+        const float hf = floorf(h), wf = floorf(w);
+        const int hl = (int)hf, wl = (int)wf;
+        const float lh = h - hf, lw = w - wf, hh = 1.f - lh, hw = 1.f - lw;
+        const int rowbase = li.start[l];
+        const bool h0 = hl >= 0, h1 = hl + 1 <= H - 1, c0 = wl >= 0, c1 = wl + 1 <= W - 1;
+        if (h0 && c0) { o0 = (rowbase + hl * W + wl) * MD + base; w0 = hh * hw * a; }
+        if (h0 && c1) { o1 = (rowbase + hl * W + wl + 1) * MD + base; w1 = hh * lw * a; }
+        if (h1 && c0) { o2 = (rowbase + (hl + 1) * W + wl) * MD + base; w2 = lh * hw * a; }
+        if (h1 && c1) { o3 = (rowbase + (hl + 1) * W + wl + 1) * MD + base; w3 = lh * lw * a; }
+    }
+    t.off[0] = o0; t.off[1] = o1; t.off[2] = o2; t.off[3] = o3;
+    t.w[0] = w0; t.w[1] = w1; t.w[2] = w2; t.w[3] = w3;
+}
+
+// f64 keeps a double-precision setup so the fp64 path matches test_double_precision.py.
+struct Tap4d {
+    int off[4];
+    double w[4];
+};
+
+template <typename T, typename TL, int VEC, int FUSED>
+__global__ __launch_bounds__(kThreads) void msda_fwd_kernel(
+    const T* __restrict__ value, const int64_t* __restrict__ shapes,
+    const TL* __restrict__ loc, const TL* __restrict__ attw,
+    const float* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
+    const uint8_t* __restrict__ qmask, float* __restrict__ loc_out, float* __restrict__ attw_out,
+    T* __restrict__ out, int S, int M, int D, int L, int Lq, int P, int QT, int LPQ) {
+    using Acc = typename Acc<T>::type;
+    using TapT = typename std::conditional<sizeof(Acc) == 8, Tap4d, Tap4>::type;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    LevelInfo& li = *reinterpret_cast<LevelInfo*>(smem);
+    TapT* taps = reinterpret_cast<TapT*>(smem + sizeof(LevelInfo));
+
+    const int b = blockIdx.y;
+    const int q0 = blockIdx.x * QT;
+    const int LP = L * P;
+    const int MD = M * D;
+    load_levels(li, shapes, L, S);
+    __syncthreads();
+
+    // ---- phase 1: per-sample setup ----
+    const int nsamp = QT * M * LP;
+    if (!FUSED) {
+        for (int s = threadIdx.x; s < nsamp; s += kThreads) {
+            const int qi = s / (M * LP);
+            const int q = q0 + qi;
+            const int rem = s - qi * (M * LP);
+            const int m = rem / LP;
+            const int l = (rem - m * LP) / P;
+            TapT t;
+            if (q < Lq) {
+                const long gi = ((long)b * Lq + q0) * M * LP + s;   // (q, m, l, p) contiguous
+                if (sizeof(Acc) == 8) {
+                    // double path: identical arithmetic in f64
+                    const double x = (double)loc[2 * gi], y = (double)loc[2 * gi + 1], a = (double)attw[gi];
+                    const int H = li.H[l], W = li.W[l];
+                    const double h = y * H - 0.5, w = x * W - 0.5;
+                    const int base = m * D;
+                    for (int k = 0; k < 4; ++k) { t.off[k] = base; t.w[k] = 0; }
+                    if (li.ok[l] && h > -1 && w > -1 && h < H && w < W) {
+                        const double hf = floor(h), wf = floor(w);
+                        const int hl = (int)hf, wl = (int)wf;
+                        const double lh = h - hf, lw = w - wf, hh = 1 - lh, hw = 1 - lw;
+                        const int rb = li.start[l];
+                        const bool h0 = hl >= 0, h1 = hl + 1 <= H - 1, c0 = wl >= 0, c1 = wl + 1 <= W - 1;
+                        if (h0 && c0) { t.off[0] = (rb + hl * W + wl) * MD + base; t.w[0] = hh * hw * a; }
+                        if (h0 && c1) { t.off[1] = (rb + hl * W + wl + 1) * MD + base; t.w[1] = hh * lw * a; }
+                        if (h1 && c0) { t.off[2] = (rb + (hl + 1) * W + wl) * MD + base; t.w[2] = lh * hw * a; }
+                        if (h1 && c1) { t.off[3] = (rb + (hl + 1) * W + wl + 1) * MD + base; t.w[3] = lh * lw * a; }
+                    }
+                } else {
+                    Tap4 t4;
+                    setup_sample<T, TL>(t4, ldf(loc + 2 * gi), ldf(loc + 2 * gi + 1), ldf(attw + gi), li, l, MD, m, D);
+                    for (int k = 0; k < 4; ++k) { t.off[k] = t4.off[k]; t.w[k] = t4.w[k]; }
+                }
+            } else {
+                for (int k = 0; k < 4; ++k) { t.off[k] = 0; t.w[k] = 0; }
+            }
+            taps[s] = t;
+        }
+    } else {
+        // fused module path (ms_deform_attn.py:69-82): logits -> softmax over L*P, offsets
+        // -> locations.  Logits go through LDS (reusing the weight slots) for the softmax.
+        float* lg = reinterpret_cast<float*>(taps + nsamp);   // nsamp floats after the taps
+        for (int s = threadIdx.x; s < nsamp; s += kThreads) {
+            const int qi = s / (M * LP);
+            const int q = q0 + qi;
+            const int rem = s - qi * (M * LP);
+            float v = -INFINITY;
+            if (q < Lq) v = to_f32(offlog[((long)b * Lq + q) * ld_off + (long)M * LP * 2 + rem]);
+            lg[s] = v;
+        }
+        __syncthreads();
+        for (int s = threadIdx.x; s < nsamp; s += kThreads) {
+            const int qi = s / (M * LP);
+            const int q = q0 + qi;
+            const int rem = s - qi * (M * LP);
+            const int m = rem / LP;
+            const int lp = rem - m * LP;
+            const int l = lp / P;
+            Tap4 t4;
+            if (q < Lq) {
+                const float* grp = lg + (s - lp);
+                float mx = -INFINITY;
+                for (int j = 0; j < LP; ++j) mx = fmaxf(mx, grp[j]);
+                float sum = 0.f;
+                for (int j = 0; j < LP; ++j) sum += __expf(grp[j] - mx);
+                float a = __expf(grp[lp] - mx) / sum;
+                if (qmask && qmask[(long)b * Lq + q]) a = 0.f;
+                const float* orow = offlog + ((long)b * Lq + q) * ld_off + (long)rem * 2;
+                const float ox = to_f32(orow[0]), oy = to_f32(orow[1]);
+                const float* rp = ref + (((long)b * Lq + q) * L + l) * ref_dim;
+                float x, y;
+                if (ref_dim == 2) {
+                    // quirk kept for parity: offsets / spatial_shapes[(H, W)] applied to (x, y)
+                    x = rp[0] + ox / (float)li.H[l];
+                    y = rp[1] + oy / (float)li.W[l];
+                } else {
+                    x = rp[0] + ox / (float)P * rp[2] * 0.5f;
+                    y = rp[1] + oy / (float)P * rp[3] * 0.5f;
+                }
+                if (loc_out) {
+                    const long gi = ((long)b * Lq + q) * M * LP + rem;
+                    loc_out[2 * gi] = x;
+                    loc_out[2 * gi + 1] = y;
+                    attw_out[gi] = a;
+                }
+                setup_sample<T, float>(t4, x, y, a, li, l, MD, m, D);
+            } else {
+                for (int k = 0; k < 4; ++k) { t4.off[k] = 0; t4.w[k] = 0.f; }
+            }
+            TapT t;   // lg lives after the taps array: no overlap, no barrier needed
+            for (int k = 0; k < 4; ++k) { t.off[k] = t4.off[k]; t.w[k] = t4.w[k]; }
+            taps[s] = t;
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 2: gather ----
+    const int g = threadIdx.x / LPQ;
+    const int lane = threadIdx.x - g * LPQ;
+    const int qi = g / M;
+    const int q = q0 + qi;
+    if (qi >= QT || q >= Lq) return;
+    const int m = g - qi * M;
+    const int c0 = lane * VEC;
+    const T* vb = value + (long)b * S * MD + c0;
+    const TapT* tp = taps + (qi * M + m) * LP;
+    Acc acc[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0;
+#pragma unroll 4
+    for (int s = 0; s < LP; ++s) {
+        const TapT t = tp[s];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const VecT<T, VEC> v = *reinterpret_cast<const VecT<T, VEC>*>(vb + t.off[k]);
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) acc[j] += (Acc)t.w[k] * to_acc(v.v[j], (Acc*)nullptr);
+        }
+    }
+    VecT<T, VEC> o;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o.v[j] = Cvt<T>::from(acc[j]);
+    *reinterpret_cast<VecT<T, VEC>*>(out + ((long)b * Lq + q) * MD + (long)m * D + c0) = o;
+}
+
+// ---------------------------------------------------------------------------------
+// backward
+// ---------------------------------------------------------------------------------
+template <typename A>
+struct BwdTap {
+    int off[4];   // -1: tap outside the image (value taken as 0, no scatter)
+    A lh, lw, a;
+    int valid;    // sample inside (-1,H) x (-1,W)
+    A H, W;
+};
+
+template <typename T, typename TL, typename GA, int VEC, int POW2>
+__global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
+    const T* __restrict__ value, const int64_t* __restrict__ shapes,
+    const TL* __restrict__ loc, const TL* __restrict__ attw, const T* __restrict__ gout,
+    GA* __restrict__ gvalue, TL* __restrict__ gloc, TL* __restrict__ gattw,
+    int S, int M, int D, int L, int Lq, int P, int QT, int LPQ) {
+    using Acc = typename Acc<T>::type;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    LevelInfo& li = *reinterpret_cast<LevelInfo*>(smem);
+    BwdTap<Acc>* taps = reinterpret_cast<BwdTap<Acc>*>(smem + sizeof(LevelInfo));
+    const int b = blockIdx.y;
+    const int q0 = blockIdx.x * QT;
+    const int LP = L * P;
+    const int MD = M * D;
+    const int nsamp = QT * M * LP;
+    Acc* red = reinterpret_cast<Acc*>(taps + nsamp);   // [nsamp][3] when !POW2
+    load_levels(li, shapes, L, S);
+    __syncthreads();
+
+    for (int s = threadIdx.x; s < nsamp; s += kThreads) {
+        const int qi = s / (M * LP);
+        const int q = q0 + qi;
+        const int rem = s - qi * (M * LP);
+        const int m = rem / LP;
+        const int l = (rem - m * LP) / P;
+        BwdTap<Acc> t;
+        for (int k = 0; k < 4; ++k) t.off[k] = -1;
+        t.lh = t.lw = t.a = 0;
+        t.valid = 0;
+        t.H = (Acc)li.H[l];
+        t.W = (Acc)li.W[l];
+        if (q < Lq) {
+            const long gi = ((long)b * Lq + q0) * M * LP + s;
+            const Acc x = (Acc)loc[2 * gi], y = (Acc)loc[2 * gi + 1];
+            t.a = (Acc)attw[gi];
+            const int H = li.H[l], W = li.W[l];
+            const Acc h = y * (Acc)H - (Acc)0.5, w = x * (Acc)W - (Acc)0.5;   // cuh:352-353
+            if (li.ok[l] && h > -1 && w > -1 && h < (Acc)H && w < (Acc)W) {  // cuh:359
+                const Acc hf = floor(h), wf = floor(w);
+                const int hl = (int)hf, wl = (int)wf;
+                t.lh = h - hf;
+                t.lw = w - wf;
+                t.valid = 1;
+                const int rb = li.start[l];
+                const int base = m * D;
+                const bool h0 = hl >= 0, h1 = hl + 1 <= H - 1, c0 = wl >= 0, c1 = wl + 1 <= W - 1;
+                if (h0 && c0) t.off[0] = (rb + hl * W + wl) * MD + base;
+                if (h0 && c1) t.off[1] = (rb + hl * W + wl + 1) * MD + base;
+                if (h1 && c0) t.off[2] = (rb + (hl + 1) * W + wl) * MD + base;
+                if (h1 && c1) t.off[3] = (rb + (hl + 1) * W + wl + 1) * MD + base;
+            }
+        }
+        taps[s] = t;
+        if (!POW2) { red[3 * s] = 0; red[3 * s + 1] = 0; red[3 * s + 2] = 0; }
+    }
+    __syncthreads();
+
+    const int g = threadIdx.x / LPQ;
+    const int lane = threadIdx.x - g * LPQ;
+    const int qi = g / M;
+    const int q = q0 + qi;
+    const bool active = qi < QT && q < Lq;
+    if (active) {
+        const int m = g - qi * M;
+        const int c0 = lane * VEC;
+        const T* vb = value + (long)b * S * MD + c0;
+        GA* gvb = gvalue + (long)b * S * MD + c0;
+        const VecT<T, VEC> gv = *reinterpret_cast<const VecT<T, VEC>*>(gout + ((long)b * Lq + q) * MD + (long)m * D + c0);
+        Acc gc[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) gc[j] = to_acc(gv.v[j], (Acc*)nullptr);
+        const int sbase = (qi * M + m) * LP;
+        for (int s = 0; s < LP; ++s) {
+            const BwdTap<Acc> t = taps[sbase + s];
+            Acc pa = 0, px = 0, py = 0;
+            if (t.valid) {
+                const Acc lh = t.lh, lw = t.lw, hh = 1 - lh, hw = 1 - lw;
+                Acc v[4][VEC];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (t.off[k] >= 0) {
+                        const VecT<T, VEC> vv = *reinterpret_cast<const VecT<T, VEC>*>(vb + t.off[k]);
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) v[k][j] = to_acc(vv.v[j], (Acc*)nullptr);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) v[k][j] = 0;
+                    }
+                }
+                const Acc wt[4] = {hh * hw, hh * lw, lh * hw, lh * lw};
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) {
+                    const Acc val = wt[0] * v[0][j] + wt[1] * v[1][j] + wt[2] * v[2][j] + wt[3] * v[3][j];
+                    const Acc dw = hh * (v[1][j] - v[0][j]) + lh * (v[3][j] - v[2][j]);   // cuh:150-160
+                    const Acc dh = hw * (v[2][j] - v[0][j]) + lw * (v[3][j] - v[1][j]);   // cuh:139-149
+                    pa += gc[j] * val;
+                    px += gc[j] * dw;
+                    py += gc[j] * dh;
+                }
+                // grad_value scatter (cuh:285-304): 4 taps x VEC contiguous channels
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (t.off[k] >= 0) {
+                        const Acc wk = wt[k] * t.a;
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) atomicAdd(gvb + t.off[k] + j, (GA)(gc[j] * wk));
+                    }
+                }
+            }
+            if (POW2) {
+                for (int o = LPQ >> 1; o > 0; o >>= 1) {
+                    pa += __shfl_xor(pa, o);
+                    px += __shfl_xor(px, o);
+                    py += __shfl_xor(py, o);
+                }
+                if (lane == 0) {
+                    const long gi = ((long)b * Lq + q) * M * LP + (long)(sbase - qi * M * LP) + s;
+                    gattw[gi] = (TL)pa;
+                    gloc[2 * gi] = (TL)(px * t.a * t.W);        // cuh:373
+                    gloc[2 * gi + 1] = (TL)(py * t.a * t.H);    // cuh:374
+                }
+            } else {
+                atomicAdd(red + 3 * (sbase + s), pa);
+                atomicAdd(red + 3 * (sbase + s) + 1, px * t.a * t.W);
+                atomicAdd(red + 3 * (sbase + s) + 2, py * t.a * t.H);
+            }
+        }
+    }
+    if (!POW2) {
+        __syncthreads();
+        for (int s = threadIdx.x; s < nsamp; s += kThreads) {
+            const int qq = q0 + s / (M * LP);
+            if (qq < Lq) {
+                const long gi = ((long)b * Lq + q0) * M * LP + s;
+                gattw[gi] = (TL)red[3 * s];
+                gloc[2 * gi] = (TL)red[3 * s + 1];
+                gloc[2 * gi + 1] = (TL)red[3 * s + 2];
+            }
+        }
+    }
+}
+
+template <typename T>
+__global__ void f32_to_kernel(const float* __restrict__ src, T* __restrict__ dst, long n) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        dst[i] = Cvt<T>::from(src[i]);
+}
+
+// ---------------------------------------------------------------------------------
+// launch configuration
+// ---------------------------------------------------------------------------------
+struct Cfg {
+    int vec, lpq, qt;
+};
+
+Cfg pick_cfg(int D, int M, size_t esize) {
+    Cfg c{1, D, 1};
+    const int maxvec = (int)(16 / esize);
+    for (int v = maxvec; v >= 1; v >>= 1) {
+        if (D % v == 0) { c.vec = v; break; }
+    }
+    c.lpq = D / c.vec;
+    const int groups = kThreads / c.lpq;
+    c.qt = groups / M;
+    return c;
+}
+
+int common_checks(int N, int S, int M, int D, int L, int Lq, int P, int im2col_step) {
+    KINET_CHECK_ARG(N >= 0 && S >= 0 && M > 0 && D > 0 && L > 0 && Lq >= 0 && P > 0,
+                    "msda: invalid sizes N=%d S=%d M=%d D=%d L=%d Lq=%d P=%d", N, S, M, D, L, Lq, P);
+    KINET_CHECK_ARG(L <= kMaxLevels, "msda: num_levels %d > %d", L, kMaxLevels);
+    KINET_CHECK_ARG((long long)S * M * D < (1LL << 31), "msda: S*M*D too large for one image");
+    if (N > 0) {
+        const int step = im2col_step < N ? im2col_step : N;   // cu:46
+        KINET_CHECK_ARG(step > 0 && N % step == 0, "batch(%d) must divide im2col_step(%d)", N, step);   // cu:48
+    }
+    return KINET_OK;
+}
+
+template <typename T, typename TL, int FUSED>
+int launch_fwd(const void* value, const int64_t* shapes, const void* loc, const void* attw,
+               const void* offlog, int ld_off, const float* ref, int ref_dim, const uint8_t* qmask,
+               float* loc_out, float* attw_out, void* out, int N, int S, int M, int D, int L, int Lq,
+               int P, hipStream_t stream) {
+    const Cfg c = pick_cfg(D, M, sizeof(T));
+    KINET_CHECK_ARG(c.qt >= 1, "msda: heads*channels/vec (%d*%d) exceeds one workgroup", M, c.lpq);
+    if (N == 0 || Lq == 0) return KINET_OK;
+    using Acc = typename Acc<T>::type;
+    const size_t tap = sizeof(Acc) == 8 ? sizeof(Tap4d) : sizeof(Tap4);
+    const size_t nsamp = (size_t)c.qt * M * L * P;
+    size_t lds = sizeof(LevelInfo) + nsamp * tap + (FUSED ? nsamp * sizeof(float) : 0);
+    KINET_CHECK_ARG(lds <= 160 * 1024, "msda: LDS request %zu too large", lds);
+    dim3 grid((Lq + c.qt - 1) / c.qt, N);
+#define KF(VEC)                                                                                             \
+    hipLaunchKernelGGL((msda_fwd_kernel<T, TL, VEC, FUSED>), grid, dim3(kThreads), lds, stream,             \
+                       (const T*)value, shapes, (const TL*)loc, (const TL*)attw, (const float*)offlog, ld_off,  \
+                       ref, ref_dim, qmask, loc_out, attw_out, (T*)out, S, M, D, L, Lq, P, c.qt, c.lpq)
+    switch (c.vec) {
+        case 1: KF(1); break;
+        case 2: KF(2); break;
+        case 4: if (16 / sizeof(T) >= 4) { KF(4); } break;
+        case 8: if (16 / sizeof(T) >= 8) { KF(8); } break;
+    }
+#undef KF
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+template <typename T, typename TL>
+int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const void* attw,
+               const void* gout, void* gvalue, void* gloc, void* gattw, void* workspace, int N, int S,
+               int M, int D, int L, int Lq, int P, hipStream_t stream) {
+    using Acc = typename Acc<T>::type;
+    using GA = typename std::conditional<sizeof(Acc) == 8, double, float>::type;
+    const Cfg c = pick_cfg(D, M, sizeof(T));
+    KINET_CHECK_ARG(c.qt >= 1, "msda: heads*channels/vec (%d*%d) exceeds one workgroup", M, c.lpq);
+    const size_t nval = (size_t)N * S * M * D;
+    GA* acc_buf;
+    const bool direct = std::is_same<T, float>::value || std::is_same<T, double>::value;
+    if (direct) {
+        acc_buf = (GA*)gvalue;
+    } else {
+        KINET_CHECK_ARG(workspace != nullptr || nval == 0, "msda backward: bf16/f16 value needs an f32 workspace");
+        acc_buf = (GA*)workspace;
+    }
+    if (nval) KINET_CHECK_HIP(hipMemsetAsync(acc_buf, 0, nval * sizeof(GA), stream));
+    if (N > 0 && Lq > 0) {
+        const bool pow2 = (c.lpq & (c.lpq - 1)) == 0 && c.lpq <= 64;
+        const size_t nsamp = (size_t)c.qt * M * L * P;
+        const size_t lds = sizeof(LevelInfo) + nsamp * sizeof(BwdTap<Acc>) + (pow2 ? 0 : nsamp * 3 * sizeof(Acc));
+        KINET_CHECK_ARG(lds <= 160 * 1024, "msda backward: LDS request %zu too large", lds);
+        dim3 grid((Lq + c.qt - 1) / c.qt, N);
+#define KB(VEC, P2)                                                                                          \
+    hipLaunchKernelGGL((msda_bwd_kernel<T, TL, GA, VEC, P2>), grid, dim3(kThreads), lds, stream,            \
+                       (const T*)value, shapes, (const TL*)loc, (const TL*)attw, (const T*)gout, acc_buf,   \
+                       (TL*)gloc, (TL*)gattw, S, M, D, L, Lq, P, c.qt, c.lpq)
+#define KBV(VEC) if (pow2) { KB(VEC, 1); } else { KB(VEC, 0); }
+        switch (c.vec) {
+            case 1: KBV(1); break;
+            case 2: KBV(2); break;
+            case 4: if (16 / sizeof(T) >= 4) { KBV(4); } break;
+            case 8: if (16 / sizeof(T) >= 8) { KBV(8); } break;
+        }
+#undef KBV
+#undef KB
+        KINET_LAUNCH_CHECK();
+    } else if (N * Lq * M * L * P > 0) {
+        KINET_CHECK_HIP(hipMemsetAsync(gloc, 0, (size_t)N * Lq * M * L * P * 2 * sizeof(TL), stream));
+        KINET_CHECK_HIP(hipMemsetAsync(gattw, 0, (size_t)N * Lq * M * L * P * sizeof(TL), stream));
+    }
+    if (!direct && nval) {
+        const long n = (long)nval;
+        int blocks = (int)((n + 255) / 256);
+        if (blocks > kMaxGridStride) blocks = kMaxGridStride;
+        hipLaunchKernelGGL((f32_to_kernel<T>), dim3(blocks), dim3(256), 0, stream, (const float*)acc_buf, (T*)gvalue, n);
+        KINET_LAUNCH_CHECK();
+    }
+    return KINET_OK;
+}
+
+}  // namespace
+}  // namespace kinet
+
+using namespace kinet;
+
+extern "C" int kinet_msda_forward(const void* value, const int64_t* spatial_shapes, const void* sampling_loc,
+                                  const void* attn_weight, void* output, int batch, int spatial_size,
+                                  int num_heads, int channels, int num_levels, int num_query, int num_point,
+                                  int im2col_step, int value_dtype, int loc_dtype, kinet_stream_t stream) {
+    int rc = common_checks(batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, im2col_step);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+#define ARGS value, spatial_shapes, sampling_loc, attn_weight, nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, \
+             output, batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, s
+    if (value_dtype == KINET_F32 && loc_dtype == KINET_F32) return launch_fwd<float, float, 0>(ARGS);
+    if (value_dtype == KINET_F64 && loc_dtype == KINET_F64) return launch_fwd<double, double, 0>(ARGS);
+    if (value_dtype == KINET_BF16 && loc_dtype == KINET_F32) return launch_fwd<bf16_t, float, 0>(ARGS);
+    if (value_dtype == KINET_F16 && loc_dtype == KINET_F32) return launch_fwd<f16_t, float, 0>(ARGS);
+#undef ARGS
+    set_error("msda forward: unsupported dtype pair value=%d loc=%d", value_dtype, loc_dtype);
+    return KINET_ERR_ARG;
+}
+
+extern "C" int kinet_msda_fused_forward(const void* value, const int64_t* spatial_shapes, const void* offsets_logits,
+                                        int ld_off, const float* ref_points, int ref_dim,
+                                        const uint8_t* query_attn_mask, void* output, float* loc_out,
+                                        float* attw_out, int batch, int spatial_size, int num_heads, int channels,
+                                        int num_levels, int num_query, int num_point, int value_dtype,
+                                        kinet_stream_t stream) {
+    int rc = common_checks(batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, 1);
+    if (rc) return rc;
+    KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.", ref_dim);
+    KINET_CHECK_ARG(ld_off >= num_heads * num_levels * num_point * 3, "msda fused: ld_off %d too small", ld_off);
+    KINET_CHECK_ARG((loc_out == nullptr) == (attw_out == nullptr), "msda fused: loc_out/attw_out must both be set or both NULL");
+    hipStream_t s = (hipStream_t)stream;
+#define ARGS value, spatial_shapes, nullptr, nullptr, offsets_logits, ld_off, ref_points, ref_dim, query_attn_mask, \
+             loc_out, attw_out, output, batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, s
+    if (value_dtype == KINET_F32) return launch_fwd<float, float, 1>(ARGS);
+    if (value_dtype == KINET_BF16) return launch_fwd<bf16_t, float, 1>(ARGS);
+    if (value_dtype == KINET_F16) return launch_fwd<f16_t, float, 1>(ARGS);
+#undef ARGS
+    set_error("msda fused forward: unsupported value dtype %d", value_dtype);
+    return KINET_ERR_ARG;
+}
+
+extern "C" int kinet_msda_backward(const void* value, const int64_t* spatial_shapes, const void* sampling_loc,
+                                   const void* attn_weight, const void* grad_output, void* grad_value,
+                                   void* grad_loc, void* grad_attw, void* workspace, int batch, int spatial_size,
+                                   int num_heads, int channels, int num_levels, int num_query, int num_point,
+                                   int im2col_step, int value_dtype, int loc_dtype, kinet_stream_t stream) {
+    int rc = common_checks(batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, im2col_step);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+#define ARGS value, spatial_shapes, sampling_loc, attn_weight, grad_output, grad_value, grad_loc, grad_attw, workspace, \
+             batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, s
+    if (value_dtype == KINET_F32 && loc_dtype == KINET_F32) return launch_bwd<float, float>(ARGS);
+    if (value_dtype == KINET_F64 && loc_dtype == KINET_F64) return launch_bwd<double, double>(ARGS);
+    if (value_dtype == KINET_BF16 && loc_dtype == KINET_F32) return launch_bwd<bf16_t, float>(ARGS);
+    if (value_dtype == KINET_F16 && loc_dtype == KINET_F32) return launch_bwd<f16_t, float>(ARGS);
+#undef ARGS
+    set_error("msda backward: unsupported dtype pair value=%d loc=%d", value_dtype, loc_dtype);
+    return KINET_ERR_ARG;
+}
+
+extern "C" int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num_heads, int channels,
+                                                       int value_dtype) {
+    if (value_dtype == KINET_F32 || value_dtype == KINET_F64) return 0;
+    return (int64_t)batch * spatial_size * num_heads * channels * 4;
+}

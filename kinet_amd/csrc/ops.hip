@@ -1,0 +1,393 @@
+// Normalisation, pooling, packing and small-attention kernels on the detection path
+// (include/kinet_ops.h).  All memory-bound: vectorised 8/16-byte accesses, f32 math.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include "../../include/kinet_ops.h"
+#include "common.h"
+
+namespace kinet {
+namespace {
+
+template <typename T> __device__ __forceinline__ void st(T* p, float v) { *p = Cvt<T>::from(v); }
+__device__ __forceinline__ void st(double* p, float v) { *p = v; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// ---------------------------------------------------------------------------------
+// LayerNorm: one wave per row, up to 16 elements per lane kept in registers (d <= 1024)
+// ---------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm_kernel(const T* __restrict__ x, const T* __restrict__ r,
+                                                        const float* __restrict__ g, const float* __restrict__ b,
+                                                        T* __restrict__ y, int rows, int d, float eps) {
+    constexpr int MAXE = 16;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wave >= rows) return;
+    const T* xr = x + (long)wave * d;
+    const T* rr = r ? r + (long)wave * d : nullptr;
+    float v[MAXE];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXE; ++j) {
+        const int c = lane + 64 * j;
+        float t = 0.f;
+        if (c < d) {
+            t = to_f32(xr[c]);
+            if (rr) t += to_f32(rr[c]);
+        }
+        v[j] = t;
+        s += t;
+    }
+    const float mean = wave_sum(s) / (float)d;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXE; ++j) {
+        const int c = lane + 64 * j;
+        if (c < d) {
+            const float t = v[j] - mean;
+            q += t * t;
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)d + eps);
+    T* yr = y + (long)wave * d;
+#pragma unroll
+    for (int j = 0; j < MAXE; ++j) {
+        const int c = lane + 64 * j;
+        if (c < d) st(yr + c, (v[j] - mean) * rstd * g[c] + b[c]);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// GroupNorm on NHWC: stats (sum, sumsq per image x group) then apply
+// ---------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x, float* __restrict__ stats, int HW,
+                                                       int C, int groups, int pix_per_block) {
+    // thread t sums channels t, t+256, ... over this block's pixel range (coalesced rows)
+    extern __shared__ float red[];   // [groups][2]
+    const int n = blockIdx.y;
+    const int p0 = blockIdx.x * pix_per_block;
+    const int p1 = min(HW, p0 + pix_per_block);
+    for (int i = threadIdx.x; i < 2 * groups; i += blockDim.x) red[i] = 0.f;
+    __syncthreads();
+    const int cpg = C / groups;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.f, q = 0.f;
+        for (int p = p0; p < p1; ++p) {
+            const float t = to_f32(x[((long)n * HW + p) * C + c]);
+            s += t;
+            q += t * t;
+        }
+        atomicAdd(&red[2 * (c / cpg)], s);
+        atomicAdd(&red[2 * (c / cpg) + 1], q);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * groups; i += blockDim.x) atomicAdd(&stats[(long)n * 2 * groups + i], red[i]);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, const float* __restrict__ stats,
+                                                       const float* __restrict__ g, const float* __restrict__ b,
+                                                       T* __restrict__ y, int N, int HW, int C, int groups,
+                                                       long y_bs, float eps) {
+    const long total = (long)N * HW * C;
+    const int cpg = C / groups;
+    const float cnt = (float)HW * cpg;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        const long np = i / C;
+        const int n = (int)(np / HW);
+        const long p = np - (long)n * HW;
+        const int grp = c / cpg;
+        const float mean = stats[(long)n * 2 * groups + 2 * grp] / cnt;
+        const float var = fmaxf(stats[(long)n * 2 * groups + 2 * grp + 1] / cnt - mean * mean, 0.f);
+        const float v = (to_f32(x[i]) - mean) * rsqrtf(var + eps) * g[c] + b[c];
+        st(y + (long)n * y_bs + p * C + c, v);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// max-pool 3x3 stride 2 pad 1 (NHWC)
+// ---------------------------------------------------------------------------------
+template <typename T>
+__global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int Ho, int Wo) {
+    const long total = (long)N * Ho * Wo * C;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        long r = i / C;
+        const int ow = (int)(r % Wo);
+        r /= Wo;
+        const int oh = (int)(r % Ho);
+        const int n = (int)(r / Ho);
+        float m = -INFINITY;
+        for (int dy = 0; dy < 3; ++dy) {
+            const int ih = oh * 2 - 1 + dy;
+            if (ih < 0 || ih >= H) continue;
+            for (int dx = 0; dx < 3; ++dx) {
+                const int iw = ow * 2 - 1 + dx;
+                if (iw < 0 || iw >= W) continue;
+                m = fmaxf(m, to_f32(x[(((long)n * H + ih) * W + iw) * C + c]));
+            }
+        }
+        st(y + i, m);
+    }
+}
+
+template <typename T>
+__global__ void pack_image_kernel(const float* __restrict__ x, T* __restrict__ y, int N, int H, int W, int Cp) {
+    const long total = (long)N * H * W * Cp;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % Cp);
+        const long pix = i / Cp;
+        const int n = (int)(pix / ((long)H * W));
+        const long hw = pix - (long)n * H * W;
+        float v = 0.f;
+        if (c < 3) v = x[((long)n * 3 + c) * H * W + hw];
+        st(y + i, v);
+    }
+}
+
+template <typename T>
+__global__ void add_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ y, long n) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        st(y + i, to_f32(a[i]) + to_f32(b[i]));
+}
+
+// ---------------------------------------------------------------------------------
+// MHA core: online softmax.  Block = 256 threads = 4 waves splitting the keys; each
+// lane owns one query row; keys/values streamed through LDS in tiles of 64.
+// ---------------------------------------------------------------------------------
+template <typename T, int D>
+__global__ __launch_bounds__(256) void mha_kernel(const T* __restrict__ Q, int ldq, const T* __restrict__ Kt, int ldk,
+                                                  const T* __restrict__ V, int ldv, T* __restrict__ O, int ldo,
+                                                  int Lq, int Lk, int heads, float scale,
+                                                  const uint8_t* __restrict__ kmask) {
+    constexpr int KT = 64;
+    __shared__ float ks[KT][D + 1];
+    __shared__ float vs[KT][D + 1];
+    __shared__ float part_m[4][64], part_l[4][64];
+    __shared__ float part_o[4][64][D + 1];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int qi = blockIdx.x * 64 + lane;
+    float q[D], o[D];
+    const bool qok = qi < Lq;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        q[j] = qok ? to_f32(Q[((long)b * Lq + qi) * ldq + h * D + j]) * scale : 0.f;
+        o[j] = 0.f;
+    }
+    float mx = -INFINITY, l = 0.f;
+    for (int k0 = 0; k0 < Lk; k0 += KT) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < KT * D; i += 256) {
+            const int kk = i / D, j = i - (i / D) * D;
+            const int kr = k0 + kk;
+            float kv = 0.f, vv = 0.f;
+            if (kr < Lk) {
+                kv = to_f32(Kt[((long)b * Lk + kr) * ldk + h * D + j]);
+                vv = to_f32(V[((long)b * Lk + kr) * ldv + h * D + j]);
+            }
+            ks[kk][j] = kv;
+            vs[kk][j] = vv;
+        }
+        __syncthreads();
+        // wave w handles keys kk = w, w+4, ...
+        for (int kk = wave; kk < KT; kk += 4) {
+            const int kr = k0 + kk;
+            if (kr >= Lk) break;
+            if (kmask && kmask[(long)b * Lk + kr]) continue;
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < D; ++j) s += q[j] * ks[kk][j];
+            const float nm = fmaxf(mx, s);
+            const float corr = __expf(mx - nm);
+            const float pexp = __expf(s - nm);
+            l = l * corr + pexp;
+#pragma unroll
+            for (int j = 0; j < D; ++j) o[j] = o[j] * corr + pexp * vs[kk][j];
+            mx = nm;
+        }
+    }
+    // merge the 4 waves' partial softmax states
+    part_m[wave][lane] = mx;
+    part_l[wave][lane] = l;
+#pragma unroll
+    for (int j = 0; j < D; ++j) part_o[wave][lane][j] = o[j];
+    __syncthreads();
+    if (wave == 0 && qok) {
+        float M_ = -INFINITY;
+        for (int w = 0; w < 4; ++w) M_ = fmaxf(M_, part_m[w][lane]);
+        float L_ = 0.f;
+        float acc[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) acc[j] = 0.f;
+        for (int w = 0; w < 4; ++w) {
+            const float pm = part_m[w][lane];
+            const float f = pm == -INFINITY ? 0.f : __expf(pm - M_);
+            L_ += part_l[w][lane] * f;
+#pragma unroll
+            for (int j = 0; j < D; ++j) acc[j] += part_o[w][lane][j] * f;
+        }
+        const float inv = L_ > 0.f ? 1.f / L_ : 0.f;
+#pragma unroll
+        for (int j = 0; j < D; ++j) st(O + ((long)b * Lq + qi) * ldo + h * D + j, acc[j] * inv);
+    }
+}
+
+__device__ __forceinline__ float inv_sigmoid(float x) {
+    // util/misc.py:609-613 (eps 1e-5)
+    x = fminf(fmaxf(x, 0.f), 1.f);
+    const float x1 = fmaxf(x, 1e-5f), x2 = fmaxf(1.f - x, 1e-5f);
+    return logf(x1 / x2);
+}
+
+__global__ void box_refine_kernel(const float* __restrict__ tmp, const float* __restrict__ ref, int rd,
+                                  const float* __restrict__ vr, float* __restrict__ nref, float* __restrict__ rin,
+                                  int N, int Q, int L) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N * Q) return;
+    const int b = i / Q;
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float t = tmp[(long)i * 4 + j];
+        if (j < rd) t += inv_sigmoid(ref[(long)i * rd + j]);
+        o[j] = 1.f / (1.f + __expf(-t));
+        nref[(long)i * 4 + j] = o[j];
+    }
+    if (rin) {
+        for (int l = 0; l < L; ++l) {
+            const float vx = vr[((long)b * L + l) * 2], vy = vr[((long)b * L + l) * 2 + 1];
+            float* p = rin + ((long)i * L + l) * 4;
+            p[0] = o[0] * vx;
+            p[1] = o[1] * vy;
+            p[2] = o[2] * vx;
+            p[3] = o[3] * vy;
+        }
+    }
+}
+
+int grid_for(long n, int block = 256) {
+    long g = (n + block - 1) / block;
+    if (g > 8 * kMaxGridStride) g = 8 * kMaxGridStride;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+}  // namespace kinet
+
+using namespace kinet;
+
+#define DISPATCH_T(dtype, F)                                                 \
+    switch (dtype) {                                                         \
+        case KINET_F32: { typedef float T; F; break; }                       \
+        case KINET_BF16: { typedef bf16_t T; F; break; }                     \
+        case KINET_F16: { typedef f16_t T; F; break; }                       \
+        default: set_error("unsupported dtype %d", dtype); return KINET_ERR_ARG; \
+    }
+
+extern "C" int kinet_layernorm(const void* x, const void* r, const float* gamma, const float* beta, void* y, int rows,
+                               int d, float eps, int dtype, int reserved, kinet_stream_t stream) {
+    (void)reserved;
+    KINET_CHECK_ARG(rows >= 0 && d > 0 && d <= 1024, "layernorm: d must be in [1, 1024] (got %d)", d);
+    if (rows == 0) return KINET_OK;
+    const int blocks = (rows + 3) / 4;
+    DISPATCH_T(dtype, hipLaunchKernelGGL((layernorm_kernel<T>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)x, (const T*)r, gamma, beta, (T*)y, rows, d, eps));
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_groupnorm(const void* x, const float* gamma, const float* beta, void* y, int N, int HW, int C,
+                               int groups, int y_batch_stride, float eps, int dtype, float* stats,
+                               kinet_stream_t stream) {
+    KINET_CHECK_ARG(N >= 0 && HW > 0 && C > 0 && groups > 0 && C % groups == 0, "groupnorm: bad geometry");
+    KINET_CHECK_ARG(y_batch_stride >= HW * C, "groupnorm: y_batch_stride < HW*C");
+    KINET_CHECK_ARG(stats != nullptr, "groupnorm: stats workspace (2*N*groups floats) required");
+    if (N == 0) return KINET_OK;
+    hipStream_t s = (hipStream_t)stream;
+    KINET_CHECK_HIP(hipMemsetAsync(stats, 0, (size_t)2 * N * groups * sizeof(float), s));
+    const int ppb = 64;
+    dim3 g1((HW + ppb - 1) / ppb, N);
+    DISPATCH_T(dtype, hipLaunchKernelGGL((gn_stats_kernel<T>), g1, dim3(256), 2 * groups * sizeof(float), s,
+                                         (const T*)x, stats, HW, C, groups, ppb));
+    KINET_LAUNCH_CHECK();
+    const long total = (long)N * HW * C;
+    DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T>), dim3(grid_for(total)), dim3(256), 0, s, (const T*)x,
+                                         stats, gamma, beta, (T*)y, N, HW, C, groups, (long)y_batch_stride, eps));
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_maxpool2d_3x3s2(const void* x, void* y, int N, int H, int W, int C, int dtype,
+                                     kinet_stream_t stream) {
+    KINET_CHECK_ARG(N >= 0 && H > 0 && W > 0 && C > 0, "maxpool: bad geometry");
+    const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+    const long total = (long)N * Ho * Wo * C;
+    if (total == 0) return KINET_OK;
+    DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool_kernel<T>), dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)x, (T*)y, N, H, W, C, Ho, Wo));
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_pack_image_nhwc(const float* x, void* y, int N, int H, int W, int Cpad, int dtype,
+                                     kinet_stream_t stream) {
+    KINET_CHECK_ARG(N >= 0 && H > 0 && W > 0 && Cpad >= 3, "pack_image: bad geometry");
+    const long total = (long)N * H * W * Cpad;
+    if (total == 0) return KINET_OK;
+    DISPATCH_T(dtype, hipLaunchKernelGGL((pack_image_kernel<T>), dim3(grid_for(total)), dim3(256), 0,
+                                         (hipStream_t)stream, x, (T*)y, N, H, W, Cpad));
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_add(const void* a, const void* b, void* y, int64_t n, int dtype, kinet_stream_t stream) {
+    KINET_CHECK_ARG(n >= 0, "add: n < 0");
+    if (n == 0) return KINET_OK;
+    DISPATCH_T(dtype, hipLaunchKernelGGL((add_kernel<T>), dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)a, (const T*)b, (T*)y, (long)n));
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_mha_core(const void* Q, int ldq, const void* Kt, int ldk, const void* V, int ldv, void* O, int ldo,
+                              int batch, int Lq, int Lk, int heads, int head_dim, float scale, int dtype,
+                              const uint8_t* key_mask, kinet_stream_t stream) {
+    KINET_CHECK_ARG(batch >= 0 && Lq >= 0 && Lk >= 0 && heads > 0, "mha: bad sizes");
+    KINET_CHECK_ARG(head_dim == 32 || head_dim == 36 || head_dim == 16 || head_dim == 64,
+                    "mha: head_dim %d not instantiated (16/32/36/64)", head_dim);
+    if (batch == 0 || Lq == 0) return KINET_OK;
+    dim3 grid((Lq + 63) / 64, heads, batch);
+    hipStream_t s = (hipStream_t)stream;
+#define MH(DD) DISPATCH_T(dtype, hipLaunchKernelGGL((mha_kernel<T, DD>), grid, dim3(256), 0, s, (const T*)Q, ldq, \
+                                                   (const T*)Kt, ldk, (const T*)V, ldv, (T*)O, ldo, Lq, Lk, heads, \
+                                                   scale, key_mask))
+    switch (head_dim) {
+        case 16: MH(16); break;
+        case 32: MH(32); break;
+        case 36: MH(36); break;
+        case 64: MH(64); break;
+    }
+#undef MH
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_box_refine(const float* tmp, const float* ref, int ref_dim, const float* valid_ratios,
+                                float* new_ref, float* ref_input, int N, int Q, int L, kinet_stream_t stream) {
+    KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "box_refine: ref_dim must be 2 or 4");
+    if (N * Q == 0) return KINET_OK;
+    hipLaunchKernelGGL(box_refine_kernel, dim3((N * Q + 255) / 256), dim3(256), 0, (hipStream_t)stream, tmp, ref,
+                       ref_dim, valid_ratios, new_ref, ref_input, N, Q, L);
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}

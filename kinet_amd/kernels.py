@@ -1,0 +1,239 @@
+"""Thin torch-tensor front-end over the kinet_amd C-ABI (include/*.h).
+
+Every function launches hand-written HIP kernels from libkinet_amd.so on the current
+stream; nothing here falls back to a torch/CPU implementation.  Weights stay torch
+Parameters (reference layout, so state_dicts load unchanged); converted copies (dtype
+casts, OIHW->OHWI conv packing, folded FrozenBatchNorm) are cached per parameter
+version.
+"""
+import weakref
+
+import torch
+
+from kinet_amd import _native as N
+
+_cache = {}   # id(tensor) -> (weakref(tensor), {tag: ((version, data_ptr), value)})
+
+
+def _drop(key):
+    def cb(_ref):
+        _cache.pop(key, None)
+    return cb
+
+
+def cached(t, tag, make):
+    """Cache make(t) per tensor object (identity-keyed and weakly held, so a freed
+    temporary never aliases a new tensor at the same address), invalidated by in-place
+    updates (_version)."""
+    if t is None:
+        return None
+    key = id(t)
+    ent = _cache.get(key)
+    if ent is None or ent[0]() is not t:
+        ent = (weakref.ref(t, _drop(key)), {})
+        _cache[key] = ent
+    slot = ent[1]
+    hit = slot.get(tag)
+    ver = (t._version, t.data_ptr())
+    if hit is not None and hit[0] == ver:
+        return hit[1]
+    v = make(t)
+    slot[tag] = (ver, v)
+    return v
+
+
+def clear_cache():
+    _cache.clear()
+
+
+def weight_as(w, dtype):
+    return cached(w, ('w', dtype), lambda t: t.detach().to(dtype).contiguous())
+
+
+def f32(t):
+    return None if t is None else cached(t, 'f32', lambda x: x.detach().float().contiguous())
+
+
+# ----------------------------------------------------------------------------------- GEMM
+def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_dtype=None,
+           scale=None, out=None):
+    """y = relu?(x @ W^T * scale + bias + residual); rows with row_mask -> 0.
+    x (..., K) in bf16/f16/f32; weight (Nout, K) any float dtype (cast+cached)."""
+    N.require_gpu(x)
+    K = x.shape[-1]
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, K)
+    if x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    M = x2.shape[0]
+    w = weight_as(weight, x.dtype)
+    Nout = w.shape[0]
+    odt = out_dtype or x.dtype
+    if out is None:
+        out = torch.empty((M, Nout), dtype=odt, device=x.device)
+        ldc = Nout
+    else:
+        ldc = out.stride(0)
+    r = None
+    ldr = 0
+    if residual is not None:
+        r = residual.reshape(-1, Nout)
+        if r.stride(-1) != 1:
+            r = r.contiguous()
+        if r.dtype != odt:
+            r = r.to(odt)
+        ldr = r.stride(0)
+    mask = None
+    if row_mask is not None:
+        mask = row_mask.reshape(-1).to(torch.uint8).contiguous()
+    N.call('kinet_gemm', N.ptr(x2), N.ptr(w), N.ptr(out), M, Nout, K, x2.stride(0), K, ldc,
+           N.dtype_code(x.dtype), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(r), ldr, int(relu),
+           N.dtype_code(odt), N.ptr(mask), 0, N.stream(x.device))
+    return out.view(*lead, Nout) if out.is_contiguous() else out
+
+
+# ----------------------------------------------------------------------------------- conv
+def pack_conv_weight(w, dtype, cin_pad=None):
+    """OIHW -> OHWI (Cin fastest), optional zero channel padding, cast."""
+    def make(t):
+        o, i, kh, kw = t.shape
+        p = t.detach().permute(0, 2, 3, 1)
+        if cin_pad and cin_pad > i:
+            p = torch.nn.functional.pad(p, (0, cin_pad - i))
+        return p.to(dtype).contiguous()
+    return cached(w, ('conv', dtype, cin_pad), make)
+
+
+def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, residual=None, out=None):
+    """x (B, H, W, Cin) NHWC contiguous; w_packed (Cout, KH, KW, Cin); returns (B, Ho, Wo, Cout)."""
+    B, H, W, Cin = x.shape
+    Cout, KH, KW, Cin2 = w_packed.shape
+    if Cin2 != Cin:
+        raise RuntimeError(f'conv2d: weight Cin {Cin2} != input Cin {Cin}')
+    Ho = (H + 2 * pad - KH) // stride + 1
+    Wo = (W + 2 * pad - KW) // stride + 1
+    if out is None:
+        out = torch.empty((B, Ho, Wo, Cout), dtype=x.dtype, device=x.device)
+    ldy = out.stride(2) if out.dim() == 4 else out.stride(-2)
+    r = None
+    if residual is not None:
+        r = residual
+    N.call('kinet_conv2d', N.ptr(x), N.ptr(w_packed), N.ptr(out), B, H, W, Cin, Ho, Wo, Cout, KH, KW,
+           stride, pad, N.dtype_code(x.dtype), N.ptr(scale), N.ptr(bias), N.ptr(r),
+           Cout if r is not None else 0, int(relu), ldy, N.stream(x.device))
+    return out
+
+
+def maxpool_3x3s2(x):
+    B, H, W, C = x.shape
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
+    N.call('kinet_maxpool2d_3x3s2', N.ptr(x), N.ptr(y), B, H, W, C, N.dtype_code(x.dtype), N.stream(x.device))
+    return y
+
+
+def pack_image(img, dtype, cpad=8):
+    """(B, 3, H, W) f32 NCHW -> (B, H, W, cpad) NHWC dtype."""
+    img = img.float().contiguous()
+    B, C, H, W = img.shape
+    if C != 3:
+        raise RuntimeError('pack_image expects 3-channel images')
+    y = torch.empty((B, H, W, cpad), dtype=dtype, device=img.device)
+    N.call('kinet_pack_image_nhwc', N.ptr(img), N.ptr(y), B, H, W, cpad, N.dtype_code(dtype), N.stream(img.device))
+    return y
+
+
+# ------------------------------------------------------------------------------ norms
+def layernorm(x, weight, bias, eps=1e-5, residual=None, out=None):
+    d = x.shape[-1]
+    x2 = x.contiguous()
+    r = residual.contiguous() if residual is not None else None
+    y = out if out is not None else torch.empty_like(x2)
+    rows = x2.numel() // d
+    N.call('kinet_layernorm', N.ptr(x2), N.ptr(r), N.ptr(f32(weight)), N.ptr(f32(bias)), N.ptr(y), rows, d,
+           float(eps), N.dtype_code(x.dtype), 0, N.stream(x.device))
+    return y
+
+
+def groupnorm_nhwc(x, weight, bias, groups, eps=1e-5, out=None, out_batch_stride=None):
+    """x (B, HW, C) contiguous -> out rows at out + b*out_batch_stride (default packed)."""
+    B, HW, C = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+        out_batch_stride = HW * C
+    stats = torch.empty(2 * B * groups, dtype=torch.float32, device=x.device)
+    N.call('kinet_groupnorm', N.ptr(x), N.ptr(f32(weight)), N.ptr(f32(bias)), N.ptr(out), B, HW, C, groups,
+           int(out_batch_stride), float(eps), N.dtype_code(x.dtype), N.ptr(stats), N.stream(x.device))
+    return out
+
+
+def add(a, b, out=None):
+    a = a.contiguous()
+    b = b.contiguous()
+    y = out if out is not None else torch.empty_like(a)
+    N.call('kinet_add', N.ptr(a), N.ptr(b), N.ptr(y), a.numel(), N.dtype_code(a.dtype), N.stream(a.device))
+    return y
+
+
+# --------------------------------------------------------------------------- attention
+def mha_core(q, k, v, heads, scale, key_mask=None, out=None):
+    """q (B, Lq, E) (row stride may exceed E), k/v (B, Lk, E) -> (B, Lq, E)."""
+    B, Lq, E = q.shape
+    Lk = k.shape[1]
+    D = E // heads
+    for t in (q, k, v):
+        if t.stride(-1) != 1 or t.stride(0) != t.shape[1] * t.stride(1):
+            raise RuntimeError('mha_core: rows must be unit-stride with packed batches')
+    o = out if out is not None else torch.empty((B, Lq, E), dtype=q.dtype, device=q.device)
+    km = key_mask.to(torch.uint8).contiguous() if key_mask is not None else None
+    N.call('kinet_mha_core', N.ptr(q), q.stride(1), N.ptr(k), k.stride(1), N.ptr(v), v.stride(1), N.ptr(o),
+           o.stride(1), B, Lq, Lk, heads, D, float(scale), N.dtype_code(q.dtype), N.ptr(km), N.stream(q.device))
+    return o
+
+
+def box_refine(tmp, ref, valid_ratios=None, want_input=True):
+    """tmp (B, Q, 4) f32, ref (B, Q, 2|4) f32 -> new_ref (B, Q, 4) [, ref_input (B, Q, L, 4)]."""
+    B, Q, _ = tmp.shape
+    tmp = tmp.float().contiguous()
+    ref = ref.float().contiguous()
+    nref = torch.empty((B, Q, 4), dtype=torch.float32, device=tmp.device)
+    rin = None
+    L = 0
+    if want_input:
+        vr = valid_ratios.float().contiguous()
+        L = vr.shape[1]
+        rin = torch.empty((B, Q, L, 4), dtype=torch.float32, device=tmp.device)
+    else:
+        vr = None
+    N.call('kinet_box_refine', N.ptr(tmp), N.ptr(ref), ref.shape[-1], N.ptr(vr), N.ptr(nref), N.ptr(rin), B, Q, L,
+           N.stream(tmp.device))
+    return nref, rin
+
+
+# ------------------------------------------------------------------------------ MSDA
+def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_levels, n_points,
+               query_attn_mask=None, want_loc_attw=False):
+    """value (B, S, d) projected; offlog (B, Lq, M*L*P*3) f32 [offsets | logits];
+    reference_points (B, Lq, L, 2|4) f32.  Returns (B, Lq, d) [, loc, attw]."""
+    B, S, d = value.shape
+    Lq = offlog.shape[1]
+    D = d // n_heads
+    value = value.contiguous()
+    offlog = offlog.contiguous()
+    ref = reference_points.float().contiguous()
+    if ref.shape[2] != n_levels:
+        raise RuntimeError(f'reference_points has {ref.shape[2]} levels, module expects {n_levels}')
+    out = torch.empty((B, Lq, d), dtype=value.dtype, device=value.device)
+    loc = attw = None
+    if want_loc_attw:
+        loc = torch.empty((B, Lq, n_heads, n_levels, n_points, 2), dtype=torch.float32, device=value.device)
+        attw = torch.empty((B, Lq, n_heads, n_levels, n_points), dtype=torch.float32, device=value.device)
+    qm = query_attn_mask.to(torch.uint8).contiguous() if query_attn_mask is not None else None
+    if offlog.dtype != torch.float32:
+        raise RuntimeError('msda_fused: the offsets/logits projection must be f32')
+    N.call('kinet_msda_fused_forward', N.ptr(value), N.ptr(spatial_shapes), N.ptr(offlog), offlog.shape[-1],
+           N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), N.ptr(loc), N.ptr(attw), B, S, n_heads, D,
+           n_levels, Lq, n_points, N.dtype_code(value.dtype), N.stream(value.device))
+    if want_loc_attw:
+        return out, loc, attw
+    return out

@@ -1,0 +1,141 @@
+"""Operator + module surface of multi-scale deformable attention, mirroring
+src/trackformer/models/ops/functions/ms_deform_attn_func.py and
+src/trackformer/models/ops/modules/ms_deform_attn.py.
+
+`MSDeformAttnFunction.apply(value, value_spatial_shapes, sampling_locations,
+attention_weights, im2col_step)` is the reference operator boundary
+(ms_deform_attn_func.py:14-31); `MSDeformAttn` keeps the reference parameter names
+(sampling_offsets / attention_weights / value_proj / output_proj, ms_deform_attn.py:27-30)
+so reference state_dicts load unchanged.
+"""
+import math
+import warnings
+
+import torch
+from torch import nn
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+from torch.nn.init import constant_, xavier_uniform_
+
+from kinet_amd import MultiScaleDeformableAttention as MSDA
+from kinet_amd import kernels as K
+
+
+class MSDeformAttnFunction(Function):
+    """ms_deform_attn_func.py:14-31 -- same forward/backward contract."""
+
+    @staticmethod
+    def forward(ctx, value, value_spatial_shapes, sampling_locations, attention_weights, im2col_step):
+        ctx.im2col_step = im2col_step
+        output = MSDA.ms_deform_attn_forward(value, value_spatial_shapes, sampling_locations,
+                                             attention_weights, ctx.im2col_step)
+        ctx.save_for_backward(value, value_spatial_shapes, sampling_locations, attention_weights)
+        return output
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_output):
+        value, value_spatial_shapes, sampling_locations, attention_weights = ctx.saved_tensors
+        grad_value, grad_sampling_loc, grad_attn_weight = MSDA.ms_deform_attn_backward(
+            value, value_spatial_shapes, sampling_locations, attention_weights, grad_output, ctx.im2col_step)
+        return grad_value, None, grad_sampling_loc, grad_attn_weight, None
+
+
+class MSDeformAttn(nn.Module):
+    """ms_deform_attn.py:15-89.  Inference runs the fused HIP path (one GEMM for
+    value_proj with the padding mask in its epilogue, one GEMM for the concatenated
+    sampling_offsets | attention_weights projection, the fused softmax/location/sampling
+    kernel, and output_proj); with autograd enabled it runs the unfused reference
+    sequence through MSDeformAttnFunction so gradients flow exactly as upstream."""
+
+    def __init__(self, d_model=256, n_levels=4, n_heads=8, n_points=4, im2col_step=64):
+        super().__init__()
+        if d_model % n_heads != 0:
+            raise ValueError('d_model must be divisible by n_heads, but got {} and {}'.format(d_model, n_heads))
+        _d_per_head = d_model // n_heads
+        if not ((_d_per_head & (_d_per_head - 1) == 0) and _d_per_head != 0):
+            warnings.warn("You'd better set d_model in MSDeformAttn to make the dimension of each attention "
+                          "head a power of 2 which is more efficient in our CUDA implementation.")
+        self.im2col_step = im2col_step
+        self.d_model = d_model
+        self.n_levels = n_levels
+        self.n_heads = n_heads
+        self.n_points = n_points
+        self.sampling_offsets = nn.Linear(d_model, n_heads * n_levels * n_points * 2)
+        self.attention_weights = nn.Linear(d_model, n_heads * n_levels * n_points)
+        self.value_proj = nn.Linear(d_model, d_model)
+        self.output_proj = nn.Linear(d_model, d_model)
+        self._reset_parameters()
+        self._packed = None
+
+    def _reset_parameters(self):
+        # ms_deform_attn.py:34-47
+        constant_(self.sampling_offsets.weight.data, 0.)
+        thetas = torch.arange(self.n_heads, dtype=torch.float32) * (2.0 * math.pi / self.n_heads)
+        grid_init = torch.stack([thetas.cos(), thetas.sin()], -1)
+        grid_init = (grid_init / grid_init.abs().max(-1, keepdim=True)[0]).view(self.n_heads, 1, 1, 2) \
+            .repeat(1, self.n_levels, self.n_points, 1)
+        for i in range(self.n_points):
+            grid_init[:, :, i, :] *= i + 1
+        with torch.no_grad():
+            self.sampling_offsets.bias = nn.Parameter(grid_init.view(-1))
+        constant_(self.attention_weights.weight.data, 0.)
+        constant_(self.attention_weights.bias.data, 0.)
+        xavier_uniform_(self.value_proj.weight.data)
+        constant_(self.value_proj.bias.data, 0.)
+        xavier_uniform_(self.output_proj.weight.data)
+        constant_(self.output_proj.bias.data, 0.)
+
+    def forward(self, query, reference_points, input_flatten, input_spatial_shapes,
+                input_padding_mask=None, query_attn_mask=None):
+        N, Len_q, _ = query.shape
+        N, Len_in, _ = input_flatten.shape
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            return self._forward_autograd(query, reference_points, input_flatten, input_spatial_shapes,
+                                          input_padding_mask, query_attn_mask)
+        value = K.linear(input_flatten, self.value_proj.weight, self.value_proj.bias,
+                         row_mask=input_padding_mask)
+        out = self.sample(query, reference_points, value, input_spatial_shapes, query_attn_mask)
+        return K.linear(out, self.output_proj.weight, self.output_proj.bias)
+
+    # -- pieces used by the fused transformer layers ------------------------------------
+    def packed_offsets_weights(self):
+        """[sampling_offsets ; attention_weights] stacked into one (M*L*P*3, d) GEMM."""
+        w = torch.cat([self.sampling_offsets.weight, self.attention_weights.weight], 0)
+        b = torch.cat([self.sampling_offsets.bias, self.attention_weights.bias], 0)
+        return w, b
+
+    def sample(self, query, reference_points, value, input_spatial_shapes, query_attn_mask=None):
+        """value already projected (N, S, d); returns the pre-output_proj (N, Lq, d)."""
+        w, b = self.packed_offsets_weights()
+        offlog = K.linear(query, w, b, out_dtype=torch.float32)
+        return K.msda_fused(value, input_spatial_shapes, offlog, reference_points,
+                            self.n_heads, self.n_levels, self.n_points, query_attn_mask)
+
+    def _forward_autograd(self, query, reference_points, input_flatten, input_spatial_shapes,
+                          input_padding_mask, query_attn_mask):
+        # ms_deform_attn.py:64-88, step by step
+        import torch.nn.functional as F
+        N, Len_q, _ = query.shape
+        N, Len_in, _ = input_flatten.shape
+        value = self.value_proj(input_flatten)
+        if input_padding_mask is not None:
+            value = value.masked_fill(input_padding_mask[..., None], float(0))
+        value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
+        sampling_offsets = self.sampling_offsets(query).view(N, Len_q, self.n_heads, self.n_levels, self.n_points, 2)
+        attention_weights = self.attention_weights(query).view(N, Len_q, self.n_heads, self.n_levels * self.n_points)
+        attention_weights = F.softmax(attention_weights, -1).view(N, Len_q, self.n_heads, self.n_levels, self.n_points)
+        if query_attn_mask is not None:
+            attention_weights = attention_weights.masked_fill(query_attn_mask[..., None, None, None], float(0))
+        if reference_points.shape[-1] == 2:
+            sampling_locations = reference_points[:, :, None, :, None, :] \
+                + sampling_offsets / input_spatial_shapes[None, None, None, :, None, :]
+        elif reference_points.shape[-1] == 4:
+            sampling_locations = reference_points[:, :, None, :, None, :2] \
+                + sampling_offsets / self.n_points * reference_points[:, :, None, :, None, 2:] * 0.5
+        else:
+            raise ValueError('Last dim of reference_points must be 2 or 4, but get {} instead.'
+                             .format(reference_points.shape[-1]))
+        output = MSDeformAttnFunction.apply(value, input_spatial_shapes, sampling_locations,
+                                            attention_weights, self.im2col_step)
+        return self.output_proj(output)
