@@ -70,10 +70,33 @@ def exported(name):
     return hasattr(lib(), name)
 
 
-def call(name, *args):
-    """Invoke a C-ABI entry point and raise RuntimeError on a non-zero status."""
+_trace = None   # list of (name, work dict, start event, end event) while tracing
+
+
+def trace_begin():
+    """Record a HIP event pair around every subsequent launch (bench.py roofline pass)."""
+    global _trace
+    _trace = []
+
+
+def trace_end():
+    global _trace
+    t, _trace = _trace, None
+    return t
+
+
+def call(name, *args, work=None):
+    """Invoke a C-ABI entry point and raise RuntimeError on a non-zero status.
+    `work` ({'flops': .., 'bytes': ..}) annotates the launch for the tracer."""
     fn = getattr(lib(), name)
-    rc = fn(*args)
+    if _trace is not None:
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        rc = fn(*args)
+        e.record()
+        _trace.append((name, work or {}, s, e))
+    else:
+        rc = fn(*args)
     if rc != 0:
         msg = lib().kinet_last_error().decode(errors='replace')
         raise RuntimeError(f'{name}: {msg}')

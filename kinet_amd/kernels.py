@@ -16,8 +16,10 @@ _cache = {}   # id(tensor) -> (weakref(tensor), {tag: ((version, data_ptr), valu
 
 
 def _drop(key):
-    def cb(_ref):
-        _cache.pop(key, None)
+    def cb(ref, _c=_cache):
+        ent = _c.get(key) if _c is not None else None
+        if ent is not None and ent[0] is ref:   # a newer tensor may have reused the id
+            del _c[key]
     return cb
 
 
@@ -44,6 +46,33 @@ def cached(t, tag, make):
 
 def clear_cache():
     _cache.clear()
+
+
+def cached_multi(tensors, tag, make):
+    """Cache make(*tensors) on the first tensor, invalidated if ANY of them changes."""
+    t0 = tensors[0]
+    key = id(t0)
+    ent = _cache.get(key)
+    if ent is None or ent[0]() is not t0:
+        ent = (weakref.ref(t0, _drop(key)), {})
+        _cache[key] = ent
+    ver = tuple((t._version, t.data_ptr()) for t in tensors)
+    hit = ent[1].get(tag)
+    if hit is not None and hit[0] == ver:
+        return hit[1]
+    v = make(*tensors)
+    ent[1][tag] = (ver, v)
+    return v
+
+
+def param_rows(p, start, end):
+    """A stable (cached) row-slice view of a parameter, so its dtype cast is cached too."""
+    return cached(p, ('rows', start, end), lambda t: t.detach()[start:end])
+
+
+def param_matrix(p):
+    """Conv 1x1 weight (O, I, 1, 1) viewed as a (O, I) GEMM operand (stable object)."""
+    return cached(p, 'matrix', lambda t: t.detach().reshape(t.shape[0], -1))
 
 
 def weight_as(w, dtype):
@@ -86,9 +115,12 @@ def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_d
     mask = None
     if row_mask is not None:
         mask = row_mask.reshape(-1).to(torch.uint8).contiguous()
+    e = x.element_size()
     N.call('kinet_gemm', N.ptr(x2), N.ptr(w), N.ptr(out), M, Nout, K, x2.stride(0), K, ldc,
            N.dtype_code(x.dtype), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(r), ldr, int(relu),
-           N.dtype_code(odt), N.ptr(mask), 0, N.stream(x.device))
+           N.dtype_code(odt), N.ptr(mask), 0, N.stream(x.device),
+           work={'family': 'gemm', 'flops': 2.0 * M * Nout * K,
+                 'bytes': (M * K + Nout * K) * e + M * Nout * out.element_size() * (2 if r is not None else 1)})
     return out.view(*lead, Nout) if out.is_contiguous() else out
 
 
@@ -118,9 +150,12 @@ def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, res
     r = None
     if residual is not None:
         r = residual
+    e = x.element_size()
     N.call('kinet_conv2d', N.ptr(x), N.ptr(w_packed), N.ptr(out), B, H, W, Cin, Ho, Wo, Cout, KH, KW,
            stride, pad, N.dtype_code(x.dtype), N.ptr(scale), N.ptr(bias), N.ptr(r),
-           Cout if r is not None else 0, int(relu), ldy, N.stream(x.device))
+           Cout if r is not None else 0, int(relu), ldy, N.stream(x.device),
+           work={'family': 'conv', 'flops': 2.0 * B * Ho * Wo * Cout * KH * KW * Cin,
+                 'bytes': (B * H * W * Cin + Cout * KH * KW * Cin + B * Ho * Wo * Cout * (2 if r is not None else 1)) * e})
     return out
 
 
@@ -151,7 +186,8 @@ def layernorm(x, weight, bias, eps=1e-5, residual=None, out=None):
     y = out if out is not None else torch.empty_like(x2)
     rows = x2.numel() // d
     N.call('kinet_layernorm', N.ptr(x2), N.ptr(r), N.ptr(f32(weight)), N.ptr(f32(bias)), N.ptr(y), rows, d,
-           float(eps), N.dtype_code(x.dtype), 0, N.stream(x.device))
+           float(eps), N.dtype_code(x.dtype), 0, N.stream(x.device),
+           work={'family': 'norm', 'bytes': rows * d * x2.element_size() * (3 if r is not None else 2)})
     return y
 
 
@@ -163,7 +199,8 @@ def groupnorm_nhwc(x, weight, bias, groups, eps=1e-5, out=None, out_batch_stride
         out_batch_stride = HW * C
     stats = torch.empty(2 * B * groups, dtype=torch.float32, device=x.device)
     N.call('kinet_groupnorm', N.ptr(x), N.ptr(f32(weight)), N.ptr(f32(bias)), N.ptr(out), B, HW, C, groups,
-           int(out_batch_stride), float(eps), N.dtype_code(x.dtype), N.ptr(stats), N.stream(x.device))
+           int(out_batch_stride), float(eps), N.dtype_code(x.dtype), N.ptr(stats), N.stream(x.device),
+           work={'family': 'norm', 'bytes': 2 * x.numel() * x.element_size()})
     return out
 
 
@@ -171,7 +208,8 @@ def add(a, b, out=None):
     a = a.contiguous()
     b = b.contiguous()
     y = out if out is not None else torch.empty_like(a)
-    N.call('kinet_add', N.ptr(a), N.ptr(b), N.ptr(y), a.numel(), N.dtype_code(a.dtype), N.stream(a.device))
+    N.call('kinet_add', N.ptr(a), N.ptr(b), N.ptr(y), a.numel(), N.dtype_code(a.dtype), N.stream(a.device),
+           work={'family': 'eltwise', 'bytes': 3 * a.numel() * a.element_size()})
     return y
 
 
@@ -187,7 +225,8 @@ def mha_core(q, k, v, heads, scale, key_mask=None, out=None):
     o = out if out is not None else torch.empty((B, Lq, E), dtype=q.dtype, device=q.device)
     km = key_mask.to(torch.uint8).contiguous() if key_mask is not None else None
     N.call('kinet_mha_core', N.ptr(q), q.stride(1), N.ptr(k), k.stride(1), N.ptr(v), v.stride(1), N.ptr(o),
-           o.stride(1), B, Lq, Lk, heads, D, float(scale), N.dtype_code(q.dtype), N.ptr(km), N.stream(q.device))
+           o.stride(1), B, Lq, Lk, heads, D, float(scale), N.dtype_code(q.dtype), N.ptr(km), N.stream(q.device),
+           work={'family': 'attn', 'flops': 4.0 * B * heads * Lq * Lk * D})
     return o
 
 
@@ -231,9 +270,16 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
     qm = query_attn_mask.to(torch.uint8).contiguous() if query_attn_mask is not None else None
     if offlog.dtype != torch.float32:
         raise RuntimeError('msda_fused: the offsets/logits projection must be f32')
+    ev = value.element_size()
+    nsamp = B * Lq * n_heads * n_levels * n_points
     N.call('kinet_msda_fused_forward', N.ptr(value), N.ptr(spatial_shapes), N.ptr(offlog), offlog.shape[-1],
            N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), N.ptr(loc), N.ptr(attw), B, S, n_heads, D,
-           n_levels, Lq, n_points, N.dtype_code(value.dtype), N.stream(value.device))
+           n_levels, Lq, n_points, N.dtype_code(value.dtype), N.stream(value.device),
+           work={'family': 'msda', 'flops': 10.0 * nsamp * D,
+                 # compulsory bytes: value once, f32 offsets+logits, refs, output once
+                 'bytes': B * S * d * ev + nsamp * 3 * 4 + ref.numel() * 4 + B * Lq * d * ev
+                 + (nsamp * 3 * 4 if want_loc_attw else 0),
+                 'Lq': Lq, 'S': S})
     if want_loc_attw:
         return out, loc, attw
     return out

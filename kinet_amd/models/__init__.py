@@ -1,0 +1,99 @@
+"""`build_model(args) -> (model, criterion, postprocessors)` for the detection hot path,
+mirroring src/trackformer/models/__init__.py:16-71 (deformable branch).
+
+    from kinet_amd.models import build_model      # instead of trackformer.models
+    model, criterion, postprocessors = build_model(args)
+    model.set_compute_dtype(torch.bfloat16)        # optional perf mode (default fp32)
+
+`args` is the reference's Namespace (cfgs/train.yaml + named configs).  Only the
+deformable image branch is on this path; `args.kine` / vanilla DETR / masks raise.
+"""
+import torch
+
+from kinet_amd.models.backbone import build_backbone
+from kinet_amd.models.deformable_detr import DeformableDETR, DeformablePostProcess
+from kinet_amd.models.deformable_transformer import build_deforamble_transformer
+from kinet_amd.models.detr_tracking import DeformableDETRTracking
+from kinet_amd.models.misc import NestedTensor, nested_tensor_from_tensor_list
+
+NUM_CLASSES = {'coco': 91, 'coco_panoptic': 250, 'coco_person': 20, 'mot': 20, 'mot_crowdhuman': 20,
+               'crowdhuman': 20, 'mot_coco_person': 20}
+
+
+def build_model(args):
+    if args.dataset not in NUM_CLASSES:
+        raise NotImplementedError(args.dataset)
+    num_classes = NUM_CLASSES[args.dataset]
+    if not args.deformable:
+        raise NotImplementedError('vanilla DETR (config 1) is outside the MSDeformAttn hot path')
+    if getattr(args, 'masks', False):
+        raise NotImplementedError('segmentation heads are outside the hot path')
+    backbone = build_backbone(args)
+    matcher = None
+    try:
+        from kinet_amd.models.matcher import build_matcher
+        matcher = build_matcher(args)
+    except ImportError:
+        pass
+    detr_kwargs = {
+        'backbone': backbone,
+        'num_classes': num_classes - 1 if args.focal_loss else num_classes,
+        'num_queries': args.num_queries,
+        'aux_loss': args.aux_loss,
+        'overflow_boxes': args.overflow_boxes,
+        'transformer': build_deforamble_transformer(args),
+        'num_feature_levels': args.num_feature_levels,
+        'with_box_refine': args.with_box_refine,
+        'two_stage': args.two_stage,
+        'multi_frame_attention': args.multi_frame_attention,
+        'multi_frame_encoding': args.multi_frame_encoding,
+        'merge_frame_features': args.merge_frame_features,
+    }
+    if args.tracking:
+        tracking_kwargs = {
+            'track_query_false_positive_prob': args.track_query_false_positive_prob,
+            'track_query_false_negative_prob': args.track_query_false_negative_prob,
+            'matcher': matcher,
+            'backprop_prev_frame': args.track_backprop_prev_frame}
+        model = DeformableDETRTracking(tracking_kwargs, detr_kwargs)
+    else:
+        model = DeformableDETR(**detr_kwargs)
+    criterion = None
+    try:
+        from kinet_amd.models.criterion import build_criterion
+        criterion = build_criterion(args, num_classes, matcher)
+    except ImportError:
+        pass
+    postprocessors = {'bbox': DeformablePostProcess()}
+    return model, criterion, postprocessors
+
+
+def smoke_forward(device):
+    """One tiny detector forward on `device` checked against the reference fixture
+    (used by __graft_entry__.smoke())."""
+    import os
+    import sys
+    import numpy as np
+    here = os.path.dirname(os.path.abspath(__file__))
+    golden = os.path.join(here, '..', '..', 'tests', 'golden')
+    sys.path.insert(0, golden)
+    from weights import make_state_dict
+    from kinet_amd.models.config import load_args
+    d = np.load(os.path.join(golden, 'detr_config2_small.npz'))
+    args = load_args('train_deformable')
+    model, _, _ = build_model(args)
+    keys = [ln.split() for ln in open(os.path.join(golden, 'detr_config2_small.keys.txt'))]
+    model.load_state_dict(make_state_dict({k[0]: [int(s) for s in k[1:]] for k in keys}, seed=21))
+    model = model.to(device).eval()
+    imgs = [torch.from_numpy(d['img0']).to(device), torch.from_numpy(d['img1']).to(device)]
+    with torch.no_grad():
+        out = model(imgs)[0]
+    torch.cuda.synchronize()
+    err_l = (out['pred_logits'].cpu() - torch.from_numpy(d['pred_logits'])).abs().max().item()
+    err_b = (out['pred_boxes'].cpu() - torch.from_numpy(d['pred_boxes'])).abs().max().item()
+    assert err_l < 1e-3 and err_b < 1e-3, (err_l, err_b)
+    print(f'smoke detector: max|dlogits|={err_l:.2e} max|dboxes|={err_b:.2e}')
+
+
+__all__ = ['build_model', 'DeformableDETR', 'DeformableDETRTracking', 'DeformablePostProcess',
+           'NestedTensor', 'nested_tensor_from_tensor_list']

@@ -1,0 +1,221 @@
+"""ResNet-50/101 backbone of the detection path, NHWC, run by the kinet_amd implicit-GEMM
+conv kernel with FrozenBatchNorm2d folded into the epilogue.
+
+Mirrors src/trackformer/models/backbone.py (FrozenBatchNorm2d :22-58, BackboneBase
+:61-91, Backbone :94-108, Joiner :180-194, build_backbone :197-230).  The ResNet body
+follows torchvision's v1.5 definition (the reference instantiates
+torchvision.models.resnet50/101, backbone.py:102): 7x7/2 stem, 3x3/2 max-pool,
+Bottleneck blocks with the stride on the 3x3 conv and a 1x1 strided downsample on the
+first block of each stage.  Module/parameter names equal torchvision's, so reference
+state_dicts (`backbone.0.body.layer1.0.conv1.weight`, ...) load unchanged.
+"""
+from collections import OrderedDict
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from kinet_amd import kernels as K
+from kinet_amd.models.misc import NestedTensor
+from kinet_amd.models.position_encoding import build_position_encoding
+
+
+class FrozenBatchNorm2d(nn.Module):
+    """backbone.py:22-58; folded to (scale, bias) = (w*rsqrt(rv+1e-5), b - rm*scale)."""
+
+    def __init__(self, n):
+        super().__init__()
+        self.register_buffer("weight", torch.ones(n))
+        self.register_buffer("bias", torch.zeros(n))
+        self.register_buffer("running_mean", torch.zeros(n))
+        self.register_buffer("running_var", torch.ones(n))
+        self._fold = None
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict,
+                              missing_keys, unexpected_keys, error_msgs):
+        state_dict.pop(prefix + 'num_batches_tracked', None)
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict,
+                                      missing_keys, unexpected_keys, error_msgs)
+
+    def folded(self):
+        key = tuple((b.data_ptr(), b._version) for b in (self.weight, self.bias, self.running_mean, self.running_var))
+        if self._fold is None or self._fold[0] != key:
+            scale = self.weight * (self.running_var + 1e-5).rsqrt()
+            bias = self.bias - self.running_mean * scale
+            self._fold = (key, scale.float().contiguous(), bias.float().contiguous())
+        return self._fold[1], self._fold[2]
+
+    def forward(self, x):   # NCHW reference semantics (used by the autograd path)
+        scale, bias = self.folded()
+        return x * scale.reshape(1, -1, 1, 1) + bias.reshape(1, -1, 1, 1)
+
+
+def conv_bn(x, conv, bn, relu, residual=None, cin_pad=None):
+    """NHWC conv + folded BN (+ residual) (+ ReLU) in one kernel launch."""
+    w = K.pack_conv_weight(conv.weight, x.dtype, cin_pad)
+    scale, bias = bn.folded()
+    return K.conv2d_nhwc(x, w, conv.stride[0], conv.padding[0], scale=scale, bias=bias, relu=relu,
+                         residual=residual)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, dilation=1):
+        super().__init__()
+        if dilation != 1:
+            raise NotImplementedError('dilated (DC5) ResNet is not on the configured hot path')
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = FrozenBatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = FrozenBatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = FrozenBatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward_nhwc(self, x):
+        out = conv_bn(x, self.conv1, self.bn1, True)
+        out = conv_bn(out, self.conv2, self.bn2, True)
+        identity = x if self.downsample is None else conv_bn(x, self.downsample[0], self.downsample[1], False)
+        return conv_bn(out, self.conv3, self.bn3, True, residual=identity)
+
+    def forward(self, x):   # NCHW autograd path
+        identity = x
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = F.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        return F.relu(out + identity)
+
+
+class ResNetBody(nn.Module):
+    """torchvision ResNet up to layer4 (what IntermediateLayerGetter keeps, backbone.py:81)."""
+
+    def __init__(self, layers, dilation=False):
+        super().__init__()
+        if dilation:
+            raise NotImplementedError('dilated (DC5) ResNet is not on the configured hot path')
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = FrozenBatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(64, layers[0])
+        self.layer2 = self._make_layer(128, layers[1], 2)
+        self.layer3 = self._make_layer(256, layers[2], 2)
+        self.layer4 = self._make_layer(512, layers[3], 2)
+
+    def _make_layer(self, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * 4:
+            downsample = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
+                                       FrozenBatchNorm2d(planes * 4))
+        layers = [Bottleneck(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * 4
+        layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward_nhwc(self, img_nchw, dtype):
+        """img (B, 3, H, W) f32 -> [layer1, layer2, layer3, layer4] NHWC in dtype."""
+        x = K.pack_image(img_nchw, dtype, 8)
+        x = conv_bn(x, self.conv1, self.bn1, True, cin_pad=8)
+        x = K.maxpool_3x3s2(x)
+        outs = []
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                x = blk.forward_nhwc(x)
+            outs.append(x)
+        return outs
+
+    def forward(self, x):   # NCHW autograd path -> OrderedDict like IntermediateLayerGetter
+        x = self.maxpool(F.relu(self.bn1(self.conv1(x))))
+        out = OrderedDict()
+        for i, layer in enumerate((self.layer1, self.layer2, self.layer3, self.layer4)):
+            x = layer(x)
+            out[str(i)] = x
+        return out
+
+
+def nhwc_as_nchw(x):
+    """(B, H, W, C) contiguous -> (B, C, H, W) view (channels_last strides, no copy)."""
+    return x.permute(0, 3, 1, 2)
+
+
+def nchw_to_nhwc(x):
+    """Accept a (B, C, H, W) tensor (e.g. prev_features from a previous frame) as NHWC."""
+    y = x.permute(0, 2, 3, 1)
+    return y if y.is_contiguous() else y.contiguous()
+
+
+def interp_mask(mask, size):
+    """backbone.py:89: nearest-neighbour resize of the padding mask."""
+    return F.interpolate(mask[None].float(), size=size).to(torch.bool)[0]
+
+
+class BackboneBase(nn.Module):
+    def __init__(self, body: nn.Module, train_backbone: bool, return_interm_layers: bool):
+        super().__init__()
+        for name, parameter in body.named_parameters():
+            if (not train_backbone or 'layer2' not in name and 'layer3' not in name and 'layer4' not in name):
+                parameter.requires_grad_(False)
+        if return_interm_layers:
+            self.strides = [4, 8, 16, 32]
+            self.num_channels = [256, 512, 1024, 2048]
+            self.return_idx = [0, 1, 2, 3]
+        else:
+            self.strides = [32]
+            self.num_channels = [2048]
+            self.return_idx = [3]
+        self.body = body
+
+    def forward_nhwc(self, img, dtype):
+        outs = self.body.forward_nhwc(img, dtype)
+        return [outs[i] for i in self.return_idx]
+
+    def forward(self, tensor_list: NestedTensor, dtype=None):
+        """backbone.py:83-91 -> {name: NestedTensor}; tensors are NCHW views of NHWC buffers."""
+        dtype = dtype or torch.float32
+        xs = self.forward_nhwc(tensor_list.tensors, dtype)
+        out = OrderedDict()
+        for i, x in enumerate(xs):
+            mask = interp_mask(tensor_list.mask, x.shape[1:3])
+            out[str(i)] = NestedTensor(nhwc_as_nchw(x), mask, tensor_list.sizes)
+        return out
+
+
+class Backbone(BackboneBase):
+    """backbone.py:94-108 (ResNet with frozen BatchNorm; pretrained ImageNet weights are a
+    remote fetch in the reference and are not fetched here -- load a state_dict instead)."""
+
+    def __init__(self, name: str, train_backbone: bool, return_interm_layers: bool, dilation: bool):
+        layers = {'resnet50': [3, 4, 6, 3], 'resnet101': [3, 4, 23, 3]}.get(name)
+        if layers is None:
+            raise ValueError(f'unsupported backbone {name}')
+        super().__init__(ResNetBody(layers, dilation), train_backbone, return_interm_layers)
+
+
+class Joiner(nn.Sequential):
+    """backbone.py:180-194 (+ the `strides` attribute the reference forgot, :183)."""
+
+    def __init__(self, backbone, position_embedding):
+        super().__init__(backbone, position_embedding)
+        self.num_channels = backbone.num_channels
+        self.strides = backbone.strides
+
+    def forward(self, tensor_list: NestedTensor, dtype=None):
+        xs = self[0](tensor_list, dtype)
+        out, pos = [], []
+        for x in xs.values():
+            out.append(x)
+            pos.append(self[1](x).to(x.tensors.dtype))
+        return out, pos
+
+
+def build_backbone(args):
+    return_interm_layers = args.masks or (args.num_feature_levels > 1)
+    position_embedding = build_position_encoding(args)
+    backbone = Backbone(args.backbone, args.lr_backbone > 0, return_interm_layers, args.dilation)
+    return Joiner(backbone, position_embedding)

@@ -1,0 +1,413 @@
+"""Deformable-DETR encoder/decoder on the kinet_amd kernels.
+
+Mirrors src/trackformer/models/deformable_transformer.py (DeformableTransformer :21-257,
+encoder layer :260-299, encoder :302-330, decoder layer :333-386, decoder :389-434,
+build_deforamble_transformer :437-457) with the same module/parameter names.
+
+Two execution paths with identical arithmetic:
+  * inference (autograd disabled) -- every op is a HIP kernel: value_proj GEMM with the
+    padding mask in its epilogue, ONE GEMM for the concatenated sampling_offsets |
+    attention_weights projection (f32 out), the fused softmax/location/sampling MSDA
+    kernel, output_proj GEMM with the residual add in its epilogue, LayerNorm kernel,
+    FFN as two GEMMs (ReLU / residual fused), decoder self-attention as in_proj GEMMs +
+    the MHA kernel, and box refinement as one small kernel.  Activations stay in the
+    compute dtype (bf16 perf mode, f32 parity mode) in (batch, tokens, channels) layout.
+  * training (autograd enabled) -- the reference's op sequence in torch with
+    MSDeformAttnFunction (HIP forward/backward kernels) at the operator boundary.
+Reference quirks kept on purpose: 2-d sampling offsets divided by
+(H, W) applied to (x, y); multi-frame memory concatenated [current, prev] while shapes,
+masks and valid ratios stay [prev, current].
+"""
+import copy
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.nn.init import constant_, normal_, xavier_uniform_
+
+from kinet_amd import kernels as K
+from kinet_amd.models.misc import inverse_sigmoid
+from kinet_amd.msda import MSDeformAttn
+
+
+def _get_clones(module, N):
+    return nn.ModuleList([copy.deepcopy(module) for _ in range(N)])
+
+
+def _get_activation_fn(activation):
+    if activation == "relu":
+        return F.relu
+    if activation == "gelu":
+        return F.gelu
+    if activation == "glu":
+        return F.glu
+    raise RuntimeError(F"activation should be relu/gelu, not {activation}.")
+
+
+def fast_path():
+    return not torch.is_grad_enabled()
+
+
+class DeformableTransformerEncoderLayer(nn.Module):
+    def __init__(self, d_model=256, d_ffn=1024, dropout=0.1, activation="relu", n_levels=4, n_heads=8, n_points=4):
+        super().__init__()
+        if activation != 'relu':
+            raise NotImplementedError('only relu FFNs are on the configured hot path')
+        self.self_attn = MSDeformAttn(d_model, n_levels, n_heads, n_points)
+        self.dropout1 = nn.Dropout(dropout)
+        self.norm1 = nn.LayerNorm(d_model)
+        self.linear1 = nn.Linear(d_model, d_ffn)
+        self.activation = _get_activation_fn(activation)
+        self.dropout2 = nn.Dropout(dropout)
+        self.linear2 = nn.Linear(d_ffn, d_model)
+        self.dropout3 = nn.Dropout(dropout)
+        self.norm2 = nn.LayerNorm(d_model)
+
+    @staticmethod
+    def with_pos_embed(tensor, pos):
+        return tensor if pos is None else tensor + pos
+
+    def forward_ffn(self, src):
+        src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
+        return self.norm2(src + self.dropout3(src2))
+
+    def forward(self, src, pos, reference_points, spatial_shapes, padding_mask=None):
+        if fast_path():
+            return self.forward_fast(src, pos, reference_points, spatial_shapes, padding_mask)
+        src2 = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, spatial_shapes, padding_mask)
+        src = self.norm1(src + self.dropout1(src2))
+        return self.forward_ffn(src)
+
+    def forward_fast(self, src, pos, reference_points, spatial_shapes, padding_mask=None):
+        # deformable_transformer.py:290-299, one kernel per step
+        a = self.self_attn
+        q = K.add(src, pos) if pos is not None else src
+        value = K.linear(src, a.value_proj.weight, a.value_proj.bias, row_mask=padding_mask)
+        samp = a.sample(q, reference_points, value, spatial_shapes)
+        src = K.linear(samp, a.output_proj.weight, a.output_proj.bias, residual=src)
+        src = K.layernorm(src, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        h = K.linear(src, self.linear1.weight, self.linear1.bias, relu=True)
+        src = K.linear(h, self.linear2.weight, self.linear2.bias, residual=src)
+        return K.layernorm(src, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+
+
+class DeformableTransformerEncoder(nn.Module):
+    def __init__(self, encoder_layer, num_layers):
+        super().__init__()
+        self.layers = _get_clones(encoder_layer, num_layers)
+        self.num_layers = num_layers
+
+    @staticmethod
+    def get_reference_points(spatial_shapes, valid_ratios, device):
+        """deformable_transformer.py:309-321: pixel centres normalised by the valid extent."""
+        reference_points_list = []
+        for lvl, (H_, W_) in enumerate(spatial_shapes):
+            H_, W_ = int(H_), int(W_)
+            ref_y, ref_x = torch.meshgrid(torch.linspace(0.5, H_ - 0.5, H_, dtype=torch.float32, device=device),
+                                          torch.linspace(0.5, W_ - 0.5, W_, dtype=torch.float32, device=device),
+                                          indexing='ij')
+            ref_y = ref_y.reshape(-1)[None] / (valid_ratios[:, None, lvl, 1] * H_)
+            ref_x = ref_x.reshape(-1)[None] / (valid_ratios[:, None, lvl, 0] * W_)
+            reference_points_list.append(torch.stack((ref_x, ref_y), -1))
+        reference_points = torch.cat(reference_points_list, 1)
+        return reference_points[:, :, None] * valid_ratios[:, None]
+
+    def forward(self, src, spatial_shapes, valid_ratios, pos=None, padding_mask=None, reference_points=None):
+        output = src
+        if reference_points is None:
+            shapes = spatial_shapes.tolist() if torch.is_tensor(spatial_shapes) else spatial_shapes
+            reference_points = self.get_reference_points(shapes, valid_ratios, device=src.device)
+        if not torch.is_tensor(spatial_shapes):
+            spatial_shapes = torch.as_tensor(spatial_shapes, dtype=torch.long, device=src.device)
+        for layer in self.layers:
+            output = layer(output, pos, reference_points, spatial_shapes, padding_mask)
+        return output
+
+
+class DeformableTransformerDecoderLayer(nn.Module):
+    def __init__(self, d_model=256, d_ffn=1024, dropout=0.1, activation="relu", n_levels=4, n_heads=8, n_points=4):
+        super().__init__()
+        if activation != 'relu':
+            raise NotImplementedError('only relu FFNs are on the configured hot path')
+        self.cross_attn = MSDeformAttn(d_model, n_levels, n_heads, n_points)
+        self.dropout1 = nn.Dropout(dropout)
+        self.norm1 = nn.LayerNorm(d_model)
+        self.self_attn = nn.MultiheadAttention(d_model, n_heads, dropout=dropout)
+        self.dropout2 = nn.Dropout(dropout)
+        self.norm2 = nn.LayerNorm(d_model)
+        self.linear1 = nn.Linear(d_model, d_ffn)
+        self.activation = _get_activation_fn(activation)
+        self.dropout3 = nn.Dropout(dropout)
+        self.linear2 = nn.Linear(d_ffn, d_model)
+        self.dropout4 = nn.Dropout(dropout)
+        self.norm3 = nn.LayerNorm(d_model)
+
+    @staticmethod
+    def with_pos_embed(tensor, pos):
+        return tensor if pos is None else tensor + pos
+
+    def forward_ffn(self, tgt):
+        tgt2 = self.linear2(self.dropout3(self.activation(self.linear1(tgt))))
+        return self.norm3(tgt + self.dropout4(tgt2))
+
+    def forward(self, tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask=None,
+                query_attn_mask=None, value=None):
+        if fast_path():
+            return self.forward_fast(tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask,
+                                     query_attn_mask, value)
+        q = k = self.with_pos_embed(tgt, query_pos)
+        tgt2 = self.self_attn(q.transpose(0, 1), k.transpose(0, 1), tgt.transpose(0, 1),
+                              key_padding_mask=query_attn_mask)[0].transpose(0, 1)
+        tgt = self.norm2(tgt + self.dropout2(tgt2))
+        tgt2 = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_spatial_shapes,
+                               src_padding_mask, query_attn_mask)
+        tgt = self.norm1(tgt + self.dropout1(tgt2))
+        return self.forward_ffn(tgt)
+
+    def forward_fast(self, tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask=None,
+                     query_attn_mask=None, value=None):
+        # deformable_transformer.py:367-386
+        d = tgt.shape[-1]
+        sa = self.self_attn
+        qk_in = K.add(tgt, query_pos) if query_pos is not None else tgt
+        qk = K.linear(qk_in, K.param_rows(sa.in_proj_weight, 0, 2 * d), K.param_rows(sa.in_proj_bias, 0, 2 * d))
+        v = K.linear(tgt, K.param_rows(sa.in_proj_weight, 2 * d, 3 * d), K.param_rows(sa.in_proj_bias, 2 * d, 3 * d))
+        attn = K.mha_core(qk[..., :d], qk[..., d:], v, sa.num_heads, sa.head_dim ** -0.5, key_mask=query_attn_mask)
+        tgt = K.linear(attn, sa.out_proj.weight, sa.out_proj.bias, residual=tgt)
+        tgt = K.layernorm(tgt, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        ca = self.cross_attn
+        q = K.add(tgt, query_pos) if query_pos is not None else tgt
+        if value is None:
+            value = K.linear(src, ca.value_proj.weight, ca.value_proj.bias, row_mask=src_padding_mask)
+        samp = ca.sample(q, reference_points, value, src_spatial_shapes, query_attn_mask)
+        tgt = K.linear(samp, ca.output_proj.weight, ca.output_proj.bias, residual=tgt)
+        tgt = K.layernorm(tgt, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        h = K.linear(tgt, self.linear1.weight, self.linear1.bias, relu=True)
+        tgt = K.linear(h, self.linear2.weight, self.linear2.bias, residual=tgt)
+        return K.layernorm(tgt, self.norm3.weight, self.norm3.bias, self.norm3.eps)
+
+
+def mlp_fast(mlp, x, out_dtype=torch.float32):
+    """detr.py:937-951 MLP (ReLU between layers) as chained GEMMs; last layer in out_dtype."""
+    n = len(mlp.layers)
+    for i, layer in enumerate(mlp.layers):
+        last = i == n - 1
+        x = K.linear(x, layer.weight, layer.bias, relu=not last, out_dtype=out_dtype if last else None)
+    return x
+
+
+class DeformableTransformerDecoder(nn.Module):
+    def __init__(self, decoder_layer, num_layers, return_intermediate=False):
+        super().__init__()
+        self.layers = _get_clones(decoder_layer, num_layers)
+        self.num_layers = num_layers
+        self.return_intermediate = return_intermediate
+        self.bbox_embed = None
+        self.class_embed = None
+
+    def forward(self, tgt, reference_points, src, src_spatial_shapes, src_valid_ratios,
+                query_pos=None, src_padding_mask=None, query_attn_mask=None):
+        if fast_path():
+            return self.forward_fast(tgt, reference_points, src, src_spatial_shapes, src_valid_ratios,
+                                     query_pos, src_padding_mask, query_attn_mask)
+        output = tgt
+        intermediate, intermediate_reference_points = [], []
+        for lid, layer in enumerate(self.layers):
+            if reference_points.shape[-1] == 4:
+                reference_points_input = reference_points[:, :, None] \
+                    * torch.cat([src_valid_ratios, src_valid_ratios], -1)[:, None]
+            else:
+                assert reference_points.shape[-1] == 2
+                reference_points_input = reference_points[:, :, None] * src_valid_ratios[:, None]
+            output = layer(output, query_pos, reference_points_input, src, src_spatial_shapes, src_padding_mask,
+                           query_attn_mask)
+            if self.bbox_embed is not None:
+                tmp = self.bbox_embed[lid](output)
+                if reference_points.shape[-1] == 4:
+                    new_reference_points = (tmp + inverse_sigmoid(reference_points)).sigmoid()
+                else:
+                    new_reference_points = tmp
+                    new_reference_points[..., :2] = tmp[..., :2] + inverse_sigmoid(reference_points)
+                    new_reference_points = new_reference_points.sigmoid()
+                reference_points = new_reference_points.detach()
+            if self.return_intermediate:
+                intermediate.append(output)
+                intermediate_reference_points.append(reference_points)
+        if self.return_intermediate:
+            return torch.stack(intermediate), torch.stack(intermediate_reference_points)
+        return output, reference_points
+
+    def forward_fast(self, tgt, reference_points, src, src_spatial_shapes, src_valid_ratios,
+                     query_pos=None, src_padding_mask=None, query_attn_mask=None):
+        output = tgt
+        reference_points = reference_points.float()
+        vr = src_valid_ratios.float()
+        if reference_points.shape[-1] == 4:
+            ref_in = reference_points[:, :, None] * torch.cat([vr, vr], -1)[:, None]
+        else:
+            ref_in = reference_points[:, :, None] * vr[:, None]
+        intermediate, intermediate_reference_points = [], []
+        for lid, layer in enumerate(self.layers):
+            output = layer(output, query_pos, ref_in, src, src_spatial_shapes, src_padding_mask, query_attn_mask)
+            last = lid == len(self.layers) - 1
+            if self.bbox_embed is not None:
+                tmp = mlp_fast(self.bbox_embed[lid], output)
+                reference_points, nxt = K.box_refine(tmp, reference_points, vr, want_input=not last)
+                if not last:
+                    ref_in = nxt
+            if self.return_intermediate:
+                intermediate.append(output)
+                intermediate_reference_points.append(reference_points)
+        if self.return_intermediate:
+            return torch.stack(intermediate), torch.stack(intermediate_reference_points)
+        return output, reference_points
+
+
+class DeformableTransformer(nn.Module):
+    def __init__(self, d_model=256, nhead=8, num_encoder_layers=6, num_decoder_layers=6, dim_feedforward=1024,
+                 dropout=0.1, activation="relu", return_intermediate_dec=False, num_feature_levels=4,
+                 dec_n_points=4, enc_n_points=4, two_stage=False, two_stage_num_proposals=300,
+                 multi_frame_attention_separate_encoder=False):
+        super().__init__()
+        if two_stage:
+            raise NotImplementedError('two-stage Deformable DETR is not on the configured hot path '
+                                      '(two_stage: false in every BASELINE config)')
+        self.d_model = d_model
+        self.nhead = nhead
+        self.two_stage = two_stage
+        self.two_stage_num_proposals = two_stage_num_proposals
+        self.num_feature_levels = num_feature_levels
+        self.multi_frame_attention_separate_encoder = multi_frame_attention_separate_encoder
+        enc_levels = num_feature_levels // 2 if multi_frame_attention_separate_encoder else num_feature_levels
+        encoder_layer = DeformableTransformerEncoderLayer(d_model, dim_feedforward, dropout, activation,
+                                                          enc_levels, nhead, enc_n_points)
+        self.encoder = DeformableTransformerEncoder(encoder_layer, num_encoder_layers)
+        decoder_layer = DeformableTransformerDecoderLayer(d_model, dim_feedforward, dropout, activation,
+                                                          num_feature_levels, nhead, dec_n_points)
+        self.decoder = DeformableTransformerDecoder(decoder_layer, num_decoder_layers, return_intermediate_dec)
+        self.level_embed = nn.Parameter(torch.Tensor(num_feature_levels, d_model))
+        self.reference_points = nn.Linear(d_model, 2)
+        self._reset_parameters()
+
+    def _reset_parameters(self):
+        for p in self.parameters():
+            if p.dim() > 1:
+                nn.init.xavier_uniform_(p)
+        for m in self.modules():
+            if isinstance(m, MSDeformAttn):
+                m._reset_parameters()
+        xavier_uniform_(self.reference_points.weight.data, gain=1.0)
+        constant_(self.reference_points.bias.data, 0.)
+        normal_(self.level_embed)
+
+    @staticmethod
+    def get_valid_ratio(mask):
+        """deformable_transformer.py:124-131."""
+        _, H, W = mask.shape
+        valid_H = torch.sum(~mask[:, :, 0], 1)
+        valid_W = torch.sum(~mask[:, 0, :], 1)
+        return torch.stack([valid_W.float() / W, valid_H.float() / H], -1)
+
+    # ---------------------------------------------------------------------------------
+    def prepare_inputs(self, srcs, masks, pos_embeds):
+        """deformable_transformer.py:136-157 for NCHW inputs (reference call signature)."""
+        src_flatten, mask_flatten, lvl_pos_embed_flatten, spatial_shapes = [], [], [], []
+        for lvl, (src, mask, pos_embed) in enumerate(zip(srcs, masks, pos_embeds)):
+            bs, c, h, w = src.shape
+            spatial_shapes.append((h, w))
+            src_flatten.append(src.flatten(2).transpose(1, 2))
+            mask_flatten.append(mask.flatten(1))
+            lvl_pos_embed_flatten.append(pos_embed.flatten(2).transpose(1, 2) + self.level_embed[lvl].view(1, 1, -1))
+        src_flatten = torch.cat(src_flatten, 1)
+        mask_flatten = torch.cat(mask_flatten, 1)
+        lvl_pos_embed_flatten = torch.cat(lvl_pos_embed_flatten, 1)
+        valid_ratios = torch.stack([self.get_valid_ratio(m) for m in masks], 1)
+        return src_flatten, mask_flatten, lvl_pos_embed_flatten, spatial_shapes, valid_ratios
+
+    def forward(self, srcs, masks, pos_embeds, query_embed=None, targets=None):
+        src_flatten, mask_flatten, lvl_pos, shapes, valid_ratios = self.prepare_inputs(srcs, masks, pos_embeds)
+        if fast_path():
+            dt = srcs[0].dtype
+            src_flatten = src_flatten.to(dt).contiguous()
+            lvl_pos = lvl_pos.to(dt).contiguous()
+        geo = self.geometry(shapes, valid_ratios, mask_flatten, src_flatten.device)
+        return self.forward_flat(src_flatten, lvl_pos, geo, query_embed, targets)
+
+    def geometry(self, shapes, valid_ratios, mask_flatten, device):
+        """Everything that depends only on the level shapes and padding masks."""
+        L = len(shapes)
+        geo = {'shapes': [tuple(int(v) for v in s) for s in shapes], 'valid_ratios': valid_ratios}
+        geo['spatial_shapes'] = torch.as_tensor(geo['shapes'], dtype=torch.long, device=device)
+        geo['mask_flatten'] = mask_flatten
+        geo['pad_mask'] = mask_flatten if (mask_flatten is not None and bool(mask_flatten.any())) else None
+        if self.multi_frame_attention_separate_encoder:
+            half = L // 2
+            s_half = sum(h * w for h, w in geo['shapes'][:half])
+            geo['enc'] = []
+            for sl_lv, sl_tok in ((slice(0, half), slice(0, s_half)), (slice(half, L), slice(s_half, None))):
+                sh = geo['shapes'][sl_lv]
+                vr = valid_ratios[:, sl_lv]
+                geo['enc'].append(dict(shapes=sh, spatial_shapes=geo['spatial_shapes'][sl_lv].contiguous(),
+                                       valid_ratios=vr, tok=sl_tok,
+                                       ref=DeformableTransformerEncoder.get_reference_points(sh, vr, device)))
+        else:
+            geo['enc'] = [dict(shapes=geo['shapes'], spatial_shapes=geo['spatial_shapes'], valid_ratios=valid_ratios,
+                               tok=slice(0, None),
+                               ref=DeformableTransformerEncoder.get_reference_points(geo['shapes'], valid_ratios,
+                                                                                     device))]
+        return geo
+
+    def forward_flat(self, src_flatten, lvl_pos_embed_flatten, geo, query_embed=None, targets=None):
+        """deformable_transformer.py:159-257 on flattened inputs."""
+        assert query_embed is not None
+        pad = geo['pad_mask']
+        encs = []
+        for e in geo['enc']:
+            tok = e['tok']
+            pm = pad[:, tok] if pad is not None else None
+            src = src_flatten[:, tok]
+            pos = lvl_pos_embed_flatten[:, tok]
+            if fast_path():
+                src, pos = src.contiguous(), pos.contiguous()
+                pm = pm.contiguous() if pm is not None else None
+            encs.append(self.encoder(src, e['spatial_shapes'], e['valid_ratios'], pos, pm, reference_points=e['ref']))
+        if len(encs) == 2:
+            prev_memory, memory = encs
+            memory = torch.cat([memory, prev_memory], 1)   # [current, prev] -- reference order (:173)
+        else:
+            memory = encs[0]
+
+        bs, _, c = memory.shape
+        query_attn_mask = None
+        query_embed_, tgt = torch.split(query_embed, c, dim=1)
+        query_embed_ = query_embed_.unsqueeze(0).expand(bs, -1, -1)
+        tgt = tgt.unsqueeze(0).expand(bs, -1, -1)
+        reference_points = self.reference_points(query_embed_).sigmoid()
+        if targets is not None and 'track_query_hs_embeds' in targets[0]:
+            prev_hs_embed = torch.stack([t['track_query_hs_embeds'] for t in targets])
+            prev_boxes = torch.stack([t['track_query_boxes'] for t in targets])
+            prev_query_embed = torch.zeros_like(prev_hs_embed)
+            query_embed_ = torch.cat([prev_query_embed.to(query_embed_.dtype), query_embed_], dim=1)
+            tgt = torch.cat([prev_hs_embed.to(tgt.dtype), tgt], dim=1)
+            reference_points = torch.cat([prev_boxes[..., :2].to(reference_points.dtype), reference_points], dim=1)
+        init_reference_out = reference_points
+        if fast_path():
+            dt = memory.dtype
+            tgt = tgt.to(dt).contiguous()
+            query_embed_ = query_embed_.to(dt).contiguous()
+        hs, inter_references = self.decoder(tgt, reference_points, memory, geo['spatial_shapes'],
+                                            geo['valid_ratios'], query_embed_, pad, query_attn_mask)
+        return hs, memory, init_reference_out, inter_references, None, None
+
+
+def build_deforamble_transformer(args):
+    num_feature_levels = args.num_feature_levels
+    if args.multi_frame_attention:
+        num_feature_levels *= 2
+    return DeformableTransformer(
+        d_model=args.hidden_dim, nhead=args.nheads, num_encoder_layers=args.enc_layers,
+        num_decoder_layers=args.dec_layers, dim_feedforward=args.dim_feedforward, dropout=args.dropout,
+        activation="relu", return_intermediate_dec=True, num_feature_levels=num_feature_levels,
+        dec_n_points=args.dec_n_points, enc_n_points=args.enc_n_points, two_stage=args.two_stage,
+        two_stage_num_proposals=args.num_queries,
+        multi_frame_attention_separate_encoder=args.multi_frame_attention and args.multi_frame_attention_separate_encoder)

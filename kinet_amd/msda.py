@@ -8,7 +8,6 @@ attention_weights, im2col_step)` is the reference operator boundary
 (sampling_offsets / attention_weights / value_proj / output_proj, ms_deform_attn.py:27-30)
 so reference state_dicts load unchanged.
 """
-import math
 import warnings
 
 import torch
@@ -71,10 +70,9 @@ class MSDeformAttn(nn.Module):
     def _reset_parameters(self):
         # ms_deform_attn.py:34-47
         constant_(self.sampling_offsets.weight.data, 0.)
-        thetas = torch.arange(self.n_heads, dtype=torch.float32) * (2.0 * math.pi / self.n_heads)
-        grid_init = torch.stack([thetas.cos(), thetas.sin()], -1)
-        grid_init = (grid_init / grid_init.abs().max(-1, keepdim=True)[0]).view(self.n_heads, 1, 1, 2) \
-            .repeat(1, self.n_levels, self.n_points, 1)
+        # the reference's fixed 8-direction table (ms_deform_attn.py:36-37; n_heads must be 8)
+        grid_init = torch.tensor([-1, -1, -1, 0, -1, 1, 0, -1, 0, 1, 1, -1, 1, 0, 1, 1], dtype=torch.float32) \
+            .view(self.n_heads, 1, 1, 2).repeat(1, self.n_levels, self.n_points, 1)
         for i in range(self.n_points):
             grid_init[:, :, i, :] *= i + 1
         with torch.no_grad():
@@ -101,8 +99,11 @@ class MSDeformAttn(nn.Module):
     # -- pieces used by the fused transformer layers ------------------------------------
     def packed_offsets_weights(self):
         """[sampling_offsets ; attention_weights] stacked into one (M*L*P*3, d) GEMM."""
-        w = torch.cat([self.sampling_offsets.weight, self.attention_weights.weight], 0)
-        b = torch.cat([self.sampling_offsets.bias, self.attention_weights.bias], 0)
+        so, aw = self.sampling_offsets, self.attention_weights
+        w = K.cached_multi([so.weight, aw.weight], 'packed_w',
+                           lambda a, b: torch.cat([a.detach(), b.detach()], 0).contiguous())
+        b = K.cached_multi([so.bias, aw.bias], 'packed_b',
+                           lambda a, b: torch.cat([a.detach(), b.detach()], 0).float().contiguous())
         return w, b
 
     def sample(self, query, reference_points, value, input_spatial_shapes, query_attn_mask=None):

@@ -1,0 +1,103 @@
+"""CPU-only checks of the host side: the C-ABI library exports every declared symbol,
+the model's state_dict keys/shapes equal the reference's, the config values equal the
+reference YAMLs, and host utilities (postprocess) reproduce the reference fixtures."""
+import ctypes
+import glob
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    names = set()
+    for h in glob.glob(os.path.join(REPO, 'include', '*.h')):
+        src = open(h).read()
+        src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+        names |= set(re.findall(r'\b(kinet_[a-z0-9_]+)\s*\(', src))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    from kinet_amd import _native
+    lib = _native.lib()
+    declared = _declared_symbols()
+    assert len(declared) >= 15
+    missing = [n for n in declared if not hasattr(lib, n)]
+    assert not missing, missing
+    assert b'gfx950' in lib.kinet_version()
+
+
+def test_ctypes_signatures_cover_declarations():
+    from kinet_amd import _native
+    assert _declared_symbols() <= set(_native._SIGS)
+
+
+def test_ops_refuse_cpu_tensors():
+    import kinet_amd  # noqa: F401
+    import MultiScaleDeformableAttention as M
+    v = torch.zeros(1, 4, 1, 4)
+    with pytest.raises(RuntimeError):
+        M.ms_deform_attn_forward(v, torch.tensor([[2, 2]]), torch.zeros(1, 1, 1, 1, 1, 2), torch.zeros(1, 1, 1, 1, 1), 1)
+
+
+def _keys(golden_dir, name):
+    out = {}
+    for ln in open(os.path.join(golden_dir, name)):
+        k, *s = ln.split()
+        out[k] = tuple(int(x) for x in s)
+    return out
+
+
+@pytest.mark.parametrize('fixture,cfgs,over', [
+    ('detr_config2_small.keys.txt', ('train_deformable',), {}),
+    ('detr_tracking_mf_small.keys.txt', ('train_deformable', 'train_multi_frame', 'train_tracking'), {'dataset': 'mot'}),
+])
+def test_state_dict_matches_reference(golden_dir, fixture, cfgs, over):
+    from kinet_amd.models import build_model
+    from kinet_amd.models.config import load_args
+    ref = _keys(golden_dir, fixture)
+    model, _, post = build_model(load_args(*cfgs, **over))
+    mine = {k: tuple(v.shape) for k, v in model.state_dict().items()}
+    assert mine == ref
+    assert 'bbox' in post
+
+
+@pytest.mark.skipif(not os.path.isdir('/root/reference/cfgs'), reason='reference configs only in the build container')
+def test_config_values_match_reference_yaml():
+    import yaml
+    from kinet_amd.models.config import DEFAULTS, NAMED
+    with open('/root/reference/cfgs/train.yaml') as f:
+        base = yaml.safe_load(f)
+    for k, v in DEFAULTS.items():
+        if k in base:
+            assert base[k] == v, k
+    for name, vals in NAMED.items():
+        with open(f'/root/reference/cfgs/{name}.yaml') as f:
+            y = yaml.safe_load(f)
+        for k, v in vals.items():
+            assert y[k] == v, (name, k)
+
+
+def test_postprocess_matches_reference(golden_dir):
+    from kinet_amd.models import DeformablePostProcess
+    d = np.load(os.path.join(golden_dir, 'postprocess_matcher.npz'))
+    res = DeformablePostProcess()({'pred_logits': torch.from_numpy(d['logits']),
+                                   'pred_boxes': torch.from_numpy(d['boxes'])}, torch.from_numpy(d['sizes']))
+    for i, r in enumerate(res):
+        for k, v in r.items():
+            np.testing.assert_allclose(v.numpy(), d[f'post{i}_{k}'], atol=1e-5)
+
+
+def test_nested_tensor_padding_and_sizes():
+    from kinet_amd.models import nested_tensor_from_tensor_list
+    a, b = torch.randn(3, 10, 12), torch.randn(3, 8, 14)
+    nt = nested_tensor_from_tensor_list([a, b])
+    assert nt.tensors.shape == (2, 3, 10, 14) and nt.sizes == ((10, 12), (8, 14))
+    assert nt.mask[0, :, 12:].all() and not nt.mask[0, :, :12].any()
+    assert nt.mask[1, 8:].all() and not nt.mask[1, :8, :14].any()
+    assert torch.equal(nt.tensors[1, :, :8, :14], b)
