@@ -91,7 +91,8 @@ def cpu_baseline(seconds):
     on one frame's MSDA work of the same workload: 6 encoder calls (Lq = S = 22,223) and
     6 decoder calls (Lq = 300), fp32, all host threads."""
     from oracle.msda_oracle import core_pytorch
-    threads = os.cpu_count() or 1
+    # the box's CPU share (OMP_NUM_THREADS=16 there); os.cpu_count() reports the whole host
+    threads = int(os.environ.get('OMP_NUM_THREADS') or torch.get_num_threads() or 1)
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     shapes = torch.tensor([[100, 167], [50, 84], [25, 42], [13, 21]], dtype=torch.long)

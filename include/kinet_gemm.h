@@ -34,6 +34,17 @@ int kinet_gemm(const void* A, const void* B, void* C, int M, int N, int K,
                int relu, int out_dtype, const uint8_t* row_mask, int reserved,
                kinet_stream_t stream);
 
+/* Extended form: A2 (optional, same layout as A) is added to A at load time
+ * (q = src + pos feeding a projection, deformable_transformer.py:292, :369, :377);
+ * ln_gamma/ln_beta (optional, f32, N <= 320) apply LayerNorm(eps) over each output row
+ * after the bias + residual add -- the post-norm of a transformer sub-layer
+ * (deformable_transformer.py:287, :294, :364, :374, :380) fused into the GEMM epilogue. */
+int kinet_gemm_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K,
+                  int lda, int ldb, int ldc, int in_dtype,
+                  const float* scale, const float* bias, const void* R, int ldr, int relu,
+                  const float* ln_gamma, const float* ln_beta, float ln_eps,
+                  int out_dtype, const uint8_t* row_mask, kinet_stream_t stream);
+
 /* Convolution, NHWC activations, weights (Cout, KH, KW, Cin) = PyTorch OIHW permuted.
  *   X (batch, Hin, Win, Cin) with Cin % 8 == 0 (pad channels with zeros otherwise)
  *   Y (batch, Hout, Wout, Cout) written with row stride ldy (>= Cout) so outputs can land

@@ -66,9 +66,11 @@ int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num
  *   offsets_logits  (N, Lq, ld_off) f32 rows holding [M*L*P*2 offsets | M*L*P logits]
  *                   (the concatenated sampling_offsets/attention_weights projection)
  *   ref_points      (N, Lq, L, ref_dim) f32, ref_dim in {2, 4}
+ *   value_ld        row stride of `value` in elements (0 = M*D): lets the six decoder
+ *                   layers read column slices of ONE batched value projection
  * Writes output (N, Lq, M*D) and, when loc_out/attw_out are non-NULL, the f32
  * sampling_loc / attn_weight tensors (needed to run kinet_msda_backward). */
-int kinet_msda_fused_forward(const void* value, const int64_t* spatial_shapes,
+int kinet_msda_fused_forward(const void* value, int value_ld, const int64_t* spatial_shapes,
                              const void* offsets_logits, int ld_off,
                              const float* ref_points, int ref_dim,
                              const uint8_t* query_attn_mask,

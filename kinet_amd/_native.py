@@ -22,8 +22,9 @@ _SIGS = {
     'kinet_msda_forward': [P, P, P, P, P] + [I] * 10 + [P],
     'kinet_msda_backward': [P] * 9 + [I] * 10 + [P],
     'kinet_msda_backward_workspace_bytes': [I] * 5,
-    'kinet_msda_fused_forward': [P, P, P, I, P, I, P, P, P, P] + [I] * 8 + [P],
+    'kinet_msda_fused_forward': [P, I, P, P, I, P, I, P, P, P, P] + [I] * 8 + [P],
     'kinet_gemm': [P, P, P] + [I] * 7 + [P, P, P, I, I, I, P, I, P],
+    'kinet_gemm_ex': [P, P, P, P] + [I] * 7 + [P, P, P, I, I, P, P, F, I, P, P],
     'kinet_conv2d': [P, P, P] + [I] * 12 + [P, P, P, I, I, I, P],
     'kinet_layernorm': [P] * 5 + [I, I, F, I, I, P],
     'kinet_groupnorm': [P] * 4 + [I] * 5 + [F, I, P, P],

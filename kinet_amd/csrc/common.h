@@ -46,13 +46,11 @@ __device__ __forceinline__ float to_f32(double v) { return (float)v; }
 __device__ __forceinline__ float to_f32(f16_t v) { return (float)v; }
 __device__ __forceinline__ float to_f32(bf16_t v) { return __uint_as_float(((uint32_t)v.x) << 16); }
 
-// round-to-nearest-even; NaN stays NaN (MI355X_MICROARCH "Correctness boundaries")
+// round-to-nearest-even, NaN stays NaN: a plain __bf16 cast lowers to v_cvt_pk_bf16_f32
+// (MI355X_MICROARCH "Correctness boundaries"), branch-free.
 __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
-    uint32_t u = __float_as_uint(f);
     bf16_t r;
-    if ((u & 0x7fffffffu) > 0x7f800000u) { r.x = (uint16_t)((u >> 16) | 0x40); return r; }
-    u += 0x7fffu + ((u >> 16) & 1u);
-    r.x = (uint16_t)(u >> 16);
+    r.x = __builtin_bit_cast(uint16_t, (__bf16)f);
     return r;
 }
 

@@ -1,20 +1,26 @@
 // MFMA GEMM + implicit-GEMM NHWC convolution for gfx950 (CDNA4), fused epilogues.
 //
 // Tiling (DESIGN.md "GEMM / conv kernel"):
-//  * workgroup = 256 threads = 4 waves in a 2 (M) x 2 (N) grid, output tile BM x BN
-//    (128/64 each), one K-step = 128 bytes of K per row (64 bf16/f16 or 32 f32);
+//  * workgroup = 256 threads = 4 waves in a WGM x WGN grid, output tile BM x BN, one
+//    K-step = 128 bytes of K per row (64 bf16/f16 or 32 f32);
 //  * operands staged global -> registers -> LDS, double-buffered LDS with ONE barrier
-//    per K-step (next tile's global loads are in flight under the current MFMAs);
+//    per K-step (the next tile's global loads are in flight under the current MFMAs);
 //  * LDS rows are 128 B with the 16-byte chunk index XOR-swizzled by (row & 7), which
 //    makes the ds_read_b128 fragment reads (16 rows x one chunk per lane group)
 //    bank-conflict free;
-//  * the weight tile is the MFMA A operand and the activation tile the B operand, so
-//    the 16x16 accumulator has the output row m on the lane and 4 consecutive output
-//    channels n in registers -> 8/16-byte stores along the contiguous NHWC channel dim;
+//  * bf16/f16: v_mfma_f32_16x16x32_{bf16,f16}; f32 (parity mode): the exact-f32
+//    v_mfma_f32_16x16x4_f32, 4 per 16-byte fragment;
+//  * epilogue through LDS: the f32 accumulator tile is parked in the (now idle) staging
+//    buffers, then each wave streams whole output rows -- 16-byte residual loads and
+//    8/16-byte stores per lane, every row written by consecutive lanes (the direct
+//    MFMA-layout store writes 32-byte pieces of 16 rows per instruction);  bias / folded
+//    BatchNorm scale, residual add, ReLU, padding-row mask and, when one tile spans the
+//    whole row (N <= BN), the post-norm LayerNorm (deformable_transformer.py:287 etc.)
+//    are applied there, so the sub-layer output is written exactly once;
+//  * optional second A operand added at load time (q = src + pos, deformable_transformer.py:
+//    292, :369, :377) -- the bf16 sum is rounded exactly as a separate add would;
 //  * blockIdx is remapped XCD-aware (bijective form, cdna_hip_programming.md T1) so the
 //    tiles that share an activation panel run on one XCD and hit its L2;
-//  * bf16/f16: v_mfma_f32_16x16x32_{bf16,f16}; f32 (parity mode): the exact-f32
-//    v_mfma_f32_16x16x4_f32, 4 per 16-byte fragment.
 //  * implicit conv: M = batch*Hout*Wout rows, K = KH*KW*Cin with Cin fastest (weights
 //    permuted OIHW -> OHWI on the host); each 16-byte chunk lies inside one filter tap
 //    (Cin % 8 == 0) so the im2col gather is a 16-byte load or a zero fill.
@@ -35,12 +41,17 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct GemmArgs {
     const void* A;
+    const void* A2;        // optional: A + A2 elementwise (same layout as A)
     const void* B;
     void* C;
     const void* R;
     const float* scale;
     const float* bias;
+    const float* ln_g;     // LayerNorm over the row (requires N <= BN)
+    const float* ln_b;
     const uint8_t* row_mask;
+    float ln_eps;
+    int a_bytes, b_bytes;   // buffer-descriptor extents (bytes, < 2^31)
     int M, N, K, lda, ldb, ldc, ldr, relu;
     int Hin, Win, Cin, Hout, Wout, KW, stride, pad;
 };
@@ -51,11 +62,24 @@ template <> struct Mma<bf16_t> {
     __device__ __forceinline__ static void run(f32x4& c, const u32x4& a, const u32x4& b) {
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
     }
+    __device__ __forceinline__ static u32x4 add(const u32x4& x, const u32x4& y) {
+        u32x4 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float lo = __uint_as_float(x[i] << 16) + __uint_as_float(y[i] << 16);
+            const float hi = __uint_as_float(x[i] & 0xffff0000u) + __uint_as_float(y[i] & 0xffff0000u);
+            r[i] = (uint32_t)f32_to_bf16(lo).x | ((uint32_t)f32_to_bf16(hi).x << 16);
+        }
+        return r;
+    }
 };
 template <> struct Mma<f16_t> {
     static constexpr int EPC = 8;
     __device__ __forceinline__ static void run(f32x4& c, const u32x4& a, const u32x4& b) {
         c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+    }
+    __device__ __forceinline__ static u32x4 add(const u32x4& x, const u32x4& y) {
+        return __builtin_bit_cast(u32x4, __builtin_bit_cast(f16x8, x) + __builtin_bit_cast(f16x8, y));
     }
 };
 template <> struct Mma<float> {
@@ -67,60 +91,74 @@ template <> struct Mma<float> {
         for (int j = 0; j < 4; ++j)
             c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[j]), __uint_as_float(b[j]), c, 0, 0, 0);
     }
+    __device__ __forceinline__ static u32x4 add(const u32x4& x, const u32x4& y) {
+        return __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, x) + __builtin_bit_cast(f32x4, y));
+    }
 };
 
-template <typename TO> struct Store4;
-template <> struct Store4<float> {
-    __device__ static void vec(float* p, const float* v) { *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]}; }
-    __device__ static void one(float* p, float v) { *p = v; }
+template <typename TO> struct IO4;
+template <> struct IO4<float> {
+    __device__ static void store(float* p, const float* v) { *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]}; }
     __device__ static void load(const float* p, float* v) {
         const f32x4 x = *reinterpret_cast<const f32x4*>(p);
         v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
     }
+    __device__ static void store1(float* p, float v) { *p = v; }
+    __device__ static float load1(const float* p) { return *p; }
 };
-template <> struct Store4<bf16_t> {
-    __device__ static void vec(bf16_t* p, const float* v) {
+template <> struct IO4<bf16_t> {
+    __device__ static void store(bf16_t* p, const float* v) {
         uint2 u;
         u.x = (uint32_t)f32_to_bf16(v[0]).x | ((uint32_t)f32_to_bf16(v[1]).x << 16);
         u.y = (uint32_t)f32_to_bf16(v[2]).x | ((uint32_t)f32_to_bf16(v[3]).x << 16);
         *reinterpret_cast<uint2*>(p) = u;
     }
-    __device__ static void one(bf16_t* p, float v) { *p = f32_to_bf16(v); }
     __device__ static void load(const bf16_t* p, float* v) {
         const uint2 u = *reinterpret_cast<const uint2*>(p);
         v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
         v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
     }
+    __device__ static void store1(bf16_t* p, float v) { *p = f32_to_bf16(v); }
+    __device__ static float load1(const bf16_t* p) { return to_f32(*p); }
 };
-template <> struct Store4<f16_t> {
-    __device__ static void vec(f16_t* p, const float* v) {
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+template <> struct IO4<f16_t> {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    __device__ static void store(f16_t* p, const float* v) {
         *reinterpret_cast<h4*>(p) = h4{(f16_t)v[0], (f16_t)v[1], (f16_t)v[2], (f16_t)v[3]};
     }
-    __device__ static void one(f16_t* p, float v) { *p = (f16_t)v; }
     __device__ static void load(const f16_t* p, float* v) {
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         const h4 x = *reinterpret_cast<const h4*>(p);
         v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
     }
+    __device__ static void store1(f16_t* p, float v) { *p = (f16_t)v; }
+    __device__ static float load1(const f16_t* p) { return (float)*p; }
 };
 
 constexpr int ROWB = 128;   // bytes of K per LDS row per K-step
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ (r & 7)) << 4); }
 
-template <typename T, typename TO, int BM, int BN, bool CONV>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const int nNt) {
+template <int BM, int BN>
+struct Smem {
+    static constexpr int STAGE = (BM + BN) * ROWB;
+    static constexpr int EPI_LD = BN + 4;                 // f32 row stride of the epilogue tile
+    static constexpr int EPI = BM * EPI_LD * 4;
+    static constexpr int BYTES = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+};
+
+template <typename T, typename TO, int BM, int BN, int WGM, int WGN, bool CONV, bool LN>
+__global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p, const int nNt) {
+    static_assert(WGM * WGN == 4, "4 waves");
     constexpr int EPC = Mma<T>::EPC;
     constexpr int BK = ROWB / (int)sizeof(T);
-    constexpr int XR = BM / 32;
-    constexpr int WR = BN / 32;
-    constexpr int TM = BM / 32;
-    constexpr int TN = BN / 32;
-    constexpr int STAGE = (BM + BN) * ROWB;
-    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+    constexpr int XR = BM / 32;                 // 16-byte staging chunks per thread (A)
+    constexpr int WR = BN / 32;                 // (B)
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;   // wave tile
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int STAGE = Smem<BM, BN>::STAGE;
+    constexpr int EPI_LD = Smem<BM, BN>::EPI_LD;
+    __shared__ __attribute__((aligned(16))) char lds[Smem<BM, BN>::BYTES];
 
-    // XCD-aware bijective remap: consecutive logical tiles land on one XCD
     int bid = blockIdx.x;
     {
         const int nblk = gridDim.x, q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
@@ -130,14 +168,23 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
     const int m0 = mt * BM, n0 = nt * BN;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
-    const int wm = wave & 1, wn = wave >> 1;
+    const int wm = wave % WGM, wn = wave / WGM;
     const int sc = tid & 7, sr = tid >> 3;
     const int M = p.M, N = p.N, K = p.K;
 
-    const T* __restrict__ A = (const T*)p.A;
-    const T* __restrict__ B = (const T*)p.B;
+    // Buffer descriptors over the whole operands (kernel arguments -> wave-uniform SGPRs).
+    // A lane that must contribute zeros (row/col past the edge, K tail, conv padding)
+    // gets an offset past num_records: the hardware range check returns 0, so the
+    // staging loads are branch-free and all stay in flight (a `cond ? load : 0` compiles
+    // to a branch + vmcnt(0) per load, cdna_hip_programming.md §5 item 4(c)).
+    constexpr unsigned OOB = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra2 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(p.A2 ? p.A2 : p.A), (short)0, p.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
+    const bool has_a2 = p.A2 != nullptr;
 
-    long xbase[XR];
+    unsigned xbase[XR];
     int xih[XR], xiw[XR];
     bool xok[XR];
 #pragma unroll
@@ -151,15 +198,22 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
             const int oh = rem / p.Wout, ow = rem - (rem / p.Wout) * p.Wout;
             xih[i] = oh * p.stride - p.pad;
             xiw[i] = ow * p.stride - p.pad;
-            xbase[i] = (long)img * p.Hin * p.Win * p.Cin;
+            xbase[i] = (unsigned)img * (unsigned)(p.Hin * p.Win * p.Cin);
         } else {
             xih[i] = xiw[i] = 0;
-            xbase[i] = (long)m * p.lda;
+            xbase[i] = (unsigned)m * (unsigned)p.lda;
         }
+    }
+    unsigned wbase[WR];
+    bool wok[WR];
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+        const int n = n0 + sr + 32 * i;
+        wok[i] = n < N;
+        wbase[i] = (unsigned)n * (unsigned)p.ldb;
     }
 
     u32x4 xs[XR], ws[WR];
-    const u32x4 zero = {0u, 0u, 0u, 0u};
 
     auto load_tile = [&](int k0) {
         const int k = k0 + sc * EPC;
@@ -174,20 +228,22 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
 #pragma unroll
         for (int i = 0; i < XR; ++i) {
             bool ok = xok[i] && kok;
-            const T* src;
+            unsigned off;
             if (CONV) {
                 const int ih = xih[i] + kh, iw = xiw[i] + kw;
                 ok = ok && ih >= 0 && ih < p.Hin && iw >= 0 && iw < p.Win;
-                src = A + xbase[i] + ((long)ih * p.Win + iw) * p.Cin + cc;
+                off = xbase[i] + (unsigned)((ih * p.Win + iw) * p.Cin + cc);
             } else {
-                src = A + xbase[i] + k;
+                off = xbase[i] + (unsigned)k;
             }
-            xs[i] = ok ? *reinterpret_cast<const u32x4*>(src) : zero;
+            const unsigned boff = ok ? off * (unsigned)sizeof(T) : OOB;
+            xs[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, boff, 0, 0);
+            if (!CONV && has_a2) xs[i] = Mma<T>::add(xs[i], __builtin_amdgcn_raw_buffer_load_b128(ra2, boff, 0, 0));
         }
 #pragma unroll
         for (int i = 0; i < WR; ++i) {
-            const int n = n0 + sr + 32 * i;
-            ws[i] = (n < N && kok) ? *reinterpret_cast<const u32x4*>(B + (long)n * p.ldb + k) : zero;
+            const unsigned boff = (wok[i] && kok) ? (wbase[i] + (unsigned)k) * (unsigned)sizeof(T) : OOB;
+            ws[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, boff, 0, 0);
         }
     };
     auto store_tile = [&](int buf) {
@@ -220,10 +276,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
             u32x4 bfr[TM], afr[TN];
 #pragma unroll
             for (int t = 0; t < TM; ++t)
-                bfr[t] = *reinterpret_cast<const u32x4*>(xl + swz(wm * (BM / 2) + t * 16 + (lane & 15), ch));
+                bfr[t] = *reinterpret_cast<const u32x4*>(xl + swz(wm * WTM + t * 16 + (lane & 15), ch));
 #pragma unroll
             for (int t = 0; t < TN; ++t)
-                afr[t] = *reinterpret_cast<const u32x4*>(wl + swz(wn * (BN / 2) + t * 16 + (lane & 15), ch));
+                afr[t] = *reinterpret_cast<const u32x4*>(wl + swz(wn * WTN + t * 16 + (lane & 15), ch));
 #pragma unroll
             for (int a = 0; a < TN; ++a)
 #pragma unroll
@@ -233,44 +289,101 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
         __syncthreads();
     }
 
-    // ---- epilogue: scale/bias (folded BN or Linear bias), residual, ReLU, row mask ----
+    // ---- epilogue: park the f32 tile in LDS (row m, col n), then stream whole rows ----
+    float* ep = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) {
+            const int ml = wm * WTM + b * 16 + (lane & 15);
+            const int nl = wn * WTN + a * 16 + (lane >> 4) * 4;
+            *reinterpret_cast<f32x4*>(ep + ml * EPI_LD + nl) = acc[a][b];
+        }
+    __syncthreads();
+
+    constexpr int LPR = BN / 4 < 64 ? BN / 4 : 64;   // lanes per row
+    constexpr int NCH = (BN + 4 * LPR - 1) / (4 * LPR);   // 4-column chunks per lane
+    constexpr int RPW = 64 / LPR;                     // rows per wave pass
+    static_assert(64 % LPR == 0, "row mapping");
     TO* __restrict__ C = (TO*)p.C;
     const TO* __restrict__ R = (const TO*)p.R;
-    const bool vec_ok = ((p.ldc & 3) == 0) && (R == nullptr || (p.ldr & 3) == 0);
+    const int lr = lane / LPR, lc = lane - (lane / LPR) * LPR;
+    const bool ld_ok = ((p.ldc & 3) == 0) && (R == nullptr || (p.ldr & 3) == 0);
+    float sc4[NCH][4], bi4[NCH][4], g4[NCH][4], be4[NCH][4];
 #pragma unroll
-    for (int b = 0; b < TM; ++b) {
-        const int m = m0 + wm * (BM / 2) + b * 16 + (lane & 15);
-        if (m >= M) continue;
-        const bool masked = p.row_mask != nullptr && p.row_mask[m] != 0;
+    for (int c = 0; c < NCH; ++c)
 #pragma unroll
-        for (int a = 0; a < TN; ++a) {
-            const int nb = n0 + wn * (BN / 2) + a * 16 + (lane >> 4) * 4;
-            if (nb >= N) continue;
-            float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
-            const bool full = vec_ok && nb + 3 < N;
+        for (int r = 0; r < 4; ++r) {
+            int nn = n0 + (c * LPR + lc) * 4 + r;
+            nn = nn < N ? nn : N - 1;
+            sc4[c][r] = p.scale ? p.scale[nn] : 1.f;
+            bi4[c][r] = p.bias ? p.bias[nn] : 0.f;
+            g4[c][r] = LN ? p.ln_g[nn] : 1.f;
+            be4[c][r] = LN ? p.ln_b[nn] : 0.f;
+        }
+    for (int rr = wave * RPW + lr; rr < BM; rr += 4 * RPW) {
+        const int m = m0 + rr;
+        // (LN needs every lane of the row in the reductions, so no early exit on m)
+        const bool mok = m < M;
+        float v[NCH][4];
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int nl0 = (c * LPR + lc) * 4;
+            const int n = n0 + nl0;
+            const bool cin = nl0 < BN;
+            f32x4 t = {0.f, 0.f, 0.f, 0.f};
+            if (cin) t = *reinterpret_cast<const f32x4*>(ep + rr * EPI_LD + nl0);
             float res[4] = {0.f, 0.f, 0.f, 0.f};
-            if (R) {
-                if (full) Store4<TO>::load(R + (long)m * p.ldr + nb, res);
+            if (R && mok && cin && n < N) {
+                if (ld_ok && n + 3 < N) IO4<TO>::load(R + (long)m * p.ldr + n, res);
                 else
                     for (int r = 0; r < 4; ++r)
-                        if (nb + r < N) res[r] = to_f32(R[(long)m * p.ldr + nb + r]);
+                        if (n + r < N) res[r] = IO4<TO>::load1(R + (long)m * p.ldr + n + r);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int n = nb + r < N ? nb + r : N - 1;
-                float x = v[r];
-                if (p.scale) x *= p.scale[n];
-                if (p.bias) x += p.bias[n];
-                x += res[r];
+                float x = t[r] * sc4[c][r] + bi4[c][r] + res[r];
                 if (p.relu) x = fmaxf(x, 0.f);
-                if (masked) x = 0.f;
-                v[r] = x;
+                x = (cin && n + r < N) ? x : 0.f;
+                v[c][r] = x;
+                s += x;
             }
-            TO* dst = C + (long)m * p.ldc + nb;
-            if (full) Store4<TO>::vec(dst, v);
+        }
+        if (LN) {
+#pragma unroll
+            for (int o = LPR >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            const float mean = s / (float)N;
+            float q = 0.f;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = n0 + (c * LPR + lc) * 4 + r;
+                    const float d = ((c * LPR + lc) * 4 < BN && n < N) ? v[c][r] - mean : 0.f;
+                    q += d * d;
+                }
+#pragma unroll
+            for (int o = LPR >> 1; o > 0; o >>= 1) q += __shfl_xor(q, o);
+            const float rstd = rsqrtf(q / (float)N + p.ln_eps);
+#pragma unroll
+            for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[c][r] = (v[c][r] - mean) * rstd * g4[c][r] + be4[c][r];
+        }
+        if (!mok) continue;
+        const bool masked = p.row_mask && p.row_mask[m];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int nl0 = (c * LPR + lc) * 4;
+            const int n = n0 + nl0;
+            if (nl0 >= BN || n >= N) continue;
+            if (masked) v[c][0] = v[c][1] = v[c][2] = v[c][3] = 0.f;
+            TO* dst = C + (long)m * p.ldc + n;
+            if (ld_ok && n + 3 < N) IO4<TO>::store(dst, v[c]);
             else
                 for (int r = 0; r < 4; ++r)
-                    if (nb + r < N) Store4<TO>::one(dst + r, v[r]);
+                    if (n + r < N) IO4<TO>::store1(dst + r, v[c][r]);
         }
     }
 }
@@ -278,18 +391,30 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
 template <typename T, typename TO, bool CONV>
 int launch(const GemmArgs& a, hipStream_t stream) {
     if (a.M == 0 || a.N == 0) return KINET_OK;
-    const int bn = a.N <= 64 ? 64 : 128;
-    const long tiles128 = (long)((a.M + 127) / 128) * ((a.N + bn - 1) / bn);
-    const int bm = tiles128 < 512 ? 64 : 128;
+    const bool ln = a.ln_g != nullptr;
+    int bm, bn;
+    if (ln) {
+        KINET_CHECK_ARG(a.N <= 320, "gemm: fused LayerNorm needs N <= 320 (got %d)", a.N);
+        bm = 64;
+        bn = a.N <= 256 ? 256 : 320;
+    } else {
+        bn = a.N <= 64 ? 64 : 128;
+        const long tiles128 = (long)((a.M + 127) / 128) * ((a.N + bn - 1) / bn);
+        bm = tiles128 < 512 ? 64 : 128;
+    }
     const int nMt = (a.M + bm - 1) / bm, nNt = (a.N + bn - 1) / bn;
     const long nblk = (long)nMt * nNt;
     KINET_CHECK_ARG(nblk < (1L << 31), "gemm: too many tiles");
     dim3 grid((unsigned)nblk), block(256);
-#define L_(BM_, BN_) hipLaunchKernelGGL((gemm_kernel<T, TO, BM_, BN_, CONV>), grid, block, 0, stream, a, nNt)
-    if (bm == 128 && bn == 128) L_(128, 128);
-    else if (bm == 128 && bn == 64) L_(128, 64);
-    else if (bm == 64 && bn == 128) L_(64, 128);
-    else L_(64, 64);
+#define L_(BM_, BN_, WM_, WN_, LN_) \
+    hipLaunchKernelGGL((gemm_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0, stream, a, nNt)
+    if (ln) {
+        if (bn == 256) L_(64, 256, 1, 4, true);
+        else L_(64, 320, 1, 4, true);
+    } else if (bm == 128 && bn == 128) L_(128, 128, 2, 2, false);
+    else if (bm == 128 && bn == 64) L_(128, 64, 2, 2, false);
+    else if (bm == 64 && bn == 128) L_(64, 128, 2, 2, false);
+    else L_(64, 64, 2, 2, false);
 #undef L_
     KINET_LAUNCH_CHECK();
     return KINET_OK;
@@ -313,19 +438,36 @@ bool aligned16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
 
 using namespace kinet;
 
+extern "C" int kinet_gemm_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K, int lda,
+                             int ldb, int ldc, int in_dtype, const float* scale, const float* bias, const void* R,
+                             int ldr, int relu, const float* ln_gamma, const float* ln_beta, float ln_eps,
+                             int out_dtype, const uint8_t* row_mask, kinet_stream_t stream) {
+    KINET_CHECK_ARG(M >= 0 && N >= 0 && K > 0, "gemm: invalid sizes M=%d N=%d K=%d", M, N, K);
+    KINET_CHECK_ARG(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "gemm: K, lda, ldb must be multiples of 8 (K=%d lda=%d ldb=%d)", K, lda, ldb);
+    KINET_CHECK_ARG(lda >= K && ldb >= K && ldc >= N, "gemm: leading dims too small");
+    KINET_CHECK_ARG(aligned16(A) && aligned16(B) && (A2 == nullptr || aligned16(A2)), "gemm: A, A2 and B must be 16-byte aligned");
+    KINET_CHECK_ARG(R == nullptr || ldr >= N, "gemm: ldr < N");
+    KINET_CHECK_ARG((ln_gamma == nullptr) == (ln_beta == nullptr), "gemm: LayerNorm needs both gamma and beta");
+    KINET_CHECK_ARG(ln_gamma == nullptr || relu == 0, "gemm: LayerNorm and ReLU are exclusive");
+    GemmArgs a{};
+    a.A = A; a.A2 = A2; a.B = B; a.C = C; a.R = R; a.scale = scale; a.bias = bias; a.row_mask = row_mask;
+    a.ln_g = ln_gamma; a.ln_b = ln_beta; a.ln_eps = ln_eps;
+    a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldr = ldr; a.relu = relu;
+    const long long es = (long long)dtype_size(in_dtype);
+    const long long ab = M > 0 ? ((long long)(M - 1) * lda + K) * es : 0;
+    const long long bb = N > 0 ? ((long long)(N - 1) * ldb + K) * es : 0;
+    KINET_CHECK_ARG(ab < (1LL << 31) && bb < (1LL << 31), "gemm: operand larger than 2 GiB (split the call)");
+    a.a_bytes = (int)ab;
+    a.b_bytes = (int)bb;
+    return dispatch<false>(a, in_dtype, out_dtype, (hipStream_t)stream);
+}
+
 extern "C" int kinet_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                           int in_dtype, const float* scale, const float* bias, const void* R, int ldr, int relu,
                           int out_dtype, const uint8_t* row_mask, int reserved, kinet_stream_t stream) {
     (void)reserved;
-    KINET_CHECK_ARG(M >= 0 && N >= 0 && K > 0, "gemm: invalid sizes M=%d N=%d K=%d", M, N, K);
-    KINET_CHECK_ARG(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "gemm: K, lda, ldb must be multiples of 8 (K=%d lda=%d ldb=%d)", K, lda, ldb);
-    KINET_CHECK_ARG(lda >= K && ldb >= K && ldc >= N, "gemm: leading dims too small");
-    KINET_CHECK_ARG(aligned16(A) && aligned16(B), "gemm: A and B must be 16-byte aligned");
-    KINET_CHECK_ARG(R == nullptr || ldr >= N, "gemm: ldr < N");
-    GemmArgs a{};
-    a.A = A; a.B = B; a.C = C; a.R = R; a.scale = scale; a.bias = bias; a.row_mask = row_mask;
-    a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldr = ldr; a.relu = relu;
-    return dispatch<false>(a, in_dtype, out_dtype, (hipStream_t)stream);
+    return kinet_gemm_ex(A, nullptr, B, C, M, N, K, lda, ldb, ldc, in_dtype, scale, bias, R, ldr, relu, nullptr,
+                         nullptr, 0.f, out_dtype, row_mask, stream);
 }
 
 extern "C" int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin, int Hout,
@@ -345,5 +487,11 @@ extern "C" int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, i
     a.M = (int)M; a.N = Cout; a.K = KH * KW * Cin; a.lda = 0; a.ldb = KH * KW * Cin; a.ldc = ldy; a.ldr = ldr;
     a.relu = relu;
     a.Hin = Hin; a.Win = Win; a.Cin = Cin; a.Hout = Hout; a.Wout = Wout; a.KW = KW; a.stride = stride; a.pad = pad;
+    const long long es = (long long)dtype_size(in_dtype);
+    const long long ab = (long long)batch * Hin * Win * Cin * es;
+    const long long bb = (long long)Cout * KH * KW * Cin * es;
+    KINET_CHECK_ARG(ab < (1LL << 31) && bb < (1LL << 31), "conv2d: operand larger than 2 GiB (split the batch)");
+    a.a_bytes = (int)ab;
+    a.b_bytes = (int)bb;
     return dispatch<true>(a, in_dtype, in_dtype, (hipStream_t)stream);
 }

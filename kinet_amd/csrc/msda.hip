@@ -110,7 +110,7 @@ __global__ __launch_bounds__(kThreads) void msda_fwd_kernel(
     const TL* __restrict__ loc, const TL* __restrict__ attw,
     const float* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
     const uint8_t* __restrict__ qmask, float* __restrict__ loc_out, float* __restrict__ attw_out,
-    T* __restrict__ out, int S, int M, int D, int L, int Lq, int P, int QT, int LPQ) {
+    T* __restrict__ out, int S, int M, int D, int L, int Lq, int P, int QT, int LPQ, int VLD) {
     using Acc = typename Acc<T>::type;
     using TapT = typename std::conditional<sizeof(Acc) == 8, Tap4d, Tap4>::type;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(kThreads) void msda_fwd_kernel(
     const int b = blockIdx.y;
     const int q0 = blockIdx.x * QT;
     const int LP = L * P;
-    const int MD = M * D;
+    const int MD = VLD;   // value row stride (elements); == M*D unless the value is a column slice
     load_levels(li, shapes, L, S);
     __syncthreads();
 
@@ -164,9 +164,59 @@ __global__ __launch_bounds__(kThreads) void msda_fwd_kernel(
             }
             taps[s] = t;
         }
+    } else if ((LP & (LP - 1)) == 0 && LP <= 64) {
+        // fused module path (ms_deform_attn.py:69-82), L*P a power of two <= 64: the L*P
+        // samples of one (query, head) are LP consecutive lanes, so the softmax max / sum are
+        // wave shuffles (the loop bound is rounded up to whole waves for the shuffles).
+        const int nsamp_r = (nsamp + 63) & ~63;
+        for (int s = threadIdx.x; s < nsamp_r; s += kThreads) {
+            const bool sv = s < nsamp;
+            const int qi = s / (M * LP);
+            const int q = q0 + qi;
+            const int rem = s - qi * (M * LP);
+            const int m = rem / LP;
+            const int lp = rem - m * LP;
+            const int l = lp / P;
+            const bool ok = sv && q < Lq;
+            const float* orow = offlog + ((long)b * Lq + (ok ? q : 0)) * ld_off;
+            const float logit = ok ? orow[(long)M * LP * 2 + rem] : -INFINITY;
+            float mx = logit;
+            for (int o = LP >> 1; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            const float e = ok ? __expf(logit - mx) : 0.f;
+            float sum = e;
+            for (int o = LP >> 1; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+            if (!sv) continue;
+            Tap4 t4;
+            if (ok) {
+                float a = e / sum;
+                if (qmask && qmask[(long)b * Lq + q]) a = 0.f;
+                const float2 o2 = *reinterpret_cast<const float2*>(orow + (long)rem * 2);
+                const float* rp = ref + (((long)b * Lq + q) * L + l) * ref_dim;
+                float x, y;
+                if (ref_dim == 2) {
+                    // quirk kept for parity: offsets / spatial_shapes[(H, W)] applied to (x, y)
+                    x = rp[0] + o2.x / (float)li.H[l];
+                    y = rp[1] + o2.y / (float)li.W[l];
+                } else {
+                    x = rp[0] + o2.x / (float)P * rp[2] * 0.5f;
+                    y = rp[1] + o2.y / (float)P * rp[3] * 0.5f;
+                }
+                if (loc_out) {
+                    const long gi = ((long)b * Lq + q) * M * LP + rem;
+                    loc_out[2 * gi] = x;
+                    loc_out[2 * gi + 1] = y;
+                    attw_out[gi] = a;
+                }
+                setup_sample<T, float>(t4, x, y, a, li, l, MD, m, D);
+            } else {
+                for (int k = 0; k < 4; ++k) { t4.off[k] = 0; t4.w[k] = 0.f; }
+            }
+            TapT t;
+            for (int k = 0; k < 4; ++k) { t.off[k] = t4.off[k]; t.w[k] = t4.w[k]; }
+            taps[s] = t;
+        }
     } else {
-        // fused module path (ms_deform_attn.py:69-82): logits -> softmax over L*P, offsets
-        // -> locations.  Logits go through LDS (reusing the weight slots) for the softmax.
+        // fused path, general L*P: logits go through LDS for the softmax.
         float* lg = reinterpret_cast<float*>(taps + nsamp);   // nsamp floats after the taps
         for (int s = threadIdx.x; s < nsamp; s += kThreads) {
             const int qi = s / (M * LP);
@@ -235,8 +285,28 @@ __global__ __launch_bounds__(kThreads) void msda_fwd_kernel(
     Acc acc[VEC];
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] = 0;
-#pragma unroll 4
-    for (int s = 0; s < LP; ++s) {
+    // Gather in groups of SG samples: all 4*SG tap loads of a group are issued before any
+    // is consumed, so 16 independent 16-byte gathers per lane are in flight (left to
+    // itself hipcc interleaves 2-4 loads with vmcnt(0) waits: latency-bound).
+    constexpr int SG = 4;
+    int s = 0;
+    for (; s + SG <= LP; s += SG) {
+        TapT t[SG];
+#pragma unroll
+        for (int g2 = 0; g2 < SG; ++g2) t[g2] = tp[s + g2];
+        VecT<T, VEC> v[SG][4];
+#pragma unroll
+        for (int g2 = 0; g2 < SG; ++g2)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[g2][k] = *reinterpret_cast<const VecT<T, VEC>*>(vb + t[g2].off[k]);
+#pragma unroll
+        for (int g2 = 0; g2 < SG; ++g2)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) acc[j] += (Acc)t[g2].w[k] * to_acc(v[g2][k].v[j], (Acc*)nullptr);
+    }
+    for (; s < LP; ++s) {
         const TapT t = tp[s];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -248,7 +318,7 @@ __global__ __launch_bounds__(kThreads) void msda_fwd_kernel(
     VecT<T, VEC> o;
 #pragma unroll
     for (int j = 0; j < VEC; ++j) o.v[j] = Cvt<T>::from(acc[j]);
-    *reinterpret_cast<VecT<T, VEC>*>(out + ((long)b * Lq + q) * MD + (long)m * D + c0) = o;
+    *reinterpret_cast<VecT<T, VEC>*>(out + ((long)b * Lq + q) * M * D + (long)m * D + c0) = o;
 }
 
 // ---------------------------------------------------------------------------------
@@ -445,9 +515,12 @@ template <typename T, typename TL, int FUSED>
 int launch_fwd(const void* value, const int64_t* shapes, const void* loc, const void* attw,
                const void* offlog, int ld_off, const float* ref, int ref_dim, const uint8_t* qmask,
                float* loc_out, float* attw_out, void* out, int N, int S, int M, int D, int L, int Lq,
-               int P, hipStream_t stream) {
+               int P, hipStream_t stream, int vld = 0) {
     const Cfg c = pick_cfg(D, M, sizeof(T));
     KINET_CHECK_ARG(c.qt >= 1, "msda: heads*channels/vec (%d*%d) exceeds one workgroup", M, c.lpq);
+    if (vld == 0) vld = M * D;
+    KINET_CHECK_ARG(vld >= M * D && vld % c.vec == 0, "msda: value row stride %d invalid", vld);
+    KINET_CHECK_ARG((long long)S * vld < (1LL << 31), "msda: S*value_ld too large for one image");
     if (N == 0 || Lq == 0) return KINET_OK;
     using Acc = typename Acc<T>::type;
     const size_t tap = sizeof(Acc) == 8 ? sizeof(Tap4d) : sizeof(Tap4);
@@ -458,7 +531,7 @@ int launch_fwd(const void* value, const int64_t* shapes, const void* loc, const 
 #define KF(VEC)                                                                                             \
     hipLaunchKernelGGL((msda_fwd_kernel<T, TL, VEC, FUSED>), grid, dim3(kThreads), lds, stream,             \
                        (const T*)value, shapes, (const TL*)loc, (const TL*)attw, (const float*)offlog, ld_off,  \
-                       ref, ref_dim, qmask, loc_out, attw_out, (T*)out, S, M, D, L, Lq, P, c.qt, c.lpq)
+                       ref, ref_dim, qmask, loc_out, attw_out, (T*)out, S, M, D, L, Lq, P, c.qt, c.lpq, vld)
     switch (c.vec) {
         case 1: KF(1); break;
         case 2: KF(2); break;
@@ -545,8 +618,8 @@ extern "C" int kinet_msda_forward(const void* value, const int64_t* spatial_shap
     return KINET_ERR_ARG;
 }
 
-extern "C" int kinet_msda_fused_forward(const void* value, const int64_t* spatial_shapes, const void* offsets_logits,
-                                        int ld_off, const float* ref_points, int ref_dim,
+extern "C" int kinet_msda_fused_forward(const void* value, int value_ld, const int64_t* spatial_shapes,
+                                        const void* offsets_logits, int ld_off, const float* ref_points, int ref_dim,
                                         const uint8_t* query_attn_mask, void* output, float* loc_out,
                                         float* attw_out, int batch, int spatial_size, int num_heads, int channels,
                                         int num_levels, int num_query, int num_point, int value_dtype,
@@ -556,9 +629,11 @@ extern "C" int kinet_msda_fused_forward(const void* value, const int64_t* spatia
     KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.", ref_dim);
     KINET_CHECK_ARG(ld_off >= num_heads * num_levels * num_point * 3, "msda fused: ld_off %d too small", ld_off);
     KINET_CHECK_ARG((loc_out == nullptr) == (attw_out == nullptr), "msda fused: loc_out/attw_out must both be set or both NULL");
+    KINET_CHECK_ARG(value_ld == 0 || value_ld >= num_heads * channels, "msda fused: value_ld %d < M*D", value_ld);
     hipStream_t s = (hipStream_t)stream;
 #define ARGS value, spatial_shapes, nullptr, nullptr, offsets_logits, ld_off, ref_points, ref_dim, query_attn_mask, \
-             loc_out, attw_out, output, batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, s
+             loc_out, attw_out, output, batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, s, \
+             value_ld
     if (value_dtype == KINET_F32) return launch_fwd<float, float, 1>(ARGS);
     if (value_dtype == KINET_BF16) return launch_fwd<bf16_t, float, 1>(ARGS);
     if (value_dtype == KINET_F16) return launch_fwd<f16_t, float, 1>(ARGS);

@@ -140,6 +140,44 @@ __global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int N
     }
 }
 
+// 16-byte vector form (C % (16/sizeof(T)) == 0): one thread = one output pixel x 16 bytes
+template <typename T>
+__global__ void maxpool_vec_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int Ho,
+                                   int Wo) {
+    constexpr int V = 16 / sizeof(T);
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const int CV = C / V;
+    const long total = (long)N * Ho * Wo * CV;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int cv = (int)(i % CV);
+        long r = i / CV;
+        const int ow = (int)(r % Wo);
+        r /= Wo;
+        const int oh = (int)(r % Ho);
+        const int n = (int)(r / Ho);
+        float m[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) m[j] = -INFINITY;
+        for (int dy = 0; dy < 3; ++dy) {
+            const int ih = oh * 2 - 1 + dy;
+            if (ih < 0 || ih >= H) continue;
+            for (int dx = 0; dx < 3; ++dx) {
+                const int iw = ow * 2 - 1 + dx;
+                if (iw < 0 || iw >= W) continue;
+                const u4 v = *reinterpret_cast<const u4*>(x + (((long)n * H + ih) * W + iw) * C + cv * V);
+                const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+                for (int j = 0; j < V; ++j) m[j] = fmaxf(m[j], to_f32(e[j]));
+            }
+        }
+        u4 o;
+        T* oe = reinterpret_cast<T*>(&o);
+#pragma unroll
+        for (int j = 0; j < V; ++j) st(oe + j, m[j]);
+        *reinterpret_cast<u4*>(y + (((long)n * Ho + oh) * Wo + ow) * C + cv * V) = o;
+    }
+}
+
 template <typename T>
 __global__ void pack_image_kernel(const float* __restrict__ x, T* __restrict__ y, int N, int H, int W, int Cp) {
     const long total = (long)N * H * W * Cp;
@@ -333,8 +371,15 @@ extern "C" int kinet_maxpool2d_3x3s2(const void* x, void* y, int N, int H, int W
     const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
     const long total = (long)N * Ho * Wo * C;
     if (total == 0) return KINET_OK;
-    DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool_kernel<T>), dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
-                                         (const T*)x, (T*)y, N, H, W, C, Ho, Wo));
+    const bool vec = (dtype == KINET_F32 ? C % 4 : C % 8) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0;
+    if (vec) {
+        const long tv = total / (dtype == KINET_F32 ? 4 : 8);
+        DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool_vec_kernel<T>), dim3(grid_for(tv)), dim3(256), 0,
+                                             (hipStream_t)stream, (const T*)x, (T*)y, N, H, W, C, Ho, Wo));
+    } else {
+        DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool_kernel<T>), dim3(grid_for(total)), dim3(256), 0,
+                                             (hipStream_t)stream, (const T*)x, (T*)y, N, H, W, C, Ho, Wo));
+    }
     KINET_LAUNCH_CHECK();
     return KINET_OK;
 }

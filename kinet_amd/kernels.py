@@ -85,15 +85,23 @@ def f32(t):
 
 # ----------------------------------------------------------------------------------- GEMM
 def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_dtype=None,
-           scale=None, out=None):
-    """y = relu?(x @ W^T * scale + bias + residual); rows with row_mask -> 0.
-    x (..., K) in bf16/f16/f32; weight (Nout, K) any float dtype (cast+cached)."""
+           scale=None, out=None, x_add=None, ln=None):
+    """y = LN?(relu?((x [+ x_add]) @ W^T * scale + bias + residual)); rows with row_mask -> 0.
+    x (..., K) in bf16/f16/f32; weight (Nout, K) any float dtype (cast+cached);
+    ln = (gamma, beta, eps) fuses the post-norm LayerNorm over each output row."""
     N.require_gpu(x)
     K = x.shape[-1]
     lead = x.shape[:-1]
     x2 = x.reshape(-1, K)
     if x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16:
         x2 = x2.contiguous()
+    a2 = None
+    if x_add is not None:
+        a2 = x_add.reshape(-1, K)
+        if a2.stride() != x2.stride() or a2.data_ptr() % 16:
+            x2, a2 = x2.contiguous(), a2.contiguous()
+            if a2.stride() != x2.stride():
+                raise RuntimeError('linear: x_add must match x layout')
     M = x2.shape[0]
     w = weight_as(weight, x.dtype)
     Nout = w.shape[0]
@@ -116,10 +124,11 @@ def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_d
     if row_mask is not None:
         mask = row_mask.reshape(-1).to(torch.uint8).contiguous()
     e = x.element_size()
-    N.call('kinet_gemm', N.ptr(x2), N.ptr(w), N.ptr(out), M, Nout, K, x2.stride(0), K, ldc,
+    g, b, eps = (f32(ln[0]), f32(ln[1]), float(ln[2])) if ln is not None else (None, None, 0.0)
+    N.call('kinet_gemm_ex', N.ptr(x2), N.ptr(a2), N.ptr(w), N.ptr(out), M, Nout, K, x2.stride(0), K, ldc,
            N.dtype_code(x.dtype), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(r), ldr, int(relu),
-           N.dtype_code(odt), N.ptr(mask), 0, N.stream(x.device),
-           work={'family': 'gemm', 'flops': 2.0 * M * Nout * K,
+           N.ptr(g), N.ptr(b), eps, N.dtype_code(odt), N.ptr(mask), N.stream(x.device),
+           work={'family': 'gemm', 'flops': 2.0 * M * Nout * K, 'shape': (M, Nout, K),
                  'bytes': (M * K + Nout * K) * e + M * Nout * out.element_size() * (2 if r is not None else 1)})
     return out.view(*lead, Nout) if out.is_contiguous() else out
 
@@ -155,6 +164,7 @@ def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, res
            stride, pad, N.dtype_code(x.dtype), N.ptr(scale), N.ptr(bias), N.ptr(r),
            Cout if r is not None else 0, int(relu), ldy, N.stream(x.device),
            work={'family': 'conv', 'flops': 2.0 * B * Ho * Wo * Cout * KH * KW * Cin,
+                 'shape': (B, H, W, Cin, Cout, KH, stride),
                  'bytes': (B * H * W * Cin + Cout * KH * KW * Cin + B * Ho * Wo * Cout * (2 if r is not None else 1)) * e})
     return out
 
@@ -257,7 +267,10 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
     B, S, d = value.shape
     Lq = offlog.shape[1]
     D = d // n_heads
-    value = value.contiguous()
+    # a column slice of a batched projection is read in place (row stride value_ld)
+    if not (value.stride(-1) == 1 and value.stride(0) == S * value.stride(1) and value.data_ptr() % 16 == 0):
+        value = value.contiguous()
+    value_ld = value.stride(1)
     offlog = offlog.contiguous()
     ref = reference_points.float().contiguous()
     if ref.shape[2] != n_levels:
@@ -272,14 +285,14 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
         raise RuntimeError('msda_fused: the offsets/logits projection must be f32')
     ev = value.element_size()
     nsamp = B * Lq * n_heads * n_levels * n_points
-    N.call('kinet_msda_fused_forward', N.ptr(value), N.ptr(spatial_shapes), N.ptr(offlog), offlog.shape[-1],
+    N.call('kinet_msda_fused_forward', N.ptr(value), value_ld, N.ptr(spatial_shapes), N.ptr(offlog), offlog.shape[-1],
            N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), N.ptr(loc), N.ptr(attw), B, S, n_heads, D,
            n_levels, Lq, n_points, N.dtype_code(value.dtype), N.stream(value.device),
            work={'family': 'msda', 'flops': 10.0 * nsamp * D,
                  # compulsory bytes: value once, f32 offsets+logits, refs, output once
                  'bytes': B * S * d * ev + nsamp * 3 * 4 + ref.numel() * 4 + B * Lq * d * ev
                  + (nsamp * 3 * 4 if want_loc_attw else 0),
-                 'Lq': Lq, 'S': S})
+                 'Lq': Lq, 'S': S, 'shape': (B, Lq, S)})
     if want_loc_attw:
         return out, loc, attw
     return out

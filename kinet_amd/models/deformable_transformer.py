@@ -81,14 +81,12 @@ class DeformableTransformerEncoderLayer(nn.Module):
     def forward_fast(self, src, pos, reference_points, spatial_shapes, padding_mask=None):
         # deformable_transformer.py:290-299, one kernel per step
         a = self.self_attn
-        q = K.add(src, pos) if pos is not None else src
         value = K.linear(src, a.value_proj.weight, a.value_proj.bias, row_mask=padding_mask)
-        samp = a.sample(q, reference_points, value, spatial_shapes)
-        src = K.linear(samp, a.output_proj.weight, a.output_proj.bias, residual=src)
-        src = K.layernorm(src, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        samp = a.sample(src, reference_points, value, spatial_shapes, query_add=pos)   # (src+pos) @ W
+        n1, n2 = self.norm1, self.norm2
+        src = K.linear(samp, a.output_proj.weight, a.output_proj.bias, residual=src, ln=(n1.weight, n1.bias, n1.eps))
         h = K.linear(src, self.linear1.weight, self.linear1.bias, relu=True)
-        src = K.linear(h, self.linear2.weight, self.linear2.bias, residual=src)
-        return K.layernorm(src, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        return K.linear(h, self.linear2.weight, self.linear2.bias, residual=src, ln=(n2.weight, n2.bias, n2.eps))
 
 
 class DeformableTransformerEncoder(nn.Module):
@@ -169,22 +167,19 @@ class DeformableTransformerDecoderLayer(nn.Module):
         # deformable_transformer.py:367-386
         d = tgt.shape[-1]
         sa = self.self_attn
-        qk_in = K.add(tgt, query_pos) if query_pos is not None else tgt
-        qk = K.linear(qk_in, K.param_rows(sa.in_proj_weight, 0, 2 * d), K.param_rows(sa.in_proj_bias, 0, 2 * d))
+        n1, n2, n3 = self.norm1, self.norm2, self.norm3
+        qk = K.linear(tgt, K.param_rows(sa.in_proj_weight, 0, 2 * d), K.param_rows(sa.in_proj_bias, 0, 2 * d),
+                      x_add=query_pos)                                            # q = k = tgt + query_pos
         v = K.linear(tgt, K.param_rows(sa.in_proj_weight, 2 * d, 3 * d), K.param_rows(sa.in_proj_bias, 2 * d, 3 * d))
         attn = K.mha_core(qk[..., :d], qk[..., d:], v, sa.num_heads, sa.head_dim ** -0.5, key_mask=query_attn_mask)
-        tgt = K.linear(attn, sa.out_proj.weight, sa.out_proj.bias, residual=tgt)
-        tgt = K.layernorm(tgt, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        tgt = K.linear(attn, sa.out_proj.weight, sa.out_proj.bias, residual=tgt, ln=(n2.weight, n2.bias, n2.eps))
         ca = self.cross_attn
-        q = K.add(tgt, query_pos) if query_pos is not None else tgt
         if value is None:
             value = K.linear(src, ca.value_proj.weight, ca.value_proj.bias, row_mask=src_padding_mask)
-        samp = ca.sample(q, reference_points, value, src_spatial_shapes, query_attn_mask)
-        tgt = K.linear(samp, ca.output_proj.weight, ca.output_proj.bias, residual=tgt)
-        tgt = K.layernorm(tgt, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        samp = ca.sample(tgt, reference_points, value, src_spatial_shapes, query_attn_mask, query_add=query_pos)
+        tgt = K.linear(samp, ca.output_proj.weight, ca.output_proj.bias, residual=tgt, ln=(n1.weight, n1.bias, n1.eps))
         h = K.linear(tgt, self.linear1.weight, self.linear1.bias, relu=True)
-        tgt = K.linear(h, self.linear2.weight, self.linear2.bias, residual=tgt)
-        return K.layernorm(tgt, self.norm3.weight, self.norm3.bias, self.norm3.eps)
+        return K.linear(h, self.linear2.weight, self.linear2.bias, residual=tgt, ln=(n3.weight, n3.bias, n3.eps))
 
 
 def mlp_fast(mlp, x, out_dtype=torch.float32):
@@ -246,10 +241,20 @@ class DeformableTransformerDecoder(nn.Module):
             ref_in = reference_points[:, :, None] * torch.cat([vr, vr], -1)[:, None]
         else:
             ref_in = reference_points[:, :, None] * vr[:, None]
+        # every layer's cross-attention value_proj reads the same memory: run them as ONE
+        # GEMM (S x d x n_layers*d) and hand each layer its column slice (read in place)
+        d = tgt.shape[-1]
+        nl = len(self.layers)
+        vw = K.cached_multi([l.cross_attn.value_proj.weight for l in self.layers], 'dec_value_w',
+                            lambda *ws: torch.cat([w.detach() for w in ws], 0).contiguous())
+        vb = K.cached_multi([l.cross_attn.value_proj.bias for l in self.layers], 'dec_value_b',
+                            lambda *bs: torch.cat([b.detach() for b in bs], 0).float().contiguous())
+        values = K.linear(src, vw, vb, row_mask=src_padding_mask)
         intermediate, intermediate_reference_points = [], []
         for lid, layer in enumerate(self.layers):
-            output = layer(output, query_pos, ref_in, src, src_spatial_shapes, src_padding_mask, query_attn_mask)
-            last = lid == len(self.layers) - 1
+            output = layer(output, query_pos, ref_in, src, src_spatial_shapes, src_padding_mask, query_attn_mask,
+                           value=values[..., lid * d:(lid + 1) * d])
+            last = lid == nl - 1
             if self.bbox_embed is not None:
                 tmp = mlp_fast(self.bbox_embed[lid], output)
                 reference_points, nxt = K.box_refine(tmp, reference_points, vr, want_input=not last)

@@ -106,10 +106,12 @@ class MSDeformAttn(nn.Module):
                            lambda a, b: torch.cat([a.detach(), b.detach()], 0).float().contiguous())
         return w, b
 
-    def sample(self, query, reference_points, value, input_spatial_shapes, query_attn_mask=None):
-        """value already projected (N, S, d); returns the pre-output_proj (N, Lq, d)."""
+    def sample(self, query, reference_points, value, input_spatial_shapes, query_attn_mask=None, query_add=None):
+        """value already projected (N, S, d) (may be a column slice); the projection input
+        is query (+ query_add, e.g. the position embedding, added at GEMM load time);
+        returns the pre-output_proj (N, Lq, d)."""
         w, b = self.packed_offsets_weights()
-        offlog = K.linear(query, w, b, out_dtype=torch.float32)
+        offlog = K.linear(query, w, b, out_dtype=torch.float32, x_add=query_add)
         return K.msda_fused(value, input_spatial_shapes, offlog, reference_points,
                             self.n_heads, self.n_levels, self.n_points, query_attn_mask)
 
