@@ -55,6 +55,14 @@ int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, int Hin, int
                  int in_dtype, const float* scale, const float* bias, const void* R, int ldr,
                  int relu, int ldy, kinet_stream_t stream);
 
+/* value_proj for MSDA: C = (A @ B^T + bias) with rows masked, stored HEAD-MAJOR:
+ * row r = b*rows_per_batch + s, column n = g*head_dim + d  ->  C[((g*batch + b)*rows_per_batch + s)*head_dim + d]
+ * i.e. (N/head_dim, batch, rows_per_batch, head_dim) -- the layout kinet_msda_fused_forward
+ * gathers from best (ms_deform_attn.py:64-67 produce the same values in (N, S, M, D)). */
+int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                         int in_dtype, const float* bias, const uint8_t* row_mask, int rows_per_batch,
+                         int head_dim, kinet_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,11 +66,15 @@ int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num
  *   offsets_logits  (N, Lq, ld_off) f32 rows holding [M*L*P*2 offsets | M*L*P logits]
  *                   (the concatenated sampling_offsets/attention_weights projection)
  *   ref_points      (N, Lq, L, ref_dim) f32, ref_dim in {2, 4}
- *   value_ld        row stride of `value` in elements (0 = M*D): lets the six decoder
- *                   layers read column slices of ONE batched value projection
+ *   value element (b, s, m, c) at value[b*value_sb + s*value_ss + m*value_sm + c]
+ *                   (elements; all three 0 = row-major (N, S, M, D)).  kinet_amd feeds the
+ *                   head-major layout (M, N, S, D) written by kinet_gemm_headmajor, so a
+ *                   wave's gathers for neighbouring queries of one head are contiguous.
+ * Launch: one head per wave, 64/(D/vec) consecutive queries per wave.
  * Writes output (N, Lq, M*D) and, when loc_out/attw_out are non-NULL, the f32
  * sampling_loc / attn_weight tensors (needed to run kinet_msda_backward). */
-int kinet_msda_fused_forward(const void* value, int value_ld, const int64_t* spatial_shapes,
+int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_ss, int64_t value_sm,
+                             const int64_t* spatial_shapes,
                              const void* offsets_logits, int ld_off,
                              const float* ref_points, int ref_dim,
                              const uint8_t* query_attn_mask,

@@ -52,6 +52,9 @@ struct GemmArgs {
     const uint8_t* row_mask;
     float ln_eps;
     int a_bytes, b_bytes;   // buffer-descriptor extents (bytes, < 2^31)
+    // head-major store (hm_rows > 0): row r = b*hm_rows + s, column n = g*hm_d + d goes to
+    // C[((g*hm_batch + b)*hm_rows + s)*hm_d + d]  -- the MSDA value layout (heads, B, S, D)
+    int hm_rows, hm_d, hm_batch;
     int M, N, K, lda, ldb, ldc, ldr, relu;
     int Hin, Win, Cin, Hout, Wout, KW, stride, pad;
 };
@@ -147,7 +150,7 @@ struct Smem {
 };
 
 template <typename T, typename TO, int BM, int BN, int WGM, int WGN, bool CONV, bool LN>
-__global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p, const int nNt) {
+__global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const int nNt) {
     static_assert(WGM * WGN == 4, "4 waves");
     constexpr int EPC = Mma<T>::EPC;
     constexpr int BK = ROWB / (int)sizeof(T);
@@ -213,9 +216,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p, const int n
         wbase[i] = (unsigned)n * (unsigned)p.ldb;
     }
 
-    u32x4 xs[XR], ws[WR];
+    // two register staging sets: the loads of K-step k+2 are issued while k computes and
+    // k+1 (issued one step earlier) is written to LDS -- two steps of load latency covered
+    u32x4 xs0[XR], ws0[WR], xs1[XR], ws1[WR];
 
-    auto load_tile = [&](int k0) {
+    auto load_tile = [&](int k0, u32x4 (&xs)[XR], u32x4 (&ws)[WR]) {
         const int k = k0 + sc * EPC;
         const bool kok = k < K;
         int kh = 0, kw = 0, cc = k;
@@ -246,7 +251,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p, const int n
             ws[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, boff, 0, 0);
         }
     };
-    auto store_tile = [&](int buf) {
+    auto store_tile = [&](int buf, const u32x4 (&xs)[XR], const u32x4 (&ws)[WR]) {
         char* xl = lds + buf * STAGE;
         char* wl = xl + BM * ROWB;
 #pragma unroll
@@ -262,12 +267,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p, const int n
         for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = (K + BK - 1) / BK;
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) load_tile((kt + 1) * BK);
+    auto compute = [&](int buf) {
         const char* xl = lds + buf * STAGE;
         const char* wl = xl + BM * ROWB;
 #pragma unroll
@@ -285,8 +285,22 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p, const int n
 #pragma unroll
                 for (int b = 0; b < TM; ++b) Mma<T>::run(acc[a][b], afr[a], bfr[b]);
         }
-        if (kt + 1 < nk) store_tile(buf ^ 1);
+    };
+    // step kt: issue K-step kt+2 into the set that held kt (already in LDS), compute kt,
+    // write kt+1 (loaded one step ago) into the other LDS buffer, one barrier
+    auto step = [&](int kt, u32x4 (&xi)[XR], u32x4 (&wi)[WR], const u32x4 (&xn)[XR], const u32x4 (&wn)[WR]) {
+        if (kt + 2 < nk) load_tile((kt + 2) * BK, xi, wi);
+        compute(kt & 1);
+        if (kt + 1 < nk) store_tile((kt + 1) & 1, xn, wn);
         __syncthreads();
+    };
+    load_tile(0, xs0, ws0);
+    if (nk > 1) load_tile(BK, xs1, ws1);
+    store_tile(0, xs0, ws0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, xs0, ws0, xs1, ws1);
+        if (kt + 1 < nk) step(kt + 1, xs1, ws1, xs0, ws0);
     }
 
     // ---- epilogue: park the f32 tile in LDS (row m, col n), then stream whole rows ----
@@ -379,7 +393,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p, const int n
             const int n = n0 + nl0;
             if (nl0 >= BN || n >= N) continue;
             if (masked) v[c][0] = v[c][1] = v[c][2] = v[c][3] = 0.f;
-            TO* dst = C + (long)m * p.ldc + n;
+            TO* dst;
+            if (p.hm_rows) {
+                const int bb = m / p.hm_rows, ss = m - bb * p.hm_rows;
+                const int g = n / p.hm_d, dd = n - g * p.hm_d;
+                dst = C + (((long)g * p.hm_batch + bb) * p.hm_rows + ss) * p.hm_d + dd;
+            } else {
+                dst = C + (long)m * p.ldc + n;
+            }
             if (ld_ok && n + 3 < N) IO4<TO>::store(dst, v[c]);
             else
                 for (int r = 0; r < 4; ++r)
@@ -395,12 +416,18 @@ int launch(const GemmArgs& a, hipStream_t stream) {
     int bm, bn;
     if (ln) {
         KINET_CHECK_ARG(a.N <= 320, "gemm: fused LayerNorm needs N <= 320 (got %d)", a.N);
-        bm = 64;
+        bm = a.M <= 8192 ? 32 : 64;     // small M (decoder queries): more workgroups
         bn = a.N <= 256 ? 256 : 320;
+    } else if (a.M <= 4096) {
+        bm = 32;
+        bn = 64;
     } else {
         bn = a.N <= 64 ? 64 : 128;
         const long tiles128 = (long)((a.M + 127) / 128) * ((a.N + bn - 1) / bn);
         bm = tiles128 < 512 ? 64 : 128;
+        // single-K-step problems (1x1 convs with Cin <= 64) are store-bound: the smaller
+        // tile's LDS footprint lets 3 workgroups share a CU and overlap their epilogues
+        if (CONV && a.K <= 128 && bm == 128 && bn == 128) bm = 64;
     }
     const int nMt = (a.M + bm - 1) / bm, nNt = (a.N + bn - 1) / bn;
     const long nblk = (long)nMt * nNt;
@@ -409,9 +436,12 @@ int launch(const GemmArgs& a, hipStream_t stream) {
 #define L_(BM_, BN_, WM_, WN_, LN_) \
     hipLaunchKernelGGL((gemm_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0, stream, a, nNt)
     if (ln) {
-        if (bn == 256) L_(64, 256, 1, 4, true);
+        if (bm == 32 && bn == 256) L_(32, 256, 1, 4, true);
+        else if (bm == 32) L_(32, 320, 1, 4, true);
+        else if (bn == 256) L_(64, 256, 1, 4, true);
         else L_(64, 320, 1, 4, true);
-    } else if (bm == 128 && bn == 128) L_(128, 128, 2, 2, false);
+    } else if (bm == 32) L_(32, 64, 2, 2, false);
+    else if (bm == 128 && bn == 128) L_(128, 128, 2, 2, false);
     else if (bm == 128 && bn == 64) L_(128, 64, 2, 2, false);
     else if (bm == 64 && bn == 128) L_(64, 128, 2, 2, false);
     else L_(64, 64, 2, 2, false);
@@ -438,6 +468,10 @@ bool aligned16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
 
 using namespace kinet;
 
+extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                                    int in_dtype, const float* bias, const uint8_t* row_mask, int rows_per_batch,
+                                    int head_dim, kinet_stream_t stream);
+
 extern "C" int kinet_gemm_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K, int lda,
                              int ldb, int ldc, int in_dtype, const float* scale, const float* bias, const void* R,
                              int ldr, int relu, const float* ln_gamma, const float* ln_beta, float ln_eps,
@@ -460,6 +494,27 @@ extern "C" int kinet_gemm_ex(const void* A, const void* A2, const void* B, void*
     a.a_bytes = (int)ab;
     a.b_bytes = (int)bb;
     return dispatch<false>(a, in_dtype, out_dtype, (hipStream_t)stream);
+}
+
+extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                                    int in_dtype, const float* bias, const uint8_t* row_mask, int rows_per_batch,
+                                    int head_dim, kinet_stream_t stream) {
+    KINET_CHECK_ARG(M >= 0 && N > 0 && K > 0, "gemm_headmajor: invalid sizes");
+    KINET_CHECK_ARG(rows_per_batch > 0 && M % rows_per_batch == 0, "gemm_headmajor: M must be batch*rows_per_batch");
+    KINET_CHECK_ARG(head_dim > 0 && head_dim % 4 == 0 && N % head_dim == 0, "gemm_headmajor: N must be a multiple of head_dim (%% 4)");
+    KINET_CHECK_ARG(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K, "gemm_headmajor: bad K/lda/ldb");
+    KINET_CHECK_ARG(aligned16(A) && aligned16(B), "gemm_headmajor: A and B must be 16-byte aligned");
+    GemmArgs a{};
+    a.A = A; a.B = B; a.C = C; a.bias = bias; a.row_mask = row_mask;
+    a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = N;
+    a.hm_rows = rows_per_batch; a.hm_d = head_dim; a.hm_batch = M / rows_per_batch;
+    const long long es = (long long)dtype_size(in_dtype);
+    const long long ab = M > 0 ? ((long long)(M - 1) * lda + K) * es : 0;
+    const long long bb = ((long long)(N - 1) * ldb + K) * es;
+    KINET_CHECK_ARG(ab < (1LL << 31) && bb < (1LL << 31), "gemm_headmajor: operand larger than 2 GiB");
+    a.a_bytes = (int)ab;
+    a.b_bytes = (int)bb;
+    return dispatch<false>(a, in_dtype, in_dtype, (hipStream_t)stream);
 }
 
 extern "C" int kinet_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,

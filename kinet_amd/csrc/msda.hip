@@ -322,6 +322,141 @@ __global__ __launch_bounds__(kThreads) void msda_fwd_kernel(
 }
 
 // ---------------------------------------------------------------------------------
+// fused module forward, head-per-wave decomposition
+// ---------------------------------------------------------------------------------
+// Workgroup = QT consecutive queries x MH heads (one head per wave, QT = 64 / LPQ queries
+// per wave).  With the head-major value layout (heads, B, S, D) the 16 queries of a wave
+// sample neighbouring pixels of ONE head map, so a wave's tap loads hit a few contiguous
+// cache lines (with the row-major (B, S, M, D) layout a 128-B line holds one pixel of two
+// heads and a wave's loads scatter over 16 unrelated pieces).  Value element (b, s, m, c)
+// is value[b*vsb + s*vss + m*vsm + c]; both layouts are strides of this form.
+template <typename T, int VEC>
+__global__ __launch_bounds__(kThreads) void msda_fused_kernel(
+    const T* __restrict__ value, long vsb, int vss, long vsm, const int64_t* __restrict__ shapes,
+    const float* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
+    const uint8_t* __restrict__ qmask, float* __restrict__ loc_out, float* __restrict__ attw_out,
+    T* __restrict__ out, int S, int M, int D, int L, int Lq, int P, int QT, int LPQ, int MH) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    LevelInfo& li = *reinterpret_cast<LevelInfo*>(smem);
+    Tap4* taps = reinterpret_cast<Tap4*>(smem + sizeof(LevelInfo));
+    const int b = blockIdx.y;
+    const int q0 = blockIdx.x * QT;
+    const int mh0 = blockIdx.z * MH;
+    const int LP = L * P;
+    const int nsamp = MH * QT * LP;
+    load_levels(li, shapes, L, S);
+    __syncthreads();
+
+    const bool pow2 = (LP & (LP - 1)) == 0 && LP <= 64;
+    float* lg = reinterpret_cast<float*>(taps + nsamp);   // logits staging (general L*P only)
+    if (!pow2) {
+        for (int s = threadIdx.x; s < nsamp; s += kThreads) {
+            const int ml = s / (QT * LP), qi = (s / LP) % QT, lp = s % LP;
+            const int m = mh0 + ml, q = q0 + qi;
+            lg[s] = (q < Lq && m < M) ? offlog[((long)b * Lq + q) * ld_off + (long)M * LP * 2 + m * LP + lp] : -INFINITY;
+        }
+        __syncthreads();
+    }
+    const int nsamp_r = (nsamp + 63) & ~63;
+    for (int s = threadIdx.x; s < nsamp_r; s += kThreads) {
+        const bool sv = s < nsamp;
+        const int ml = s / (QT * LP), qi = (s / LP) % QT, lp = s % LP;
+        const int m = mh0 + ml, q = q0 + qi;
+        const int l = lp / P;
+        const bool ok = sv && q < Lq && m < M;
+        const float* orow = offlog + ((long)b * Lq + (ok ? q : 0)) * ld_off;
+        float a;
+        if (pow2) {   // the LP samples of one (query, head) are LP consecutive lanes
+            const float logit = ok ? orow[(long)M * LP * 2 + m * LP + lp] : -INFINITY;
+            float mx = logit;
+            for (int o = LP >> 1; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            const float e = ok ? __expf(logit - mx) : 0.f;
+            float sum = e;
+            for (int o = LP >> 1; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+            a = ok ? e / sum : 0.f;
+        } else if (ok) {
+            const float* grp = lg + (s - lp);
+            float mx = -INFINITY, sum = 0.f;
+            for (int j = 0; j < LP; ++j) mx = fmaxf(mx, grp[j]);
+            for (int j = 0; j < LP; ++j) sum += __expf(grp[j] - mx);
+            a = __expf(grp[lp] - mx) / sum;
+        } else {
+            a = 0.f;
+        }
+        if (!sv) continue;
+        Tap4 t4;
+        if (ok) {
+            if (qmask && qmask[(long)b * Lq + q]) a = 0.f;                  // ms_deform_attn.py:73-74
+            const float2 o2 = *reinterpret_cast<const float2*>(orow + (long)(m * LP + lp) * 2);
+            const float* rp = ref + (((long)b * Lq + q) * L + l) * ref_dim;
+            float x, y;
+            if (ref_dim == 2) {
+                // quirk kept for parity: offsets / spatial_shapes[(H, W)] applied to (x, y) (:77-79)
+                x = rp[0] + o2.x / (float)li.H[l];
+                y = rp[1] + o2.y / (float)li.W[l];
+            } else {                                                       // :80-82
+                x = rp[0] + o2.x / (float)P * rp[2] * 0.5f;
+                y = rp[1] + o2.y / (float)P * rp[3] * 0.5f;
+            }
+            if (loc_out) {
+                const long gi = (((long)b * Lq + q) * M + m) * LP + lp;
+                loc_out[2 * gi] = x;
+                loc_out[2 * gi + 1] = y;
+                attw_out[gi] = a;
+            }
+            setup_sample<T, float>(t4, x, y, a, li, l, vss, 0, D);          // offsets within one head map
+        } else {
+            for (int k = 0; k < 4; ++k) { t4.off[k] = 0; t4.w[k] = 0.f; }
+        }
+        taps[s] = t4;
+    }
+    __syncthreads();
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int qi = lane / LPQ;
+    const int m = mh0 + wave;
+    const int q = q0 + qi;
+    if (wave >= MH || m >= M || qi >= QT || q >= Lq) return;
+    const int c0 = (lane - qi * LPQ) * VEC;
+    const T* vb = value + (long)b * vsb + (long)m * vsm + c0;
+    const Tap4* tp = taps + (wave * QT + qi) * LP;
+    float acc[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+    constexpr int SG = 4;   // 4 samples x 4 taps = 16 gathers in flight per lane
+    int s = 0;
+    for (; s + SG <= LP; s += SG) {
+        Tap4 t[SG];
+#pragma unroll
+        for (int g2 = 0; g2 < SG; ++g2) t[g2] = tp[s + g2];
+        VecT<T, VEC> v[SG][4];
+#pragma unroll
+        for (int g2 = 0; g2 < SG; ++g2)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[g2][k] = *reinterpret_cast<const VecT<T, VEC>*>(vb + t[g2].off[k]);
+#pragma unroll
+        for (int g2 = 0; g2 < SG; ++g2)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) acc[j] += t[g2].w[k] * to_f32(v[g2][k].v[j]);
+    }
+    for (; s < LP; ++s) {
+        const Tap4 t = tp[s];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const VecT<T, VEC> v = *reinterpret_cast<const VecT<T, VEC>*>(vb + t.off[k]);
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) acc[j] += t.w[k] * to_f32(v.v[j]);
+        }
+    }
+    VecT<T, VEC> o;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o.v[j] = Cvt<T>::from(acc[j]);
+    *reinterpret_cast<VecT<T, VEC>*>(out + ((long)b * Lq + q) * M * D + (long)m * D + c0) = o;
+}
+
+// ---------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------
 template <typename A>
@@ -618,25 +753,70 @@ extern "C" int kinet_msda_forward(const void* value, const int64_t* spatial_shap
     return KINET_ERR_ARG;
 }
 
-extern "C" int kinet_msda_fused_forward(const void* value, int value_ld, const int64_t* spatial_shapes,
-                                        const void* offsets_logits, int ld_off, const float* ref_points, int ref_dim,
-                                        const uint8_t* query_attn_mask, void* output, float* loc_out,
-                                        float* attw_out, int batch, int spatial_size, int num_heads, int channels,
-                                        int num_levels, int num_query, int num_point, int value_dtype,
-                                        kinet_stream_t stream) {
+namespace kinet {
+namespace {
+template <typename T>
+int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* shapes, const float* offlog,
+                 int ld_off, const float* ref, int ref_dim, const uint8_t* qmask, void* out, float* loc_out,
+                 float* attw_out, int N, int S, int M, int D, int L, int Lq, int P, hipStream_t stream) {
+    const Cfg c = pick_cfg(D, M, sizeof(T));
+    KINET_CHECK_ARG(c.lpq <= 64, "msda fused: head_dim/vec (%d) exceeds a wave", c.lpq);
+    if (N == 0 || Lq == 0) return KINET_OK;
+    KINET_CHECK_ARG(vsb % c.vec == 0 && vss % c.vec == 0 && vsm % c.vec == 0 && ((uintptr_t)value % 16) == 0,
+                    "msda fused: value strides must keep %d-element vectors aligned", c.vec);
+    const int QT = 64 / c.lpq;          // queries per wave (= per workgroup)
+    const int MH = kThreads / 64;       // one head per wave
+    const int LP = L * P;
+    const size_t nsamp = (size_t)MH * QT * LP;
+    const bool pow2 = (LP & (LP - 1)) == 0 && LP <= 64;
+    const size_t lds = sizeof(LevelInfo) + nsamp * sizeof(Tap4) + (pow2 ? 0 : nsamp * sizeof(float));
+    KINET_CHECK_ARG(lds <= 160 * 1024, "msda fused: LDS request %zu too large", lds);
+    dim3 grid((Lq + QT - 1) / QT, N, (M + MH - 1) / MH);
+#define KF(VEC)                                                                                                  \
+    hipLaunchKernelGGL((msda_fused_kernel<T, VEC>), grid, dim3(kThreads), lds, stream, (const T*)value, vsb, vss, \
+                       vsm, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out, attw_out, (T*)out, S, M, D, L,   \
+                       Lq, P, QT, c.lpq, MH)
+    switch (c.vec) {
+        case 1: KF(1); break;
+        case 2: KF(2); break;
+        case 4: if (16 / sizeof(T) >= 4) { KF(4); } break;
+        case 8: if (16 / sizeof(T) >= 8) { KF(8); } break;
+    }
+#undef KF
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+}  // namespace
+}  // namespace kinet
+
+extern "C" int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_ss, int64_t value_sm,
+                                        const int64_t* spatial_shapes, const void* offsets_logits, int ld_off,
+                                        const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
+                                        void* output, float* loc_out, float* attw_out, int batch, int spatial_size,
+                                        int num_heads, int channels, int num_levels, int num_query, int num_point,
+                                        int value_dtype, kinet_stream_t stream) {
     int rc = common_checks(batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, 1);
     if (rc) return rc;
     KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.", ref_dim);
     KINET_CHECK_ARG(ld_off >= num_heads * num_levels * num_point * 3, "msda fused: ld_off %d too small", ld_off);
     KINET_CHECK_ARG((loc_out == nullptr) == (attw_out == nullptr), "msda fused: loc_out/attw_out must both be set or both NULL");
-    KINET_CHECK_ARG(value_ld == 0 || value_ld >= num_heads * channels, "msda fused: value_ld %d < M*D", value_ld);
+    if (value_sb == 0 && value_ss == 0 && value_sm == 0) {   // row-major (N, S, M, D)
+        value_ss = (int64_t)num_heads * channels;
+        value_sm = channels;
+        value_sb = value_ss * spatial_size;
+    }
+    KINET_CHECK_ARG(value_ss >= channels && value_sm >= 0 && value_sb >= 0, "msda fused: invalid value strides");
+    KINET_CHECK_ARG((long long)spatial_size * value_ss < (1LL << 31), "msda fused: S*value_ss too large");
+    const size_t es = dtype_size(value_dtype);
+    const int vec_el = (int)(16 / (es ? es : 1));
+    (void)vec_el;
     hipStream_t s = (hipStream_t)stream;
-#define ARGS value, spatial_shapes, nullptr, nullptr, offsets_logits, ld_off, ref_points, ref_dim, query_attn_mask, \
-             loc_out, attw_out, output, batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, s, \
-             value_ld
-    if (value_dtype == KINET_F32) return launch_fwd<float, float, 1>(ARGS);
-    if (value_dtype == KINET_BF16) return launch_fwd<bf16_t, float, 1>(ARGS);
-    if (value_dtype == KINET_F16) return launch_fwd<f16_t, float, 1>(ARGS);
+#define ARGS value, (long)value_sb, (int)value_ss, (long)value_sm, spatial_shapes, (const float*)offsets_logits, ld_off, \
+             ref_points, ref_dim, query_attn_mask, output, loc_out, attw_out, batch, spatial_size, num_heads, channels, \
+             num_levels, num_query, num_point, s
+    if (value_dtype == KINET_F32) return launch_fused<float>(ARGS);
+    if (value_dtype == KINET_BF16) return launch_fused<bf16_t>(ARGS);
+    if (value_dtype == KINET_F16) return launch_fused<f16_t>(ARGS);
 #undef ARGS
     set_error("msda fused forward: unsupported value dtype %d", value_dtype);
     return KINET_ERR_ARG;

@@ -199,8 +199,11 @@ __global__ void add_kernel(const T* __restrict__ a, const T* __restrict__ b, T* 
 }
 
 // ---------------------------------------------------------------------------------
-// MHA core: online softmax.  Block = 256 threads = 4 waves splitting the keys; each
-// lane owns one query row; keys/values streamed through LDS in tiles of 64.
+// MHA core (decoder query self-attention, a few hundred queries): online softmax.
+// Block = 256 threads = 16 queries x 4 lanes per query (each lane D/4 dims, dot products
+// reduced by two shuffles) x 4 waves, wave w taking keys w, w+4, ... of each 64-key tile
+// staged in LDS as f32 rows (broadcast vector reads); the 4 partial softmax states per
+// query are merged through LDS at the end.
 // ---------------------------------------------------------------------------------
 template <typename T, int D>
 __global__ __launch_bounds__(256) void mha_kernel(const T* __restrict__ Q, int ldq, const T* __restrict__ Kt, int ldk,
@@ -208,25 +211,30 @@ __global__ __launch_bounds__(256) void mha_kernel(const T* __restrict__ Q, int l
                                                   int Lq, int Lk, int heads, float scale,
                                                   const uint8_t* __restrict__ kmask) {
     constexpr int KT = 64;
-    __shared__ float ks[KT][D + 1];
-    __shared__ float vs[KT][D + 1];
-    __shared__ float part_m[4][64], part_l[4][64];
-    __shared__ float part_o[4][64][D + 1];
+    constexpr int QB = 16;                // queries per block
+    constexpr int DPL = D / 4;            // dims per lane
+    constexpr int LDR = D + 4;            // LDS row stride (floats)
+    __shared__ __attribute__((aligned(16))) float ks[KT][LDR];
+    __shared__ __attribute__((aligned(16))) float vs[KT][LDR];
+    __shared__ float kvalid[KT];
+    __shared__ float pm[4][QB], pl[4][QB];
+    __shared__ float po[4][QB][D + 1];
     const int b = blockIdx.z, h = blockIdx.y;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int qi = blockIdx.x * 64 + lane;
-    float q[D], o[D];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sub = lane & 3, ql = lane >> 2;
+    const int qi = blockIdx.x * QB + ql;
     const bool qok = qi < Lq;
+    float q[DPL], o[DPL];
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
-        q[j] = qok ? to_f32(Q[((long)b * Lq + qi) * ldq + h * D + j]) * scale : 0.f;
+    for (int j = 0; j < DPL; ++j) {
+        q[j] = qok ? to_f32(Q[((long)b * Lq + qi) * ldq + h * D + sub * DPL + j]) * scale : 0.f;
         o[j] = 0.f;
     }
     float mx = -INFINITY, l = 0.f;
     for (int k0 = 0; k0 < Lk; k0 += KT) {
         __syncthreads();
         for (int i = threadIdx.x; i < KT * D; i += 256) {
-            const int kk = i / D, j = i - (i / D) * D;
+            const int kk = i / D, j = i - kk * D;
             const int kr = k0 + kk;
             float kv = 0.f, vv = 0.f;
             if (kr < Lk) {
@@ -236,48 +244,52 @@ __global__ __launch_bounds__(256) void mha_kernel(const T* __restrict__ Q, int l
             ks[kk][j] = kv;
             vs[kk][j] = vv;
         }
+        if (threadIdx.x < KT) {
+            const int kr = k0 + threadIdx.x;
+            kvalid[threadIdx.x] = (kr < Lk && !(kmask && kmask[(long)b * Lk + kr])) ? 1.f : 0.f;
+        }
         __syncthreads();
-        // wave w handles keys kk = w, w+4, ...
-        for (int kk = wave; kk < KT; kk += 4) {
-            const int kr = k0 + kk;
-            if (kr >= Lk) break;
-            if (kmask && kmask[(long)b * Lk + kr]) continue;
+        const int kn = min(KT, Lk - k0);
+        for (int kk = wave; kk < kn; kk += 4) {
+            const float* kr = &ks[kk][sub * DPL];
             float s = 0.f;
 #pragma unroll
-            for (int j = 0; j < D; ++j) s += q[j] * ks[kk][j];
+            for (int j = 0; j < DPL; ++j) s += q[j] * kr[j];
+            s += __shfl_xor(s, 1);
+            s += __shfl_xor(s, 2);
+            if (kvalid[kk] == 0.f) continue;      // uniform across the 4 lanes of a query
             const float nm = fmaxf(mx, s);
             const float corr = __expf(mx - nm);
             const float pexp = __expf(s - nm);
             l = l * corr + pexp;
+            const float* vr = &vs[kk][sub * DPL];
 #pragma unroll
-            for (int j = 0; j < D; ++j) o[j] = o[j] * corr + pexp * vs[kk][j];
+            for (int j = 0; j < DPL; ++j) o[j] = o[j] * corr + pexp * vr[j];
             mx = nm;
         }
     }
-    // merge the 4 waves' partial softmax states
-    part_m[wave][lane] = mx;
-    part_l[wave][lane] = l;
-#pragma unroll
-    for (int j = 0; j < D; ++j) part_o[wave][lane][j] = o[j];
-    __syncthreads();
-    if (wave == 0 && qok) {
-        float M_ = -INFINITY;
-        for (int w = 0; w < 4; ++w) M_ = fmaxf(M_, part_m[w][lane]);
-        float L_ = 0.f;
-        float acc[D];
-#pragma unroll
-        for (int j = 0; j < D; ++j) acc[j] = 0.f;
-        for (int w = 0; w < 4; ++w) {
-            const float pm = part_m[w][lane];
-            const float f = pm == -INFINITY ? 0.f : __expf(pm - M_);
-            L_ += part_l[w][lane] * f;
-#pragma unroll
-            for (int j = 0; j < D; ++j) acc[j] += part_o[w][lane][j] * f;
-        }
-        const float inv = L_ > 0.f ? 1.f / L_ : 0.f;
-#pragma unroll
-        for (int j = 0; j < D; ++j) st(O + ((long)b * Lq + qi) * ldo + h * D + j, acc[j] * inv);
+    if (sub == 0) {
+        pm[wave][ql] = mx;
+        pl[wave][ql] = l;
     }
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) po[wave][ql][sub * DPL + j] = o[j];
+    __syncthreads();
+    if (wave != 0 || !qok) return;
+    float M_ = -INFINITY;
+    for (int w = 0; w < 4; ++w) M_ = fmaxf(M_, pm[w][ql]);
+    float L_ = 0.f, acc[DPL];
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
+    for (int w = 0; w < 4; ++w) {
+        const float f = pm[w][ql] == -INFINITY ? 0.f : __expf(pm[w][ql] - M_);
+        L_ += pl[w][ql] * f;
+#pragma unroll
+        for (int j = 0; j < DPL; ++j) acc[j] += po[w][ql][sub * DPL + j] * f;
+    }
+    const float inv = L_ > 0.f ? 1.f / L_ : 0.f;
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) st(O + ((long)b * Lq + qi) * ldo + h * D + sub * DPL + j, acc[j] * inv);
 }
 
 __device__ __forceinline__ float inv_sigmoid(float x) {
@@ -411,7 +423,7 @@ extern "C" int kinet_mha_core(const void* Q, int ldq, const void* Kt, int ldk, c
     KINET_CHECK_ARG(head_dim == 32 || head_dim == 36 || head_dim == 16 || head_dim == 64,
                     "mha: head_dim %d not instantiated (16/32/36/64)", head_dim);
     if (batch == 0 || Lq == 0) return KINET_OK;
-    dim3 grid((Lq + 63) / 64, heads, batch);
+    dim3 grid((Lq + 15) / 16, heads, batch);
     hipStream_t s = (hipStream_t)stream;
 #define MH(DD) DISPATCH_T(dtype, hipLaunchKernelGGL((mha_kernel<T, DD>), grid, dim3(256), 0, s, (const T*)Q, ldq, \
                                                    (const T*)Kt, ldk, (const T*)V, ldv, (T*)O, ldo, Lq, Lk, heads, \

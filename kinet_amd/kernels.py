@@ -133,6 +133,26 @@ def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_d
     return out.view(*lead, Nout) if out.is_contiguous() else out
 
 
+def value_proj_headmajor(x, weight, bias, head_dim, row_mask=None):
+    """MSDA value projection written head-major: x (B, S, K) -> (Nout/head_dim, B, S, head_dim),
+    padding rows zeroed (ms_deform_attn.py:64-67)."""
+    N.require_gpu(x)
+    B, S, K = x.shape
+    x2 = x.reshape(B * S, K)
+    if x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    w = weight_as(weight, x.dtype)
+    Nout = w.shape[0]
+    out = torch.empty((Nout // head_dim, B, S, head_dim), dtype=x.dtype, device=x.device)
+    mask = row_mask.reshape(-1).to(torch.uint8).contiguous() if row_mask is not None else None
+    e = x.element_size()
+    N.call('kinet_gemm_headmajor', N.ptr(x2), N.ptr(w), N.ptr(out), B * S, Nout, K, x2.stride(0), K,
+           N.dtype_code(x.dtype), N.ptr(f32(bias)), N.ptr(mask), S, head_dim, N.stream(x.device),
+           work={'family': 'gemm', 'flops': 2.0 * B * S * Nout * K, 'shape': (B * S, Nout, K),
+                 'bytes': (B * S * K + Nout * K + B * S * Nout) * e})
+    return out
+
+
 # ----------------------------------------------------------------------------------- conv
 def pack_conv_weight(w, dtype, cin_pad=None):
     """OIHW -> OHWI (Cin fastest), optional zero channel padding, cast."""
@@ -261,16 +281,27 @@ def box_refine(tmp, ref, valid_ratios=None, want_input=True):
 
 # ------------------------------------------------------------------------------ MSDA
 def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_levels, n_points,
-               query_attn_mask=None, want_loc_attw=False):
-    """value (B, S, d) projected; offlog (B, Lq, M*L*P*3) f32 [offsets | logits];
-    reference_points (B, Lq, L, 2|4) f32.  Returns (B, Lq, d) [, loc, attw]."""
-    B, S, d = value.shape
+               query_attn_mask=None, want_loc_attw=False, head_major=False):
+    """Sampling of MSDeformAttn.forward (ms_deform_attn.py:69-87) in one kernel.
+    value: projected values, either (B, S, d) row-major (column slices allowed) or, with
+    head_major=True, (M, B, S, D) as written by value_proj_headmajor;
+    offlog (B, Lq, M*L*P*3) f32 [offsets | logits]; reference_points (B, Lq, L, 2|4) f32.
+    Returns (B, Lq, d) [, loc, attw]."""
+    if head_major:
+        M_, B, S, D = value.shape
+        if M_ != n_heads:
+            raise RuntimeError(f'head-major value has {M_} heads, module expects {n_heads}')
+        d = M_ * D
+        if value.stride(-1) != 1 or value.data_ptr() % 16:
+            value = value.contiguous()
+        vsb, vss, vsm = value.stride(1), value.stride(2), value.stride(0)
+    else:
+        B, S, d = value.shape
+        D = d // n_heads
+        if not (value.stride(-1) == 1 and value.data_ptr() % 16 == 0):
+            value = value.contiguous()
+        vsb, vss, vsm = value.stride(0), value.stride(1), D
     Lq = offlog.shape[1]
-    D = d // n_heads
-    # a column slice of a batched projection is read in place (row stride value_ld)
-    if not (value.stride(-1) == 1 and value.stride(0) == S * value.stride(1) and value.data_ptr() % 16 == 0):
-        value = value.contiguous()
-    value_ld = value.stride(1)
     offlog = offlog.contiguous()
     ref = reference_points.float().contiguous()
     if ref.shape[2] != n_levels:
@@ -285,9 +316,9 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
         raise RuntimeError('msda_fused: the offsets/logits projection must be f32')
     ev = value.element_size()
     nsamp = B * Lq * n_heads * n_levels * n_points
-    N.call('kinet_msda_fused_forward', N.ptr(value), value_ld, N.ptr(spatial_shapes), N.ptr(offlog), offlog.shape[-1],
-           N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), N.ptr(loc), N.ptr(attw), B, S, n_heads, D,
-           n_levels, Lq, n_points, N.dtype_code(value.dtype), N.stream(value.device),
+    N.call('kinet_msda_fused_forward', N.ptr(value), vsb, vss, vsm, N.ptr(spatial_shapes), N.ptr(offlog),
+           offlog.shape[-1], N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), N.ptr(loc), N.ptr(attw), B, S,
+           n_heads, D, n_levels, Lq, n_points, N.dtype_code(value.dtype), N.stream(value.device),
            work={'family': 'msda', 'flops': 10.0 * nsamp * D,
                  # compulsory bytes: value once, f32 offsets+logits, refs, output once
                  'bytes': B * S * d * ev + nsamp * 3 * 4 + ref.numel() * 4 + B * Lq * d * ev

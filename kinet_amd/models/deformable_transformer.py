@@ -81,7 +81,7 @@ class DeformableTransformerEncoderLayer(nn.Module):
     def forward_fast(self, src, pos, reference_points, spatial_shapes, padding_mask=None):
         # deformable_transformer.py:290-299, one kernel per step
         a = self.self_attn
-        value = K.linear(src, a.value_proj.weight, a.value_proj.bias, row_mask=padding_mask)
+        value = a.project_value(src, padding_mask)                                     # head-major
         samp = a.sample(src, reference_points, value, spatial_shapes, query_add=pos)   # (src+pos) @ W
         n1, n2 = self.norm1, self.norm2
         src = K.linear(samp, a.output_proj.weight, a.output_proj.bias, residual=src, ln=(n1.weight, n1.bias, n1.eps))
@@ -175,7 +175,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
         tgt = K.linear(attn, sa.out_proj.weight, sa.out_proj.bias, residual=tgt, ln=(n2.weight, n2.bias, n2.eps))
         ca = self.cross_attn
         if value is None:
-            value = K.linear(src, ca.value_proj.weight, ca.value_proj.bias, row_mask=src_padding_mask)
+            value = ca.project_value(src, src_padding_mask)
         samp = ca.sample(tgt, reference_points, value, src_spatial_shapes, query_attn_mask, query_add=query_pos)
         tgt = K.linear(samp, ca.output_proj.weight, ca.output_proj.bias, residual=tgt, ln=(n1.weight, n1.bias, n1.eps))
         h = K.linear(tgt, self.linear1.weight, self.linear1.bias, relu=True)
@@ -249,11 +249,13 @@ class DeformableTransformerDecoder(nn.Module):
                             lambda *ws: torch.cat([w.detach() for w in ws], 0).contiguous())
         vb = K.cached_multi([l.cross_attn.value_proj.bias for l in self.layers], 'dec_value_b',
                             lambda *bs: torch.cat([b.detach() for b in bs], 0).float().contiguous())
-        values = K.linear(src, vw, vb, row_mask=src_padding_mask)
+        ca0 = self.layers[0].cross_attn
+        nh = ca0.n_heads
+        values = K.value_proj_headmajor(src, vw, vb, d // nh, row_mask=src_padding_mask)   # (nl*M, B, S, D)
         intermediate, intermediate_reference_points = [], []
         for lid, layer in enumerate(self.layers):
             output = layer(output, query_pos, ref_in, src, src_spatial_shapes, src_padding_mask, query_attn_mask,
-                           value=values[..., lid * d:(lid + 1) * d])
+                           value=values[lid * nh:(lid + 1) * nh])
             last = lid == nl - 1
             if self.bbox_embed is not None:
                 tmp = mlp_fast(self.bbox_embed[lid], output)

@@ -91,10 +91,15 @@ class MSDeformAttn(nn.Module):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             return self._forward_autograd(query, reference_points, input_flatten, input_spatial_shapes,
                                           input_padding_mask, query_attn_mask)
-        value = K.linear(input_flatten, self.value_proj.weight, self.value_proj.bias,
-                         row_mask=input_padding_mask)
+        value = self.project_value(input_flatten, input_padding_mask)
         out = self.sample(query, reference_points, value, input_spatial_shapes, query_attn_mask)
         return K.linear(out, self.output_proj.weight, self.output_proj.bias)
+
+    def project_value(self, input_flatten, input_padding_mask=None):
+        """value_proj + padding masked_fill (ms_deform_attn.py:64-66), written head-major
+        (M, N, S, D) for the gather kernel."""
+        return K.value_proj_headmajor(input_flatten, self.value_proj.weight, self.value_proj.bias,
+                                      self.d_model // self.n_heads, row_mask=input_padding_mask)
 
     # -- pieces used by the fused transformer layers ------------------------------------
     def packed_offsets_weights(self):
@@ -107,13 +112,15 @@ class MSDeformAttn(nn.Module):
         return w, b
 
     def sample(self, query, reference_points, value, input_spatial_shapes, query_attn_mask=None, query_add=None):
-        """value already projected (N, S, d) (may be a column slice); the projection input
-        is query (+ query_add, e.g. the position embedding, added at GEMM load time);
-        returns the pre-output_proj (N, Lq, d)."""
+        """value already projected: head-major (M, N, S, D) from project_value (or a
+        row-major (N, S, d) tensor); the offsets/weights projection input is query
+        (+ query_add, e.g. the position embedding, added at GEMM load time); returns the
+        pre-output_proj (N, Lq, d)."""
         w, b = self.packed_offsets_weights()
         offlog = K.linear(query, w, b, out_dtype=torch.float32, x_add=query_add)
         return K.msda_fused(value, input_spatial_shapes, offlog, reference_points,
-                            self.n_heads, self.n_levels, self.n_points, query_attn_mask)
+                            self.n_heads, self.n_levels, self.n_points, query_attn_mask,
+                            head_major=(value.dim() == 4))
 
     def _forward_autograd(self, query, reference_points, input_flatten, input_spatial_shapes,
                           input_padding_mask, query_attn_mask):
