@@ -63,6 +63,12 @@ int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, in
                          int in_dtype, const float* bias, const uint8_t* row_mask, int rows_per_batch,
                          int head_dim, kinet_stream_t stream);
 
+/* Diagnostic kernel-selection knob (no reference counterpart; used by the kernel
+ * benchmarks to A/B GEMM kernels in one process).  bit 1: allow the 512-thread
+ * 256x256-tile LDS-DMA kernel for large-M problems.  Returns the previous flags.
+ * Not thread-safe. */
+int kinet_gemm_set_flags(int flags);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,6 +34,10 @@
 namespace kinet {
 namespace {
 
+// diagnostic kernel-selection flags (kinet_gemm_set_flags): bit 1 = allow gemm_big_kernel
+// (measured slower than gemm_kernel on every detector shape, DESIGN.md, so off by default)
+int kinet_gemm_flags = 0;
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -148,6 +152,108 @@ struct Smem {
     static constexpr int EPI = BM * EPI_LD * 4;
     static constexpr int BYTES = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
 };
+
+// Fused epilogue over tile rows [r0, r1): the f32 accumulators of those rows are parked
+// in LDS at ep[(row - r0) * EPI_LD + col]; each wave streams whole rows (LPR lanes per row,
+// 4 columns per lane): scale/bias, residual, ReLU, LayerNorm, row mask, plain or
+// head-major store.
+template <typename TO, int BN, int EPI_LD, int NW, bool LN>
+__device__ __forceinline__ void epilogue_rows(const GemmArgs& p, const float* ep, int m0, int n0, int r0, int r1,
+                                              int wave, int lane) {
+    const int M = p.M, N = p.N;
+    constexpr int LPR = BN / 4 < 64 ? BN / 4 : 64;   // lanes per row
+    constexpr int NCH = (BN + 4 * LPR - 1) / (4 * LPR);   // 4-column chunks per lane
+    constexpr int RPW = 64 / LPR;                     // rows per wave pass
+    static_assert(64 % LPR == 0, "row mapping");
+    TO* __restrict__ C = (TO*)p.C;
+    const TO* __restrict__ R = (const TO*)p.R;
+    const int lr = lane / LPR, lc = lane - (lane / LPR) * LPR;
+    const bool ld_ok = ((p.ldc & 3) == 0) && (R == nullptr || (p.ldr & 3) == 0);
+    float sc4[NCH][4], bi4[NCH][4], g4[NCH][4], be4[NCH][4];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            int nn = n0 + (c * LPR + lc) * 4 + r;
+            nn = nn < N ? nn : N - 1;
+            sc4[c][r] = p.scale ? p.scale[nn] : 1.f;
+            bi4[c][r] = p.bias ? p.bias[nn] : 0.f;
+            g4[c][r] = LN ? p.ln_g[nn] : 1.f;
+            be4[c][r] = LN ? p.ln_b[nn] : 0.f;
+        }
+    for (int rr = r0 + wave * RPW + lr; rr < r1; rr += NW * RPW) {
+        const int m = m0 + rr;
+        // (LN needs every lane of the row in the reductions, so no early exit on m)
+        const bool mok = m < M;
+        float v[NCH][4];
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int nl0 = (c * LPR + lc) * 4;
+            const int n = n0 + nl0;
+            const bool cin = nl0 < BN;
+            f32x4 t = {0.f, 0.f, 0.f, 0.f};
+            if (cin) t = *reinterpret_cast<const f32x4*>(ep + (rr - r0) * EPI_LD + nl0);
+            float res[4] = {0.f, 0.f, 0.f, 0.f};
+            if (R && mok && cin && n < N) {
+                if (ld_ok && n + 3 < N) IO4<TO>::load(R + (long)m * p.ldr + n, res);
+                else
+                    for (int r = 0; r < 4; ++r)
+                        if (n + r < N) res[r] = IO4<TO>::load1(R + (long)m * p.ldr + n + r);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float x = t[r] * sc4[c][r] + bi4[c][r] + res[r];
+                if (p.relu) x = fmaxf(x, 0.f);
+                x = (cin && n + r < N) ? x : 0.f;
+                v[c][r] = x;
+                s += x;
+            }
+        }
+        if (LN) {
+#pragma unroll
+            for (int o = LPR >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            const float mean = s / (float)N;
+            float q = 0.f;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = n0 + (c * LPR + lc) * 4 + r;
+                    const float d = ((c * LPR + lc) * 4 < BN && n < N) ? v[c][r] - mean : 0.f;
+                    q += d * d;
+                }
+#pragma unroll
+            for (int o = LPR >> 1; o > 0; o >>= 1) q += __shfl_xor(q, o);
+            const float rstd = rsqrtf(q / (float)N + p.ln_eps);
+#pragma unroll
+            for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[c][r] = (v[c][r] - mean) * rstd * g4[c][r] + be4[c][r];
+        }
+        if (!mok) continue;
+        const bool masked = p.row_mask && p.row_mask[m];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int nl0 = (c * LPR + lc) * 4;
+            const int n = n0 + nl0;
+            if (nl0 >= BN || n >= N) continue;
+            if (masked) v[c][0] = v[c][1] = v[c][2] = v[c][3] = 0.f;
+            TO* dst;
+            if (p.hm_rows) {
+                const int bb = m / p.hm_rows, ss = m - bb * p.hm_rows;
+                const int g = n / p.hm_d, dd = n - g * p.hm_d;
+                dst = C + (((long)g * p.hm_batch + bb) * p.hm_rows + ss) * p.hm_d + dd;
+            } else {
+                dst = C + (long)m * p.ldc + n;
+            }
+            if (ld_ok && n + 3 < N) IO4<TO>::store(dst, v[c]);
+            else
+                for (int r = 0; r < 4; ++r)
+                    if (n + r < N) IO4<TO>::store1(dst + r, v[c][r]);
+        }
+    }
+}
 
 template <typename T, typename TO, int BM, int BN, int WGM, int WGN, bool CONV, bool LN>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const int nNt) {
@@ -314,105 +420,221 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
             *reinterpret_cast<f32x4*>(ep + ml * EPI_LD + nl) = acc[a][b];
         }
     __syncthreads();
+    epilogue_rows<TO, BN, EPI_LD, 4, LN>(p, ep, m0, n0, 0, BM, wave, lane);
+}
 
-    constexpr int LPR = BN / 4 < 64 ? BN / 4 : 64;   // lanes per row
-    constexpr int NCH = (BN + 4 * LPR - 1) / (4 * LPR);   // 4-column chunks per lane
-    constexpr int RPW = 64 / LPR;                     // rows per wave pass
-    static_assert(64 % LPR == 0, "row mapping");
-    TO* __restrict__ C = (TO*)p.C;
-    const TO* __restrict__ R = (const TO*)p.R;
-    const int lr = lane / LPR, lc = lane - (lane / LPR) * LPR;
-    const bool ld_ok = ((p.ldc & 3) == 0) && (R == nullptr || (p.ldr & 3) == 0);
-    float sc4[NCH][4], bi4[NCH][4], g4[NCH][4], be4[NCH][4];
+// Large-M GEMM / implicit conv: 512 threads (8 waves, WGM x WGN, each wave a (BM/WGM) x 64
+// output tile), BM x BN tile with BN in {128, 256}, BK = 64 (one 128-byte LDS row).
+// Operands are staged by LDS-DMA (buffer_load_dwordx4 ... lds): one wave-instruction fills
+// 8 consecutive 128-byte LDS rows (1 KiB, lane-linear), so the XOR swizzle is applied on
+// the SOURCE side -- lane l of a row-group loads logical chunk (l & 7) ^ (row & 7), and the
+// fragment reads use the same swz().  Out-of-range lanes (M/N edge, K tail, conv padding)
+// get an offset past num_records: the hardware writes zeros into LDS, so staging is
+// branch-free and needs no VGPRs.  Two LDS buffers; the loads of K-step k+1 are issued
+// before the MFMAs of step k.  The epilogue parks half the tile at a time in LDS and runs
+// the shared row epilogue with all 8 waves.
+template <int BM, int BN>
+struct BigSmem {
+    static constexpr int STAGE = (BM + BN) * ROWB;
+    static constexpr int EPI_LD = BN + 4;
+    static constexpr int EPI = (BM / 2) * EPI_LD * 4;
+    static constexpr int BYTES = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+};
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// one 16-byte-per-lane LDS-DMA: LDS[dst + 16*lane] = buffer[off] (zeros if off is out of
+// range).  Kept out of the kernel templates: hipcc (ROCm 7.2) drops the host launch stub
+// of a kernel template whose body calls the builtin directly.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* dst, unsigned off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)dst, 16, off, 0, 0, 0);
+}
+
+template <typename T, typename TO, int BM, int BN, bool CONV, bool LN>
+__global__ __launch_bounds__(512, 1) void gemm_big_kernel(const GemmArgs p, const int nNt) {
+    static_assert(sizeof(T) == 2, "16-bit operands only");
+    constexpr int WGN = BN / 64, WGM = 8 / WGN;
+    constexpr int WTM = BM / WGM, TM = WTM / 16, TN = 4;
+    constexpr int BK = ROWB / (int)sizeof(T);
+    constexpr int XR = BM / 64, WR = BN / 64;     // LDS row-groups of 64 rows per operand
+    constexpr int STAGE = BigSmem<BM, BN>::STAGE;
+    constexpr int EPI_LD = BigSmem<BM, BN>::EPI_LD;
+    constexpr int HALF = BM / 2;
+    static_assert(HALF % WTM == 0, "a wave's rows must lie in one epilogue half");
+    __shared__ __attribute__((aligned(16))) char lds[BigSmem<BM, BN>::BYTES];
+
+    int bid = blockIdx.x;
+    {
+        const int nblk = gridDim.x, q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    }
+    const int mt = bid / nNt, nt = bid - (bid / nNt) * nNt;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WGM, wn = wave / WGM;
+    const int M = p.M, N = p.N, K = p.K;
+
+    constexpr unsigned OOB = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
+
+    // this lane stages, in row-group i, tile row i*64 + wave*8 + (lane>>3), logical chunk sch
+    const int srow = wave * 8 + (lane >> 3);
+    const int sch = (lane & 7) ^ ((lane >> 3) & 7);
+    unsigned xbase[XR];
+    int xih[XR], xiw[XR];
+    bool xok[XR];
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            int nn = n0 + (c * LPR + lc) * 4 + r;
-            nn = nn < N ? nn : N - 1;
-            sc4[c][r] = p.scale ? p.scale[nn] : 1.f;
-            bi4[c][r] = p.bias ? p.bias[nn] : 0.f;
-            g4[c][r] = LN ? p.ln_g[nn] : 1.f;
-            be4[c][r] = LN ? p.ln_b[nn] : 0.f;
-        }
-    for (int rr = wave * RPW + lr; rr < BM; rr += 4 * RPW) {
-        const int m = m0 + rr;
-        // (LN needs every lane of the row in the reductions, so no early exit on m)
-        const bool mok = m < M;
-        float v[NCH][4];
-        float s = 0.f;
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const int nl0 = (c * LPR + lc) * 4;
-            const int n = n0 + nl0;
-            const bool cin = nl0 < BN;
-            f32x4 t = {0.f, 0.f, 0.f, 0.f};
-            if (cin) t = *reinterpret_cast<const f32x4*>(ep + rr * EPI_LD + nl0);
-            float res[4] = {0.f, 0.f, 0.f, 0.f};
-            if (R && mok && cin && n < N) {
-                if (ld_ok && n + 3 < N) IO4<TO>::load(R + (long)m * p.ldr + n, res);
-                else
-                    for (int r = 0; r < 4; ++r)
-                        if (n + r < N) res[r] = IO4<TO>::load1(R + (long)m * p.ldr + n + r);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float x = t[r] * sc4[c][r] + bi4[c][r] + res[r];
-                if (p.relu) x = fmaxf(x, 0.f);
-                x = (cin && n + r < N) ? x : 0.f;
-                v[c][r] = x;
-                s += x;
-            }
-        }
-        if (LN) {
-#pragma unroll
-            for (int o = LPR >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o);
-            const float mean = s / (float)N;
-            float q = 0.f;
-#pragma unroll
-            for (int c = 0; c < NCH; ++c)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int n = n0 + (c * LPR + lc) * 4 + r;
-                    const float d = ((c * LPR + lc) * 4 < BN && n < N) ? v[c][r] - mean : 0.f;
-                    q += d * d;
-                }
-#pragma unroll
-            for (int o = LPR >> 1; o > 0; o >>= 1) q += __shfl_xor(q, o);
-            const float rstd = rsqrtf(q / (float)N + p.ln_eps);
-#pragma unroll
-            for (int c = 0; c < NCH; ++c)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[c][r] = (v[c][r] - mean) * rstd * g4[c][r] + be4[c][r];
-        }
-        if (!mok) continue;
-        const bool masked = p.row_mask && p.row_mask[m];
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const int nl0 = (c * LPR + lc) * 4;
-            const int n = n0 + nl0;
-            if (nl0 >= BN || n >= N) continue;
-            if (masked) v[c][0] = v[c][1] = v[c][2] = v[c][3] = 0.f;
-            TO* dst;
-            if (p.hm_rows) {
-                const int bb = m / p.hm_rows, ss = m - bb * p.hm_rows;
-                const int g = n / p.hm_d, dd = n - g * p.hm_d;
-                dst = C + (((long)g * p.hm_batch + bb) * p.hm_rows + ss) * p.hm_d + dd;
-            } else {
-                dst = C + (long)m * p.ldc + n;
-            }
-            if (ld_ok && n + 3 < N) IO4<TO>::store(dst, v[c]);
-            else
-                for (int r = 0; r < 4; ++r)
-                    if (n + r < N) IO4<TO>::store1(dst + r, v[c][r]);
+    for (int i = 0; i < XR; ++i) {
+        const int m = m0 + srow + 64 * i;
+        xok[i] = m < M;
+        if (CONV) {
+            const int hw = p.Hout * p.Wout;
+            const int img = m / hw;
+            const int rem = m - img * hw;
+            const int oh = rem / p.Wout, ow = rem - (rem / p.Wout) * p.Wout;
+            xih[i] = oh * p.stride - p.pad;
+            xiw[i] = ow * p.stride - p.pad;
+            xbase[i] = (unsigned)img * (unsigned)(p.Hin * p.Win * p.Cin);
+        } else {
+            xih[i] = xiw[i] = 0;
+            xbase[i] = (unsigned)m * (unsigned)p.lda;
         }
     }
+    unsigned wbase[WR];
+    bool wok[WR];
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+        const int n = n0 + srow + 64 * i;
+        wok[i] = n < N;
+        wbase[i] = (unsigned)n * (unsigned)p.ldb;
+    }
+
+    auto stage = [&](int k0, int buf) {
+        char* xl = lds + buf * STAGE + wave * 8 * ROWB;
+        char* wl = lds + buf * STAGE + BM * ROWB + wave * 8 * ROWB;
+        const int k = k0 + sch * 8;
+        const bool kok = k < K;
+        int kh = 0, kw = 0, cc = k;
+        if (CONV) {
+            const int tap = k / p.Cin;
+            cc = k - tap * p.Cin;
+            kh = tap / p.KW;
+            kw = tap - kh * p.KW;
+        }
+#pragma unroll
+        for (int i = 0; i < XR; ++i) {
+            bool ok = xok[i] && kok;
+            unsigned off;
+            if (CONV) {
+                const int ih = xih[i] + kh, iw = xiw[i] + kw;
+                ok = ok && ih >= 0 && ih < p.Hin && iw >= 0 && iw < p.Win;
+                off = xbase[i] + (unsigned)((ih * p.Win + iw) * p.Cin + cc);
+            } else {
+                off = xbase[i] + (unsigned)k;
+            }
+            dma16(ra, xl + i * 64 * ROWB, ok ? off * (unsigned)sizeof(T) : OOB);
+        }
+#pragma unroll
+        for (int i = 0; i < WR; ++i)
+            dma16(rb, wl + i * 64 * ROWB, (wok[i] && kok) ? (wbase[i] + (unsigned)k) * (unsigned)sizeof(T) : OOB);
+    };
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int buf) {
+        const char* xl = lds + buf * STAGE;
+        const char* wl = xl + BM * ROWB;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + (lane >> 4);
+            u32x4 bfr[TM], afr[TN];
+#pragma unroll
+            for (int t = 0; t < TN; ++t)
+                afr[t] = *reinterpret_cast<const u32x4*>(wl + swz(wn * 64 + t * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int t = 0; t < TM; ++t)
+                bfr[t] = *reinterpret_cast<const u32x4*>(xl + swz(wm * WTM + t * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int b = 0; b < TM; ++b)
+#pragma unroll
+                for (int a = 0; a < TN; ++a) Mma<T>::run(acc[a][b], afr[a], bfr[b]);
+        }
+    };
+
+    const int nk = (K + BK - 1) / BK;
+    stage(0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) stage((kt + 1) * BK, (kt + 1) & 1);
+        compute(kt & 1);
+        __syncthreads();   // waits this thread's DMA (vmcnt) and everyone's reads of kt
+    }
+
+    float* ep = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h) __syncthreads();
+        if ((wm * WTM) / HALF == h) {
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int b = 0; b < TM; ++b) {
+                    const int ml = wm * WTM - h * HALF + b * 16 + (lane & 15);
+                    const int nl = wn * 64 + a * 16 + (lane >> 4) * 4;
+                    *reinterpret_cast<f32x4*>(ep + ml * EPI_LD + nl) = acc[a][b];
+                }
+        }
+        __syncthreads();
+        epilogue_rows<TO, BN, EPI_LD, 8, LN>(p, ep, m0, n0, h * HALF, (h + 1) * HALF, wave, lane);
+    }
 }
+
+// Launch the 512-thread LDS-DMA kernel when the problem suits it (16-bit operands, large
+// M, N >= 128, no load-time A2 add); false = use the 256-thread kernel.
+template <typename T, typename TO, bool CONV>
+bool launch_big(const GemmArgs& a, hipStream_t stream) {
+    const bool ln = a.ln_g != nullptr;
+    if (a.A2 == nullptr && a.M >= 16384 && a.N >= 128 && (!ln || a.N <= 256) && (kinet_gemm_flags & 2)) {
+        const int bn = (a.N > 128 || ln) ? 256 : 128;   // LN needs the whole row in one tile
+        const long t256 = (long)((a.M + 255) / 256) * ((a.N + bn - 1) / bn);
+        const int bm = (bn == 256 && t256 < 512) ? 128 : 256;
+        const int nMt = (a.M + bm - 1) / bm, nNt = (a.N + bn - 1) / bn;
+        const long nblk = (long)nMt * nNt;
+        if (nblk >= (1L << 31)) return false;
+        dim3 grid((unsigned)nblk), block(512);
+#define B_(BM_, BN_, LN_) \
+    hipLaunchKernelGGL((gemm_big_kernel<T, TO, BM_, BN_, CONV, LN_>), grid, block, 0, stream, a, nNt)
+        if (ln) {
+            if (bm == 128) B_(128, 256, true);
+            else B_(256, 256, true);
+        } else if (bn == 128) B_(256, 128, false);
+        else if (bm == 128) B_(128, 256, false);
+        else B_(256, 256, false);
+#undef B_
+        return true;
+    }
+    return false;
+}
+template <>
+bool launch_big<float, float, false>(const GemmArgs&, hipStream_t) { return false; }
+template <>
+bool launch_big<float, float, true>(const GemmArgs&, hipStream_t) { return false; }
 
 template <typename T, typename TO, bool CONV>
 int launch(const GemmArgs& a, hipStream_t stream) {
     if (a.M == 0 || a.N == 0) return KINET_OK;
     const bool ln = a.ln_g != nullptr;
+    if (launch_big<T, TO, CONV>(a, stream)) {
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
     int bm, bn;
     if (ln) {
         KINET_CHECK_ARG(a.N <= 320, "gemm: fused LayerNorm needs N <= 320 (got %d)", a.N);
@@ -515,6 +737,12 @@ extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M
     a.a_bytes = (int)ab;
     a.b_bytes = (int)bb;
     return dispatch<false>(a, in_dtype, in_dtype, (hipStream_t)stream);
+}
+
+extern "C" int kinet_gemm_set_flags(int flags) {
+    const int old = kinet_gemm_flags;
+    kinet_gemm_flags = flags;
+    return old;
 }
 
 extern "C" int kinet_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,

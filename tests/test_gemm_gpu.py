@@ -114,3 +114,116 @@ def test_mha_core(K, D, Lq):
     ref = F.scaled_dot_product_attention(split(q), split(k), split(v)).transpose(1, 2).reshape(B, Lq, E)
     y = K.mha_core(q.cuda(), k.cuda(), v.cuda(), heads, D ** -0.5)
     assert _rel(y, ref) < 1e-5
+
+
+# ---- the 512-thread LDS-DMA kernel (M >= 16384, N >= 128, 16-bit operands) ----------------
+
+@pytest.fixture
+def gemm_flags():
+    """Select the GEMM kernel family for one test and restore the default afterwards."""
+    from kinet_amd import _native
+    lib = _native.lib()
+    yield lib.kinet_gemm_set_flags
+    lib.kinet_gemm_set_flags(0)
+
+
+@pytest.fixture
+def big(gemm_flags):
+    gemm_flags(2)
+    yield
+
+
+@pytest.mark.parametrize('M,N,Kd,mode', [
+    (20000, 256, 256, 'ln'),          # output_proj + residual + LayerNorm (256x256 tiles)
+    (16411, 1024, 256, 'relu'),       # FFN linear1, ragged M
+    (17000, 384, 264, 'plain'),       # K tail inside a 64-wide K-step
+    (16390, 128, 1024, 'relu'),       # BN = 128 tiles
+    (18000, 200, 256, 'ln'),          # ragged N inside one 256-wide tile, LN over 200 columns
+    (16500, 160, 512, 'residual'),    # ragged N on the 256-wide tile without LN
+])
+def test_big_gemm_vs_fp32(K, big, M, N, Kd, mode):
+    g = torch.Generator().manual_seed(M + N + Kd)
+    x = torch.randn(M, Kd, generator=g).bfloat16()
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).bfloat16()
+    b = torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g).bfloat16()
+    mask = torch.rand(M, generator=g) < 0.1
+    ref = F.linear(x.float(), w.float(), b)
+    kw = {}
+    if mode in ('ln', 'residual'):
+        ref = ref + r.float()
+        kw['residual'] = r.cuda()
+    if mode == 'relu':
+        ref = F.relu(ref)
+        kw['relu'] = True
+    if mode == 'ln':
+        gam, bet = torch.rand(N, generator=g) + 0.5, torch.randn(N, generator=g)
+        ref = F.layer_norm(ref, (N,), gam, bet, 1e-5)
+        kw['ln'] = (gam.cuda(), bet.cuda(), 1e-5)
+    ref = ref.masked_fill(mask[:, None], 0)
+    y = K.linear(x.cuda(), w.cuda(), b.cuda(), row_mask=mask.cuda(), **kw)
+    torch.cuda.synchronize()
+    # bf16 output rounding only (fp32 accumulation of bf16 products)
+    err = (y.float().cpu() - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
+
+
+@pytest.mark.parametrize('M,N,Kd', [(20000, 256, 256), (16411, 1024, 264), (16390, 128, 1024)])
+def test_big_gemm_matches_small_kernel(K, gemm_flags, M, N, Kd):
+    """Both kernels accumulate the same bf16 products in the same K-step order in f32, so
+    they must agree to the last bit of the bf16 output (or within one rounding step)."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(M, Kd, generator=g).bfloat16().cuda()
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).bfloat16().cuda()
+    b = torch.randn(N, generator=g).cuda()
+    gemm_flags(2)
+    y_big = K.linear(x, w, b, relu=True)
+    gemm_flags(0)
+    y_small = K.linear(x, w, b, relu=True)
+    torch.cuda.synchronize()
+    d = (y_big.float() - y_small.float()).abs()
+    tol = y_small.float().abs() * 2.0 ** -7 + 1e-6
+    assert (d <= tol).all(), d.max().item()
+    assert (d == 0).float().mean().item() > 0.95
+
+
+def test_big_gemm_headmajor(K, big):
+    B, S, d, hd = 2, 9000, 256, 32
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, S, d, generator=g).bfloat16()
+    w = (torch.randn(d, d, generator=g) / 16).bfloat16()
+    b = torch.randn(d, generator=g)
+    mask = torch.rand(B, S, generator=g) < 0.2
+    ref = F.linear(x.float(), w.float(), b).masked_fill(mask[..., None], 0)      # (B, S, d)
+    ref = ref.view(B, S, d // hd, hd).permute(2, 0, 1, 3)                         # (heads, B, S, hd)
+    y = K.value_proj_headmajor(x.cuda(), w.cuda(), b.cuda(), hd, row_mask=mask.cuda())
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == tuple(ref.shape)
+    err = (y.float().cpu() - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
+
+
+@pytest.mark.parametrize('B,H,W,Cin,Cout,k,s,p', [
+    (2, 96, 96, 64, 256, 1, 1, 0),      # 1x1, BN = 256 tiles
+    (2, 100, 100, 64, 128, 3, 1, 1),    # 3x3 padded, BN = 128 tiles
+    (2, 190, 190, 64, 128, 3, 2, 1),    # strided
+    (1, 260, 260, 8, 128, 7, 2, 3),     # stem-like: K = 392 (tail), Cin = 8
+    (4, 100, 168, 256, 512, 1, 2, 0),   # strided 1x1 downsample
+])
+def test_big_conv_vs_fp32(K, big, B, H, W, Cin, Cout, k, s, p):
+    g = torch.Generator().manual_seed(H * W + Cin + Cout)
+    x = torch.randn(B, Cin, H, W, generator=g).bfloat16()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * (2.0 / (Cin * k * k)) ** 0.5).bfloat16()
+    scale = torch.rand(Cout, generator=g) + 0.5
+    bias = torch.randn(Cout, generator=g) * 0.1
+    y_ref = F.conv2d(x.float(), w.float(), stride=s, padding=p) * scale[None, :, None, None] + bias[None, :, None, None]
+    res = torch.randn_like(y_ref).bfloat16()
+    y_ref = F.relu(y_ref + res.float())
+    xn = x.permute(0, 2, 3, 1).contiguous().cuda()
+    wp = K.pack_conv_weight(w.cuda(), torch.bfloat16)
+    rn = res.permute(0, 2, 3, 1).contiguous().cuda()
+    y = K.conv2d_nhwc(xn, wp, s, p, scale=scale.cuda(), bias=bias.cuda(), relu=True, residual=rn)
+    torch.cuda.synchronize()
+    assert y.shape[0] * y.shape[1] * y.shape[2] >= 16384        # really on the big-tile path
+    err = (y.permute(0, 3, 1, 2).float().cpu() - y_ref).abs()
+    assert (err <= 1e-2 * y_ref.abs() + 2e-2).all(), err.max().item()
