@@ -65,7 +65,8 @@ int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, in
 
 /* Diagnostic kernel-selection knob (no reference counterpart; used by the kernel
  * benchmarks to A/B GEMM kernels in one process).  bit 1: allow the 512-thread
- * 256x256-tile LDS-DMA kernel for large-M problems.  Returns the previous flags.
+ * 256x256-tile LDS-DMA kernel for large-M problems; bit 2: never use the
+ * resident-weight streaming kernel (K <= 256).  Returns the previous flags.
  * Not thread-safe. */
 int kinet_gemm_set_flags(int flags);
 

@@ -1,0 +1,390 @@
+// Resident-weight streaming GEMM for gfx950: C[M, N] = epilogue(A[M, K] @ W[N, K]^T) for
+// large M and K <= 256 -- the deformable-encoder projections (value_proj, output_proj +
+// residual + LayerNorm, FFN linear1, sampling offsets / attention logits) and the 1x1
+// stride-1 convolutions of the ResNet body (NHWC activations are plain row-major GEMM
+// operands).  DESIGN.md "Resident-weight GEMM".
+//
+// Why a second GEMM: with K = 256 the MFMA work per output byte is small and the tiled
+// kernel (gemm.hip) spends its time re-loading W tiles and re-reading A once per N-tile
+// through the CU load path.  Here
+//  * a workgroup (4 waves) owns a column group of GW = 4*NT*16 output columns for the
+//    whole launch; wave w keeps W rows [w*NT*16, (w+1)*NT*16) x K as MFMA A-fragments in
+//    VGPRs (NT*KC*4 registers), loaded once;
+//  * the workgroup walks row tiles of BMR rows (persistent: tile = blockIdx.x + i*gridDim.x);
+//    each A tile (and the residual tile and the row-mask bytes) is staged into an NS-deep
+//    LDS ring by LDS-DMA (buffer_load_dwordx4 ... lds, XOR swizzle on the source side,
+//    hardware zero fill past the edges), issued NS-1 tiles ahead;  a counted
+//    `s_waitcnt vmcnt` + raw s_barrier retires one tile per iteration, so the DMA of later
+//    tiles stays in flight across the barrier (cdna_hip_programming.md §5 "Pipelining
+//    across barriers");  no VGPR-destination global load appears in the loop, so hipcc
+//    never drains the ring with a vmcnt(0) of its own;
+//  * W rows are assigned to fragment rows so that every lane ends up holding NT*4
+//    CONSECUTIVE output columns of one row: the epilogue (scale/bias, residual, ReLU,
+//    LayerNorm across the 4 waves through a tiny LDS exchange, row mask, plain or
+//    head-major store) runs straight from the accumulators with 16-byte stores;
+//  * the packed outputs of tile i are stored after the barrier of iteration i+1, behind
+//    the newest DMA, so outstanding stores never hold up the ring's counted wait.
+#include <hip/hip_runtime.h>
+
+#include "../../include/kinet_gemm.h"
+#include "common.h"
+#include "gemm_common.h"
+
+namespace kinet {
+namespace {
+
+template <int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2>
+struct RwCfg {
+    static constexpr int ROW = KC * 64;                     // A row bytes (K = 32*KC, 16-bit)
+    static constexpr int CPR = ROW / 16;                    // 16-byte chunks per A row
+    static constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;   // source-side XOR swizzle mask
+    static constexpr int GW = 4 * NT * 16;                  // columns per workgroup
+    static constexpr int A_BYTES = BMR * ROW;
+    static constexpr int A2_BYTES = HAS_A2 ? A_BYTES : 0;   // second A operand (A + A2)
+    static constexpr int R_ROW = GW * 2;
+    static constexpr int R_CPR = R_ROW / 16;
+    static constexpr int R_SWM = (R_CPR < 16 ? R_CPR : 16) - 1;
+    static constexpr int R_BYTES = HAS_R ? BMR * R_ROW : 0;
+    static constexpr int R_OFF = A_BYTES + A2_BYTES;
+    static constexpr int MASK_OFF = R_OFF + R_BYTES;
+    static constexpr int STAGE = MASK_OFF + 1024;           // + one DMA of row-mask bytes
+    static constexpr int PAR = 4 * GW * 4;                  // scale, bias, gamma, beta (f32)
+    static constexpr int LNS = LN ? 2 * BMR * 4 * 4 : 0;    // [2][BMR][4 waves] partial sums
+    static constexpr int BYTES = PAR + LNS + NS * STAGE;
+    static constexpr int A_OPS = A_BYTES / 4096;            // DMA instructions per thread per tile
+    static constexpr int R_OPS = R_BYTES / 4096;
+    static constexpr int D = A_OPS * (HAS_A2 ? 2 : 1) + R_OPS + 1;
+    static_assert(A_BYTES % 4096 == 0 && R_BYTES % 4096 == 0, "whole DMA rounds per tile");
+    static_assert((CPR & (CPR - 1)) == 0 && (R_CPR & (R_CPR - 1)) == 0, "power-of-two rows");
+    static_assert(BMR / 16 <= 64, "mask DMA lanes");
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// raw workgroup barrier for LDS traffic only: unlike __syncthreads() it does not drain the
+// vector-memory counter, so LDS-DMA issued earlier stays in flight across it
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <typename TO> struct Pack;
+template <> struct Pack<bf16_t> {
+    static constexpr int WORDS_PER_4 = 2;
+    __device__ static void put(uint32_t* w, const float* v) {
+        w[0] = (uint32_t)f32_to_bf16(v[0]).x | ((uint32_t)f32_to_bf16(v[1]).x << 16);
+        w[1] = (uint32_t)f32_to_bf16(v[2]).x | ((uint32_t)f32_to_bf16(v[3]).x << 16);
+    }
+};
+template <> struct Pack<f16_t> {
+    static constexpr int WORDS_PER_4 = 2;
+    __device__ static void put(uint32_t* w, const float* v) {
+        const f16_t a = (f16_t)v[0], b = (f16_t)v[1], c = (f16_t)v[2], d = (f16_t)v[3];
+        w[0] = (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+        w[1] = (uint32_t)__builtin_bit_cast(uint16_t, c) | ((uint32_t)__builtin_bit_cast(uint16_t, d) << 16);
+    }
+};
+template <> struct Pack<float> {
+    static constexpr int WORDS_PER_4 = 4;
+    __device__ static void put(uint32_t* w, const float* v) {
+        for (int i = 0; i < 4; ++i) w[i] = __float_as_uint(v[i]);
+    }
+};
+
+__device__ __forceinline__ void unpack8(const u32x4& u, float* v, bool f16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (f16) {
+            v[2 * i] = (float)__builtin_bit_cast(f16_t, (uint16_t)(u[i] & 0xffffu));
+            v[2 * i + 1] = (float)__builtin_bit_cast(f16_t, (uint16_t)(u[i] >> 16));
+        } else {
+            v[2 * i] = __uint_as_float(u[i] << 16);
+            v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+        }
+    }
+}
+
+template <typename T, typename TO, int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2>
+__global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const int n_mtiles) {
+    using C_ = RwCfg<KC, NT, BMR, NS, HAS_R, LN, HAS_A2>;
+    constexpr int TMR = BMR / 16;             // 16-row MFMA tiles per row tile
+    constexpr int GW = C_::GW;
+    constexpr int NC = NT * 4;                // consecutive columns per lane
+    constexpr int PW = NC / 4 * Pack<TO>::WORDS_PER_4;   // packed 32-bit words per lane-row
+    constexpr unsigned OOB = 0x80000000u;
+    __shared__ __attribute__((aligned(16))) char lds[C_::BYTES];
+    float* par = reinterpret_cast<float*>(lds);
+    float* lns = reinterpret_cast<float*>(lds + C_::PAR);
+    char* stages = lds + C_::PAR + C_::LNS;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int P = gridDim.x, bx = blockIdx.x;
+    const int ncol0 = blockIdx.y * GW;
+    const int M = p.M, N = p.N;
+    const int cnt = bx < n_mtiles ? (n_mtiles - 1 - bx) / P + 1 : 0;
+
+    for (int i = tid; i < GW; i += 256) {
+        const int n = ncol0 + i;
+        const bool ok = n < N;
+        par[i] = (ok && p.scale) ? p.scale[n] : 1.f;
+        par[GW + i] = (ok && p.bias) ? p.bias[n] : 0.f;
+        par[2 * GW + i] = (LN && ok) ? p.ln_g[n] : 0.f;
+        par[3 * GW + i] = (LN && ok) ? p.ln_b[n] : 0.f;
+    }
+
+    // this wave's W slice as MFMA A-fragments: fragment row i of n-tile a is output column
+    // ncol0 + wave*NC*4 + (i>>2)*NC + a*4 + (i&3), so lane group g = lane>>4 of the result
+    // holds columns [g*NC, g*NC + NC) of the wave's range -- NC consecutive columns
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
+    u32x4 wf[NT][KC];
+    {
+        const int i = lane & 15;
+#pragma unroll
+        for (int a = 0; a < NT; ++a) {
+            const int n = ncol0 + wave * NC * 4 + (i >> 2) * NC + a * 4 + (i & 3);
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+                const unsigned off = n < N ? ((unsigned)n * (unsigned)p.ldb + (unsigned)(c * 32 + (lane >> 4) * 8)) * 2u : OOB;
+                wf[a][c] = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0);
+            }
+        }
+    }
+
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra2 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(HAS_A2 ? p.A2 : p.A), (short)0, p.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(HAS_R ? p.R : p.A), (short)0, HAS_R ? p.r_bytes : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rm =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(p.row_mask ? (const void*)p.row_mask : p.A), (short)0,
+                                          p.row_mask ? M : 0, 0x00020000);
+
+    auto issue = [&](int i) {
+        const int m0 = (bx + i * P) * BMR;
+        char* st = stages + (i % NS) * C_::STAGE;
+#pragma unroll
+        for (int j = 0; j < C_::A_OPS; ++j) {
+            const int idx = j * 256 + tid;
+            const int row = idx / C_::CPR, s = idx % C_::CPR;
+            const int q = s ^ (row & C_::SWM);
+            const int m = m0 + row;
+            const unsigned off = m < M ? ((unsigned)m * (unsigned)p.lda + (unsigned)(q * 8)) * 2u : OOB;
+            dma16(ra, st + (j * 256 + wave * 64) * 16, off);
+            if (HAS_A2) dma16(ra2, st + C_::A_BYTES + (j * 256 + wave * 64) * 16, off);
+        }
+#pragma unroll
+        for (int j = 0; j < C_::R_OPS; ++j) {
+            const int idx = j * 256 + tid;
+            const int row = idx / C_::R_CPR, s = idx % C_::R_CPR;
+            const int q = s ^ (row & C_::R_SWM);
+            const int m = m0 + row, n = ncol0 + q * 8;
+            const unsigned off = (m < M && n < N) ? ((unsigned)m * (unsigned)p.ldr + (unsigned)n) * 2u : OOB;
+            dma16(rr, st + C_::R_OFF + (j * 256 + wave * 64) * 16, off);
+        }
+        // row-mask bytes m0 .. m0+BMR (every wave writes the same 1 KiB; bytes past M read 0)
+        dma16(rm, st + C_::MASK_OFF, lane < TMR ? (unsigned)(m0 + lane * 16) : OOB);
+    };
+
+    __syncthreads();   // parameters visible; no DMA in flight yet
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < cnt) issue(s);
+
+    const int cl0 = wave * NC * 4 + (lane >> 4) * NC;   // this lane's first column in the group
+    uint32_t pend[TMR][PW];
+    int pend_m0 = 0;
+    auto store_pending = [&]() {
+        TO* __restrict__ C = (TO*)p.C;
+        constexpr int EPC16 = 16 / (int)sizeof(TO);     // elements per 16-byte store
+#pragma unroll
+        for (int t = 0; t < TMR; ++t) {
+            const int m = pend_m0 + t * 16 + (lane & 15);
+            if (m >= M) continue;
+#pragma unroll
+            for (int h = 0; h < NC / EPC16; ++h) {
+                const int n = ncol0 + cl0 + h * EPC16;
+                if (n >= N) continue;
+                TO* dst;
+                if (p.hm_rows) {
+                    const int bb = m / p.hm_rows, ss = m - bb * p.hm_rows;
+                    const int g = n / p.hm_d, dd = n - g * p.hm_d;
+                    dst = C + (((long)g * p.hm_batch + bb) * p.hm_rows + ss) * p.hm_d + dd;
+                } else {
+                    dst = C + (long)m * p.ldc + n;
+                }
+                *reinterpret_cast<u32x4*>(dst) =
+                    u32x4{pend[t][4 * h], pend[t][4 * h + 1], pend[t][4 * h + 2], pend[t][4 * h + 3]};
+            }
+        }
+    };
+
+    for (int i = 0; i < cnt; ++i) {
+        // retire tile i's DMA: loads issued after it are the (NS-2) later tiles' D each
+        if (i + NS - 2 < cnt) wait_vmcnt<(NS - 2) * C_::D>();
+        else wait_vmcnt<0>();
+        lds_barrier();
+        if (i > 0) store_pending();
+        if (i + NS - 1 < cnt) issue(i + NS - 1);
+
+        const char* st = stages + (i % NS) * C_::STAGE;
+        const int m0 = (bx + i * P) * BMR;
+        f32x4 acc[NT][TMR];
+#pragma unroll
+        for (int a = 0; a < NT; ++a)
+#pragma unroll
+            for (int t = 0; t < TMR; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < KC; ++c)
+#pragma unroll
+            for (int t = 0; t < TMR; ++t) {
+                const int row = t * 16 + (lane & 15);
+                const int q = c * 4 + (lane >> 4);
+                const int xo = row * C_::ROW + ((q ^ (row & C_::SWM)) << 4);
+                u32x4 xf = *reinterpret_cast<const u32x4*>(st + xo);
+                // q = src + pos rounded to the operand type, exactly as gemm.hip's load-time add
+                if (HAS_A2) xf = Mma<T>::add(xf, *reinterpret_cast<const u32x4*>(st + C_::A_BYTES + xo));
+#pragma unroll
+                for (int a = 0; a < NT; ++a) Mma<T>::run(acc[a][t], wf[a][c], xf);
+            }
+
+        // ---- epilogue (registers) ----
+        float v[TMR][NC];
+#pragma unroll
+        for (int t = 0; t < TMR; ++t) {
+            const int rl = t * 16 + (lane & 15);
+#pragma unroll
+            for (int j = 0; j < NC; ++j)
+                v[t][j] = acc[j >> 2][t][j & 3] * par[cl0 + j] + par[GW + cl0 + j];
+            if (HAS_R) {
+#pragma unroll
+                for (int h = 0; h < NC / 8; ++h) {
+                    const int q = (cl0 >> 3) + h;
+                    const u32x4 u = *reinterpret_cast<const u32x4*>(st + C_::R_OFF + rl * C_::R_ROW +
+                                                                    ((q ^ (rl & C_::R_SWM)) << 4));
+                    float r8[8];
+                    unpack8(u, r8, std::is_same<TO, f16_t>::value);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[t][h * 8 + e] += r8[e];
+                }
+            }
+            if (p.relu)
+#pragma unroll
+                for (int j = 0; j < NC; ++j) v[t][j] = fmaxf(v[t][j], 0.f);
+        }
+        if (LN) {
+            // columns past N are exactly 0 here (zero W rows, zero bias, zero residual)
+            float mean[TMR], rstd[TMR];
+#pragma unroll
+            for (int t = 0; t < TMR; ++t) {
+                float s = 0.f;
+#pragma unroll
+                for (int j = 0; j < NC; ++j) s += v[t][j];
+                s += __shfl_xor(s, 16);
+                s += __shfl_xor(s, 32);
+                if ((lane >> 4) == 0) lns[(t * 16 + (lane & 15)) * 4 + wave] = s;
+            }
+            lds_barrier();
+#pragma unroll
+            for (int t = 0; t < TMR; ++t) {
+                const f32x4 w4 = *reinterpret_cast<const f32x4*>(lns + (t * 16 + (lane & 15)) * 4);
+                mean[t] = (w4[0] + w4[1] + w4[2] + w4[3]) / (float)N;
+                float q = 0.f;
+#pragma unroll
+                for (int j = 0; j < NC; ++j) {
+                    const float d = (ncol0 + cl0 + j < N) ? v[t][j] - mean[t] : 0.f;
+                    q += d * d;
+                }
+                q += __shfl_xor(q, 16);
+                q += __shfl_xor(q, 32);
+                if ((lane >> 4) == 0) lns[BMR * 4 + (t * 16 + (lane & 15)) * 4 + wave] = q;
+            }
+            lds_barrier();
+#pragma unroll
+            for (int t = 0; t < TMR; ++t) {
+                const f32x4 w4 = *reinterpret_cast<const f32x4*>(lns + BMR * 4 + (t * 16 + (lane & 15)) * 4);
+                rstd[t] = rsqrtf((w4[0] + w4[1] + w4[2] + w4[3]) / (float)N + p.ln_eps);
+#pragma unroll
+                for (int j = 0; j < NC; ++j)
+                    v[t][j] = (v[t][j] - mean[t]) * rstd[t] * par[2 * GW + cl0 + j] + par[3 * GW + cl0 + j];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < TMR; ++t) {
+            const int rl = t * 16 + (lane & 15);
+            if (st[C_::MASK_OFF + rl])
+#pragma unroll
+                for (int j = 0; j < NC; ++j) v[t][j] = 0.f;
+#pragma unroll
+            for (int j4 = 0; j4 < NC / 4; ++j4) Pack<TO>::put(&pend[t][j4 * Pack<TO>::WORDS_PER_4], &v[t][j4 * 4]);
+        }
+        pend_m0 = m0;
+    }
+    if (cnt > 0) store_pending();
+}
+
+template <typename T, typename TO, int KC, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2 = false>
+void launch_cfg(const GemmArgs& a, hipStream_t stream) {
+    constexpr int GW = 256;
+    const int n_mtiles = (a.M + BMR - 1) / BMR;
+    const int ng = (a.N + GW - 1) / GW;
+    int P = (512 / ng + 7) / 8 * 8;           // 2 resident workgroups per CU over all groups
+    if (P > n_mtiles) P = n_mtiles;
+    dim3 grid(P, ng), block(256);
+    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, 4, BMR, NS, HAS_R, LN, HAS_A2>), grid, block, 0, stream, a, n_mtiles);
+}
+
+template <typename T, typename TO, int KC>
+void launch_k(const GemmArgs& a, hipStream_t stream) {
+    const bool r = a.R != nullptr, ln = a.ln_g != nullptr;
+    // LDS per workgroup <= 80 KiB (two per CU): A 16 KiB + R 16 KiB per 32-row tile at
+    // K = 256; the LayerNorm epilogue at K = 256 needs 16-row tiles to stay in 256 VGPRs
+    constexpr int BL = KC == 8 ? 16 : 32;
+    if (a.A2 != nullptr) {
+        // the query + position-embedding projections (no residual / LayerNorm there)
+        if (r || ln) return;
+        launch_cfg<T, TO, KC, 32, 2, false, false, true>(a, stream);
+    } else if (r && ln) launch_cfg<T, TO, KC, BL, 4, true, true>(a, stream);
+    else if (r) launch_cfg<T, TO, KC, 32, 2, true, false>(a, stream);
+    else if (ln) launch_cfg<T, TO, KC, BL, 4, false, true>(a, stream);
+    else launch_cfg<T, TO, KC, 32, 4, false, false>(a, stream);
+}
+
+template <typename T, typename TO>
+void launch_t(const GemmArgs& a, hipStream_t stream) {
+    if (a.K == 64) launch_k<T, TO, 2>(a, stream);
+    else if (a.K == 128) launch_k<T, TO, 4>(a, stream);
+    else launch_k<T, TO, 8>(a, stream);
+}
+
+bool al16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
+
+}  // namespace
+
+// Entry from gemm.hip's dispatcher: launch the resident-weight kernel when the problem
+// fits it; false leaves the call to the tiled kernel.
+bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t stream) {
+    if (in_dtype != KINET_BF16 && in_dtype != KINET_F16) return false;
+    if (a.M < 4096 || (a.K != 64 && a.K != 128 && a.K != 256)) return false;
+    if (a.A2 != nullptr && (a.R != nullptr || a.ln_g != nullptr || !al16(a.A2))) return false;
+    if (a.N % 8 != 0 || (a.ln_g != nullptr && a.N > 256)) return false;
+    const bool o16 = out_dtype == in_dtype, o32 = out_dtype == KINET_F32;
+    if (!o16 && !o32) return false;
+    if (o16 ? (a.ldc % 8 != 0) : (a.ldc % 4 != 0)) return false;
+    if (!al16(a.C) || (a.R != nullptr && (!o16 || a.ldr % 8 != 0 || !al16(a.R)))) return false;
+    if (a.hm_rows && a.hm_d % 8 != 0) return false;
+    if (in_dtype == KINET_BF16) {
+        if (o16) launch_t<bf16_t, bf16_t>(a, stream);
+        else launch_t<bf16_t, float>(a, stream);
+    } else {
+        if (o16) launch_t<f16_t, f16_t>(a, stream);
+        else launch_t<f16_t, float>(a, stream);
+    }
+    return true;
+}
+
+}  // namespace kinet

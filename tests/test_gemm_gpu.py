@@ -227,3 +227,103 @@ def test_big_conv_vs_fp32(K, big, B, H, W, Cin, Cout, k, s, p):
     assert y.shape[0] * y.shape[1] * y.shape[2] >= 16384        # really on the big-tile path
     err = (y.permute(0, 3, 1, 2).float().cpu() - y_ref).abs()
     assert (err <= 1e-2 * y_ref.abs() + 2e-2).all(), err.max().item()
+
+
+# ---- resident-weight streaming kernel (gemm_rw.hip: 16-bit, K in {64, 128, 256}, M >= 4096) ----
+
+def _rw_case(M, N, Kd, mode, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(M, Kd, generator=g).bfloat16()
+    x2 = torch.randn(M, Kd, generator=g).bfloat16()
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).bfloat16()
+    b = torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g).bfloat16()
+    mask = torch.rand(M, generator=g) < 0.1
+    gam, bet = torch.rand(N, generator=g) + 0.5, torch.randn(N, generator=g)
+    xin = (x.float() + x2.float()).bfloat16() if 'add' in mode else x
+    ref = F.linear(xin.float(), w.float(), b)
+    kw = {}
+    if 'res' in mode:
+        ref = ref + r.float()
+        kw['residual'] = r.cuda()
+    if 'relu' in mode:
+        ref = F.relu(ref)
+        kw['relu'] = True
+    if 'ln' in mode:
+        ref = F.layer_norm(ref, (N,), gam, bet, 1e-5)
+        kw['ln'] = (gam.cuda(), bet.cuda(), 1e-5)
+    if 'mask' in mode:
+        ref = ref.masked_fill(mask[:, None], 0)
+        kw['row_mask'] = mask.cuda()
+    if 'add' in mode:
+        kw['x_add'] = x2.cuda()
+    if 'f32' in mode:
+        kw['out_dtype'] = torch.float32
+    return x, w, b, kw, ref
+
+
+@pytest.mark.parametrize('M,N,Kd,mode', [
+    (8192, 256, 256, 'plain'), (10001, 256, 256, 'res_ln'), (9999, 256, 256, 'ln_mask'),
+    (12345, 1024, 256, 'relu'), (8200, 384, 256, 'add_f32'), (8200, 384, 256, 'add'),
+    (8197, 200, 256, 'res_ln'), (8197, 200, 128, 'relu_mask'), (16800, 256, 64, 'res_relu'),
+    (16800, 512, 128, 'res'), (5000, 64, 64, 'plain'), (4099, 1032, 256, 'f32'),
+    (20001, 256, 256, 'res_relu_mask'),
+])
+def test_rw_gemm_vs_fp32(K, M, N, Kd, mode):
+    x, w, b, kw, ref = _rw_case(M, N, Kd, mode, M + N + Kd)
+    y = K.linear(x.cuda(), w.cuda(), b.cuda(), **kw)
+    torch.cuda.synchronize()
+    assert y.dtype == (torch.float32 if 'f32' in mode else torch.bfloat16)
+    err = (y.float().cpu() - ref).abs()
+    tol = (1e-4 * ref.abs() + 2e-3) if 'f32' in mode else (1e-2 * ref.abs() + 2e-2)
+    assert (err <= tol).all(), err.max().item()
+
+
+@pytest.mark.parametrize('M,N,Kd,mode', [(10001, 256, 256, 'res_ln_mask'), (12345, 1024, 256, 'relu'),
+                                         (8200, 384, 256, 'add_f32'), (16800, 256, 64, 'res_relu')])
+def test_rw_matches_tiled_kernel(K, gemm_flags, M, N, Kd, mode):
+    """Same bf16 products summed in the same K order in f32: the two kernels agree to
+    (nearly) the last bit."""
+    x, w, b, kw, _ = _rw_case(M, N, Kd, mode, 7)
+    args = (x.cuda(), w.cuda(), b.cuda())
+    gemm_flags(0)
+    y_rw = K.linear(*args, **kw)
+    gemm_flags(4)
+    y_tiled = K.linear(*args, **kw)
+    torch.cuda.synchronize()
+    d = (y_rw.float() - y_tiled.float()).abs()
+    tol = y_tiled.float().abs() * 2.0 ** -7 + 1e-5
+    assert (d <= tol).all(), d.max().item()
+    assert (d == 0).float().mean().item() > 0.9
+
+
+def test_rw_headmajor_value_proj(K):
+    B, S, d, hd = 2, 4500, 256, 32
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(B, S, d, generator=g).bfloat16()
+    w = (torch.randn(d, d, generator=g) / 16).bfloat16()
+    b = torch.randn(d, generator=g)
+    mask = torch.rand(B, S, generator=g) < 0.2
+    ref = F.linear(x.float(), w.float(), b).masked_fill(mask[..., None], 0)
+    ref = ref.view(B, S, d // hd, hd).permute(2, 0, 1, 3)
+    y = K.value_proj_headmajor(x.cuda(), w.cuda(), b.cuda(), hd, row_mask=mask.cuda())
+    torch.cuda.synchronize()
+    err = (y.float().cpu() - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
+
+
+@pytest.mark.parametrize('Cin,Cout', [(64, 256), (256, 64), (128, 512), (256, 1024)])
+def test_rw_conv1x1(K, Cin, Cout):
+    B, H, W = 4, 60, 70
+    g = torch.Generator().manual_seed(Cin + Cout)
+    x = torch.randn(B, Cin, H, W, generator=g).bfloat16()
+    w = (torch.randn(Cout, Cin, 1, 1, generator=g) * (2.0 / Cin) ** 0.5).bfloat16()
+    scale = torch.rand(Cout, generator=g) + 0.5
+    bias = torch.randn(Cout, generator=g) * 0.1
+    res = torch.randn(B, Cout, H, W, generator=g).bfloat16()
+    ref = F.relu(F.conv2d(x.float(), w.float()) * scale[None, :, None, None] + bias[None, :, None, None] + res.float())
+    y = K.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().cuda(), K.pack_conv_weight(w.cuda(), torch.bfloat16), 1, 0,
+                      scale=scale.cuda(), bias=bias.cuda(), relu=True, residual=res.permute(0, 2, 3, 1).contiguous().cuda())
+    torch.cuda.synchronize()
+    err = (y.permute(0, 3, 1, 2).float().cpu() - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()

@@ -83,6 +83,10 @@ def model():
 
 if __name__ == '__main__':
     which = sys.argv[1:] or ['gemm', 'model']
+    if 'norw' in which:    # never use the resident-weight streaming kernel
+        from kinet_amd import _native
+        _native.lib().kinet_gemm_set_flags(4)
+        print('[bench_kernels] GEMM flags = 4 (no resident-weight kernel)')
     if 'big' in which:     # allow the 512-thread 256x256-tile LDS-DMA kernel
         from kinet_amd import _native
         _native.lib().kinet_gemm_set_flags(2)
