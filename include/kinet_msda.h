@@ -73,6 +73,10 @@ int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num
  * Launch: one head per wave, 64/(D/vec) consecutive queries per wave.
  * Writes output (N, Lq, M*D) and, when loc_out/attw_out are non-NULL, the f32
  * sampling_loc / attn_weight tensors (needed to run kinet_msda_backward). */
+/* Diagnostic kernel-selection knob (no reference counterpart): bit 0 = never use the
+ * specialised 16-bit / head_dim-32 fused kernel.  Returns the previous flags. */
+int kinet_msda_set_flags(int flags);
+
 int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_ss, int64_t value_sm,
                              const int64_t* spatial_shapes,
                              const void* offsets_logits, int ld_off,

@@ -33,6 +33,9 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxLevels = 16;
 
+// diagnostic flags (kinet_msda_set_flags): bit 0 = never use msda_fused_fast_kernel
+int msda_flags = 0;
+
 template <typename T, int VEC>
 struct alignas(sizeof(T) * VEC) VecT {
     T v[VEC];
@@ -457,6 +460,191 @@ __global__ __launch_bounds__(kThreads) void msda_fused_kernel(
 }
 
 // ---------------------------------------------------------------------------------
+// fused module forward, specialised: 16-bit values, head_dim 32, L and P compile-time
+// ---------------------------------------------------------------------------------
+// Same decomposition and results contract as msda_fused_kernel (one head per wave, 16
+// queries x 4 lanes x 8 channels), rebuilt around what bounds it on gfx950 -- VALU issue,
+// not memory (rocprofv3: ~2.3k VALU wave-instructions per wave for ~80 loads):
+//  * the sample index split (head, query, level, point) is shifts on compile-time sizes,
+//    not runtime integer division;
+//  * the per-level normalisers are reciprocals staged in LDS (one multiply instead of an
+//    IEEE divide), the softmax divides through one reciprocal;
+//  * taps are byte offsets for raw buffer loads off a per-wave head-map descriptor: an
+//    out-of-image corner gets an offset past num_records and the hardware returns 0, so
+//    there is neither a per-corner branch nor 64-bit address arithmetic;
+//  * the 4-corner x 8-channel accumulation runs as v_pk_fma_f32 on bf16 pairs widened by
+//    one shift / one mask.
+struct FastLevels {
+    int start[kMaxLevels], H[kMaxLevels], W[kMaxLevels], ok[kMaxLevels];
+    float Hf[kMaxLevels], Wf[kMaxLevels], rH[kMaxLevels], rW[kMaxLevels];
+};
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ void widen2(uint32_t u, f32x2& x) {
+    if constexpr (std::is_same<T, f16_t>::value) {
+        x = f32x2{(float)__builtin_bit_cast(f16_t, (uint16_t)(u & 0xffffu)), (float)__builtin_bit_cast(f16_t, (uint16_t)(u >> 16))};
+    } else {
+        x = f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+    }
+}
+
+// max / sum over each aligned group of G lanes (G = 2..64), result in every lane: DPP
+// butterflies inside a 16-lane row (quad_perm xor1, xor2, half-mirror, mirror -- each pairs
+// lanes of the two halves of the previous group), cross-row steps by swizzle / bpermute.
+template <bool MAX>
+__device__ __forceinline__ float combine(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
+
+template <int G, bool MAX>
+__device__ __forceinline__ float group_reduce(float x) {
+    static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "group size");
+    auto dpp = [](float v, auto ctrl) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), decltype(ctrl)::value, 0xf, 0xf, false));
+    };
+    if constexpr (G >= 2) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0xB1>{}));    // quad_perm [1,0,3,2]
+    if constexpr (G >= 4) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0x4E>{}));    // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0x141>{}));   // row_half_mirror
+    if constexpr (G >= 16) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0x140>{}));  // row_mirror
+    if constexpr (G >= 32) x = combine<MAX>(x, __shfl_xor(x, 16));
+    if constexpr (G >= 64) x = combine<MAX>(x, __shfl_xor(x, 32));
+    return x;
+}
+
+template <typename T, int L, int P>
+__global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
+    const T* __restrict__ value, long vsb, int vss, long vsm, int head_bytes, const int64_t* __restrict__ shapes,
+    const float* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
+    const uint8_t* __restrict__ qmask, float* __restrict__ loc_out, float* __restrict__ attw_out,
+    T* __restrict__ out, int S, int M, int Lq) {
+    static_assert(sizeof(T) == 2, "16-bit values");
+    constexpr int D = 32, QT = 16, MH = kThreads / 64, LP = L * P;
+    static_assert((LP & (LP - 1)) == 0 && LP <= 64 && L <= kMaxLevels, "L*P: power of two <= 64");
+    constexpr int NSB = MH * QT * LP;               // samples per workgroup
+    constexpr unsigned OOB = 0x80000000u;
+    __shared__ FastLevels lv;
+    __shared__ Tap4 taps[NSB];
+    const int b = blockIdx.y, q0 = blockIdx.x * QT, mh0 = blockIdx.z * MH;
+    if (threadIdx.x == 0) {
+        long long acc = 0;
+        for (int l = 0; l < L; ++l) {
+            const long long H = shapes[2 * l], W = shapes[2 * l + 1];
+            lv.start[l] = (int)acc;
+            lv.H[l] = (int)H;
+            lv.W[l] = (int)W;
+            lv.ok[l] = (H > 0 && W > 0 && acc + H * W <= S) ? 1 : 0;
+            lv.Hf[l] = (float)H;
+            lv.Wf[l] = (float)W;
+            lv.rH[l] = H > 0 ? 1.f / (float)H : 0.f;
+            lv.rW[l] = W > 0 ? 1.f / (float)W : 0.f;
+            acc += H * W;
+        }
+    }
+    __syncthreads();
+
+    const int rowb = vss * (int)sizeof(T);           // bytes between pixels of one head map
+#pragma unroll
+    for (int i = 0; i < NSB / kThreads; ++i) {
+        const int s = threadIdx.x + kThreads * i;
+        const int ml = s / (QT * LP), qi = (s / LP) % QT, lp = s % LP, l = lp / P;
+        const int m = mh0 + ml, q = q0 + qi;
+        const bool ok = q < Lq && m < M;
+        const float* orow = offlog + ((long)b * Lq + (ok ? q : 0)) * ld_off;
+        // softmax over the LP consecutive lanes of one (query, head) (ms_deform_attn.py:71-72)
+        const float logit = ok ? orow[M * LP * 2 + (ok ? m : 0) * LP + lp] : -INFINITY;
+        const float mx = group_reduce<LP, true>(logit);
+        const float e = ok ? __expf(logit - mx) : 0.f;
+        const float sum = group_reduce<LP, false>(e);
+        float a = ok ? e * __builtin_amdgcn_rcpf(sum) : 0.f;
+        Tap4 t4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { t4.off[k] = (int)OOB; t4.w[k] = 0.f; }
+        if (ok) {
+            if (qmask && qmask[(long)b * Lq + q]) a = 0.f;                  // ms_deform_attn.py:73-74
+            const float2 o2 = *reinterpret_cast<const float2*>(orow + (m * LP + lp) * 2);
+            const float* rp = ref + (((long)b * Lq + q) * L + l) * ref_dim;
+            float x, y;
+            if (ref_dim == 2) {   // offsets / spatial_shapes[(H, W)] on (x, y): the reference's quirk (:77-79)
+                x = rp[0] + o2.x * lv.rH[l];
+                y = rp[1] + o2.y * lv.rW[l];
+            } else {              // :80-82
+                x = rp[0] + o2.x * (0.5f / (float)P) * rp[2];
+                y = rp[1] + o2.y * (0.5f / (float)P) * rp[3];
+            }
+            if (loc_out) {
+                const long gi = (((long)b * Lq + q) * M + m) * LP + lp;
+                loc_out[2 * gi] = x;
+                loc_out[2 * gi + 1] = y;
+                attw_out[gi] = a;
+            }
+            const int H = lv.H[l], W = lv.W[l];
+            const float h = y * lv.Hf[l] - 0.5f, w = x * lv.Wf[l] - 0.5f;   // cuh:227-228
+            if (lv.ok[l] && h > -1.f && w > -1.f && h < lv.Hf[l] && w < lv.Wf[l]) {   // cuh:229
+                const float hf = floorf(h), wf = floorf(w);
+                const int hl = (int)hf, wl = (int)wf;
+                const float lh = h - hf, lw = w - wf, hh = 1.f - lh, hw = 1.f - lw;
+                const bool h0 = hl >= 0, h1 = hl + 1 < H, c0 = wl >= 0, c1 = wl + 1 < W;
+                const int o00 = (lv.start[l] + hl * W + wl) * rowb;
+                t4.off[0] = (h0 && c0) ? o00 : (int)OOB;
+                t4.off[1] = (h0 && c1) ? o00 + rowb : (int)OOB;
+                t4.off[2] = (h1 && c0) ? o00 + W * rowb : (int)OOB;
+                t4.off[3] = (h1 && c1) ? o00 + W * rowb + rowb : (int)OOB;
+                t4.w[0] = hh * hw * a;
+                t4.w[1] = hh * lw * a;
+                t4.w[2] = lh * hw * a;
+                t4.w[3] = lh * lw * a;
+            }
+        }
+        taps[s] = t4;
+    }
+    __syncthreads();
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int m = mh0 + wave;
+    if (m >= M) return;
+    const int qi = lane >> 2, q = q0 + qi;
+    const unsigned cb = (unsigned)(lane & 3) * 16u;   // this lane's 8 channels, bytes
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(value + (long)b * vsb + (long)m * vsm), (short)0, head_bytes, 0x00020000);
+    const Tap4* tp = taps + (wave * QT + qi) * LP;
+    f32x2 acc[4] = {};
+    constexpr int SG = 4;   // 4 samples x 4 corners = 16 gathers in flight per lane
+#pragma unroll 1
+    for (int s = 0; s < LP; s += SG) {
+        Tap4 t[SG];
+#pragma unroll
+        for (int g = 0; g < SG; ++g) t[g] = tp[s + g];
+        u32x4v v[SG][4];
+#pragma unroll
+        for (int g = 0; g < SG; ++g)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                v[g][k] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)t[g].off[k] + cb, 0, 0));
+#pragma unroll
+        for (int g = 0; g < SG; ++g)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f32x2 w2 = {t[g].w[k], t[g].w[k]};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    f32x2 x;
+                    widen2<T>(v[g][k][j], x);
+                    acc[j] = __builtin_elementwise_fma(x, w2, acc[j]);
+                }
+            }
+    }
+    if (q >= Lq) return;
+    VecT<T, 8> o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        o.v[2 * j] = Cvt<T>::from(acc[j][0]);
+        o.v[2 * j + 1] = Cvt<T>::from(acc[j][1]);
+    }
+    *reinterpret_cast<VecT<T, 8>*>(out + ((long)b * Lq + q) * M * D + (long)m * D + (lane & 3) * 8) = o;
+}
+
+// ---------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------
 template <typename A>
@@ -762,6 +950,24 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
     const Cfg c = pick_cfg(D, M, sizeof(T));
     KINET_CHECK_ARG(c.lpq <= 64, "msda fused: head_dim/vec (%d) exceeds a wave", c.lpq);
     if (N == 0 || Lq == 0) return KINET_OK;
+    if constexpr (sizeof(T) == 2) {
+        // specialised kernel: head_dim 32, (L, P) in {(4, 4), (8, 4)}, 16-byte aligned vectors
+        const long long head_bytes = ((long long)(S - 1) * vss + D) * (long long)sizeof(T);
+        if (D == 32 && P == 4 && (L == 4 || L == 8) && vss % 8 == 0 && vsb % 8 == 0 && vsm % 8 == 0 &&
+            ((uintptr_t)value % 16) == 0 && head_bytes < (1LL << 31) && !(msda_flags & 1)) {
+            dim3 grid((Lq + 15) / 16, N, (M + 3) / 4);
+            if (L == 4)
+                hipLaunchKernelGGL((msda_fused_fast_kernel<T, 4, 4>), grid, dim3(kThreads), 0, stream, (const T*)value, vsb,
+                                   vss, vsm, (int)head_bytes, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out,
+                                   attw_out, (T*)out, S, M, Lq);
+            else
+                hipLaunchKernelGGL((msda_fused_fast_kernel<T, 8, 4>), grid, dim3(kThreads), 0, stream, (const T*)value, vsb,
+                                   vss, vsm, (int)head_bytes, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out,
+                                   attw_out, (T*)out, S, M, Lq);
+            KINET_LAUNCH_CHECK();
+            return KINET_OK;
+        }
+    }
     KINET_CHECK_ARG(vsb % c.vec == 0 && vss % c.vec == 0 && vsm % c.vec == 0 && ((uintptr_t)value % 16) == 0,
                     "msda fused: value strides must keep %d-element vectors aligned", c.vec);
     const int QT = 64 / c.lpq;          // queries per wave (= per workgroup)
@@ -788,6 +994,12 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
 }
 }  // namespace
 }  // namespace kinet
+
+extern "C" int kinet_msda_set_flags(int flags) {
+    const int old = kinet::msda_flags;
+    kinet::msda_flags = flags;
+    return old;
+}
 
 extern "C" int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_ss, int64_t value_sm,
                                         const int64_t* spatial_shapes, const void* offsets_logits, int ld_off,

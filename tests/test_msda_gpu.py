@@ -134,3 +134,66 @@ def test_fused_module_path_matches_reference(golden_dir):
         out4 = mod(t['query'], t['ref4'], t['input_flatten'], t['shapes'], None)
     np.testing.assert_allclose(out2.cpu().numpy(), d['out_ref2_masked'], atol=1e-3, rtol=0)
     np.testing.assert_allclose(out4.cpu().numpy(), d['out_ref4'], atol=1e-3, rtol=0)
+
+
+# ---- specialised fused kernel (16-bit values, head_dim 32, L*P in {16, 32}) vs the generic one ----
+
+def _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, seed, dtype=torch.bfloat16):
+    g = torch.Generator().manual_seed(seed)
+    L = len(shapes)
+    S = sum(h * w for h, w in shapes)
+    value = torch.randn(M, B, S, 32, generator=g).to(dtype)
+    ref = torch.rand(B, Lq, L, ref_dim, generator=g)
+    if ref_dim == 4:
+        ref[..., 2:] = ref[..., 2:] * 0.5 + 0.05
+    off = noise * torch.randn(B, Lq, M * L * P * 2, generator=g)
+    logits = torch.randn(B, Lq, M * L * P, generator=g)
+    offlog = torch.cat([off, logits], -1)
+    qmask = torch.rand(B, Lq, generator=g) < 0.1
+    ss = torch.tensor(shapes, dtype=torch.int64)
+    return [t.cuda() for t in (value, ss, offlog, ref, qmask)]
+
+
+@pytest.mark.parametrize('shapes,Lq,ref_dim,noise', [
+    (((40, 50), (20, 25), (10, 13), (5, 7)), 3000, 2, 3.0),    # encoder-like, samples leave the image
+    (((40, 50), (20, 25), (10, 13), (5, 7)), 300, 4, 8.0),     # decoder-like, box references
+    (((23, 31), (12, 16), (6, 8), (3, 4), (23, 31), (12, 16), (6, 8), (3, 4)), 517, 2, 2.0),  # 8 levels (2 frames)
+])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_fast_fused_kernel_matches_generic(shapes, Lq, ref_dim, noise, dtype):
+    from kinet_amd import _native
+    from kinet_amd import kernels as K
+    B, M, P = 2, 8, 4
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, Lq, dtype)
+    L = len(shapes)
+    lib = _native.lib()
+    try:
+        lib.kinet_msda_set_flags(0)
+        out_f, loc_f, aw_f = K.msda_fused(value, ss, offlog, ref, M, L, P, qmask, want_loc_attw=True, head_major=True)
+        lib.kinet_msda_set_flags(1)
+        out_g, loc_g, aw_g = K.msda_fused(value, ss, offlog, ref, M, L, P, qmask, want_loc_attw=True, head_major=True)
+    finally:
+        lib.kinet_msda_set_flags(0)
+    torch.cuda.synchronize()
+    # reciprocal-multiply normalisation / approximate reciprocal in the softmax: a few ulp
+    assert torch.allclose(loc_f, loc_g, rtol=1e-6, atol=1e-6)
+    assert torch.allclose(aw_f, aw_g, rtol=1e-5, atol=1e-7)
+    d = (out_f.float() - out_g.float()).abs()
+    tol = out_g.float().abs() * 2.0 ** -7 + 1e-3
+    assert (d <= tol).all(), d.max().item()
+    assert (out_f.float()[qmask] == 0).all()
+
+
+def test_fast_fused_kernel_vs_oracle():
+    """The specialised kernel against the C oracle (through loc/attw it reports)."""
+    from kinet_amd import kernels as K
+    from oracle import msda_oracle as O
+    shapes = ((40, 50), (20, 25), (10, 13), (5, 7))
+    B, M, P, Lq = 2, 8, 4, 700
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 5)
+    out, loc, aw = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, want_loc_attw=True, head_major=True)
+    torch.cuda.synchronize()
+    v = value.float().permute(1, 2, 0, 3).contiguous().cpu().numpy()          # (B, S, M, D)
+    ref_out = O.fwd(v, ss.cpu().numpy(), loc.cpu().numpy(), aw.cpu().numpy())
+    d = (out.float().cpu() - torch.from_numpy(ref_out).reshape(out.shape)).abs()
+    assert (d <= 1e-2 * torch.from_numpy(ref_out).reshape(out.shape).abs() + 1e-2).all(), d.max().item()
