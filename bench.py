@@ -29,6 +29,10 @@ sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'f16': 2500.0, 'f32': 157.3}   # dense
+# per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command
+# (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950 per MI355X_MICROARCH.md "HBM")
+PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
+MSDA_KERNEL = 'msda_fused_fast_kernel'
 
 
 def parse():
@@ -84,6 +88,17 @@ def summarize_trace(trace, steps_traced=1):
         for k in ('ms', 'flops', 'bytes', 'launches'):
             a[k] /= steps_traced
     return fam, msda
+
+
+def pmc_traffic(kernel):
+    """(bytes per launch, provenance) of `kernel` from the committed PMC summary, or (None, None)."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            d = json.load(f)
+        k = d['kernels'][kernel]
+        return k['hbm_bytes_per_launch'], d.get('source')
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def cpu_baseline(seconds):
@@ -178,25 +193,32 @@ def main():
         dec = [m for m in msda if m[0] != m[1]]
         msda_enc_ms = statistics.mean(m[2] for m in enc) if enc else None
         msda_dec_ms = statistics.mean(m[2] for m in dec) if dec else None
-        enc_bytes = enc[0][3] if enc else None
         mfma_ms = sum(fam[f]['ms'] for f in ('gemm', 'conv') if f in fam)
         mfma_flops = sum(fam[f]['flops'] for f in ('gemm', 'conv') if f in fam)
-        # the dominant kernel family by device time in the traced steps
-        dominant = max(fam.items(), key=lambda kv: kv[1]['ms'])[0]
+        # Headline roofline: the fused MSDA sampling kernel -- the operator this path is
+        # built around and the single kernel with the most device time in the rocprofv3
+        # summary (profiles/) -- over ALL its launches (6 encoder + 6 decoder per frame
+        # batch), so avg_launch_ms is the rocprof average of that kernel name.
         msda_roof = None
-        if enc:
-            ach = enc_bytes / (msda_enc_ms * 1e-3) / 1e9
-            msda_roof = {'bound': 'hbm', 'kernel': 'kinet msda_fwd_kernel (fused, encoder call)',
+        if msda:
+            tot_ms = sum(m[2] for m in msda)
+            tot_bytes = sum(m[3] for m in msda)
+            ach = tot_bytes / (tot_ms * 1e-3) / 1e9
+            traffic, src = pmc_traffic(MSDA_KERNEL)
+            msda_roof = {'bound': 'hbm', 'kernel': MSDA_KERNEL + '<bf16_t, 4, 4> (encoder + decoder launches)',
                          'achieved': ach, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': ach / HBM_PEAK_GBS,
-                         'traffic': None, 'algorithmic_bytes_per_launch': enc_bytes,
-                         'avg_launch_ms': msda_enc_ms}
+                         'traffic': traffic, 'traffic_source': src,
+                         'algorithmic_bytes_per_launch': tot_bytes / len(msda),
+                         'avg_launch_ms': tot_ms / len(msda), 'launches_per_step': len(msda) / 3,
+                         'encoder_launch': {'ms': msda_enc_ms, 'bytes': enc[0][3] if enc else None},
+                         'decoder_launch': {'ms': msda_dec_ms, 'bytes': dec[0][3] if dec else None}}
         mfma_ach = mfma_flops / (mfma_ms * 1e-3) / 1e12 if mfma_ms else 0.0
-        mfma_roof = {'bound': 'mfma', 'kernel': 'kinet gemm_kernel (GEMM + implicit-GEMM conv, all launches)',
+        mfma_roof = {'bound': 'mfma', 'kernel': 'all GEMM + conv launches (gemm_kernel, gemm_rw_kernel)',
                      'achieved': mfma_ach, 'peak': MFMA_PEAK_TFLOPS[dt_name], 'unit': 'TFLOP/s',
                      'frac': mfma_ach / MFMA_PEAK_TFLOPS[dt_name], 'traffic': None,
                      'algorithmic_flops_per_frame': mfma_flops / a.batch,
                      'device_ms_per_step': mfma_ms}
-        roofline = mfma_roof if dominant in ('gemm', 'conv') else (msda_roof or mfma_roof)
+        roofline = msda_roof or mfma_roof
         line = {
             'metric': 'frames/sec (3x800x1333, 300 obj+track queries) at 1/2/4/8 GPUs; MSDeformAttn ms/call',
             'value': value, 'unit': 'frames/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
@@ -208,7 +230,6 @@ def main():
                        'frames_per_gpu_per_step': a.batch, 'frame': [3, a.height, a.width],
                        'parallelism': f'replicas x{world}'},
             'roofline': roofline,
-            'roofline_msda': msda_roof,
             'roofline_mfma': mfma_roof,
             'msda_ms_per_call': {'encoder': msda_enc_ms, 'decoder': msda_dec_ms},
             'device_ms_per_step_by_family': {k: round(v['ms'], 4) for k, v in fam.items()},

@@ -1,6 +1,8 @@
 // Shared helpers for the kinet_amd HIP kernels (gfx950 / CDNA4 only).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -83,6 +85,27 @@ inline size_t dtype_size(int dt) {
         case KINET_F16: return 2;
         default: return 0;
     }
+}
+
+// max / sum over each aligned group of G lanes (G = 2..64), result in every lane: DPP
+// butterflies inside a 16-lane row (quad_perm xor1, xor2, half-mirror, mirror -- each pairs
+// lanes of the two halves of the previous group), cross-row steps by swizzle / bpermute.
+template <bool MAX>
+__device__ __forceinline__ float combine(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
+
+template <int G, bool MAX>
+__device__ __forceinline__ float group_reduce(float x) {
+    static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "group size");
+    auto dpp = [](float v, auto ctrl) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), decltype(ctrl)::value, 0xf, 0xf, false));
+    };
+    if constexpr (G >= 2) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0xB1>{}));    // quad_perm [1,0,3,2]
+    if constexpr (G >= 4) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0x4E>{}));    // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0x141>{}));   // row_half_mirror
+    if constexpr (G >= 16) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0x140>{}));  // row_mirror
+    if constexpr (G >= 32) x = combine<MAX>(x, __shfl_xor(x, 16));
+    if constexpr (G >= 64) x = combine<MAX>(x, __shfl_xor(x, 32));
+    return x;
 }
 
 // number of workgroups that fill the chip for a grid-stride kernel (256 CUs x 8)

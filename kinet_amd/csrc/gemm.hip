@@ -49,17 +49,74 @@ struct Smem {
     static constexpr int BYTES = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
 };
 
-// Fused epilogue over tile rows [r0, r1): the f32 accumulators of those rows are parked
-// in LDS at ep[(row - r0) * EPI_LD + col]; each wave streams whole rows (LPR lanes per row,
-// 4 columns per lane): scale/bias, residual, ReLU, LayerNorm, row mask, plain or
-// head-major store.
-template <typename TO, int BN, int EPI_LD, int NW, bool LN>
-__device__ __forceinline__ void epilogue_rows(const GemmArgs& p, const float* ep, int m0, int n0, int r0, int r1,
-                                              int wave, int lane) {
+// Residual rows of one epilogue pass, loaded ahead: every wave issues the loads of ALL its
+// rows (branch-free buffer loads, zeros past the edges) before the accumulators are parked,
+// so their latency overlaps the park + barrier instead of serialising one HBM round trip per
+// row.  Used when the residual rows are 4-column aligned (ldr % 4 == 0, N % 4 == 0); other
+// shapes fall back to in-loop loads.
+template <typename TO, int BN, int NW, int ROWS>
+struct ResRows {
+    static constexpr int LPR = BN / 4 < 64 ? BN / 4 : 64;
+    static constexpr int NCH = (BN + 4 * LPR - 1) / (4 * LPR);
+    static constexpr int RPW = 64 / LPR;
+    static constexpr int NR = (ROWS + NW * RPW - 1) / (NW * RPW);
+    static constexpr int WPC = 4 * (int)sizeof(TO) / 4;   // 32-bit words per 4-column chunk
+    uint32_t w[NR][NCH][WPC];
+    bool on;
+
+    __device__ __forceinline__ void issue(const GemmArgs& p, int m0, int n0, int r0, int wave, int lane) {
+        on = p.R != nullptr && (p.ldr & 3) == 0 && (p.N & 3) == 0;
+        if (!on) return;
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)p.R, (short)0, p.r_bytes, 0x00020000);
+        const int lr = lane / LPR, lc = lane - (lane / LPR) * LPR;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const int rl = wave * RPW + lr + i * NW * RPW;
+            const int m = m0 + r0 + rl;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                const int nl0 = (c * LPR + lc) * 4, n = n0 + nl0;
+                const bool ok = rl < ROWS && m < p.M && nl0 < BN && n < p.N;
+                const unsigned off = ok ? ((unsigned)m * (unsigned)p.ldr + (unsigned)n) * (unsigned)sizeof(TO) : 0x80000000u;
+                if constexpr (WPC == 4) {
+                    const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
+                    for (int k = 0; k < 4; ++k) w[i][c][k] = v[k];
+                } else {
+                    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                    const u32x2 v = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0));
+                    w[i][c][0] = v[0];
+                    w[i][c][1] = v[1];
+                }
+            }
+        }
+    }
+    __device__ __forceinline__ void get(int i, int c, float* r) const {
+        if constexpr (WPC == 4) {
+            for (int k = 0; k < 4; ++k) r[k] = __uint_as_float(w[i][c][k]);
+        } else if constexpr (std::is_same<TO, f16_t>::value) {
+            for (int k = 0; k < 2; ++k) {
+                r[2 * k] = (float)__builtin_bit_cast(f16_t, (uint16_t)(w[i][c][k] & 0xffffu));
+                r[2 * k + 1] = (float)__builtin_bit_cast(f16_t, (uint16_t)(w[i][c][k] >> 16));
+            }
+        } else {
+            for (int k = 0; k < 2; ++k) {
+                r[2 * k] = __uint_as_float(w[i][c][k] << 16);
+                r[2 * k + 1] = __uint_as_float(w[i][c][k] & 0xffff0000u);
+            }
+        }
+    }
+};
+
+// Fused epilogue over tile rows [r0, r0 + ROWS): the f32 accumulators of those rows are
+// parked in LDS at ep[(row - r0) * EPI_LD + col]; each wave streams whole rows (LPR lanes
+// per row, 4 columns per lane): scale/bias, residual, ReLU, LayerNorm (DPP row reductions),
+// row mask, plain or head-major store.
+template <typename TO, int BN, int EPI_LD, int NW, bool LN, int ROWS>
+__device__ __forceinline__ void epilogue_rows(const GemmArgs& p, const float* ep, int m0, int n0, int r0, int wave,
+                                              int lane, const ResRows<TO, BN, NW, ROWS>& rp) {
+    using RR = ResRows<TO, BN, NW, ROWS>;
     const int M = p.M, N = p.N;
-    constexpr int LPR = BN / 4 < 64 ? BN / 4 : 64;   // lanes per row
-    constexpr int NCH = (BN + 4 * LPR - 1) / (4 * LPR);   // 4-column chunks per lane
-    constexpr int RPW = 64 / LPR;                     // rows per wave pass
+    constexpr int LPR = RR::LPR, NCH = RR::NCH, RPW = RR::RPW;
     static_assert(64 % LPR == 0, "row mapping");
     TO* __restrict__ C = (TO*)p.C;
     const TO* __restrict__ R = (const TO*)p.R;
@@ -77,7 +134,11 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& p, const float* ep
             g4[c][r] = LN ? p.ln_g[nn] : 1.f;
             be4[c][r] = LN ? p.ln_b[nn] : 0.f;
         }
-    for (int rr = r0 + wave * RPW + lr; rr < r1; rr += NW * RPW) {
+#pragma unroll
+    for (int i = 0; i < RR::NR; ++i) {
+        const int rl = wave * RPW + lr + i * NW * RPW;
+        if (RR::NR * NW * RPW > ROWS && rl >= ROWS) break;   // (wave-uniform: ROWS % RPW == 0)
+        const int rr = r0 + rl;
         const int m = m0 + rr;
         // (LN needs every lane of the row in the reductions, so no early exit on m)
         const bool mok = m < M;
@@ -89,9 +150,11 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& p, const float* ep
             const int n = n0 + nl0;
             const bool cin = nl0 < BN;
             f32x4 t = {0.f, 0.f, 0.f, 0.f};
-            if (cin) t = *reinterpret_cast<const f32x4*>(ep + (rr - r0) * EPI_LD + nl0);
+            if (cin) t = *reinterpret_cast<const f32x4*>(ep + rl * EPI_LD + nl0);
             float res[4] = {0.f, 0.f, 0.f, 0.f};
-            if (R && mok && cin && n < N) {
+            if (rp.on) {
+                rp.get(i, c, res);
+            } else if (R && mok && cin && n < N) {
                 if (ld_ok && n + 3 < N) IO4<TO>::load(R + (long)m * p.ldr + n, res);
                 else
                     for (int r = 0; r < 4; ++r)
@@ -107,8 +170,7 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& p, const float* ep
             }
         }
         if (LN) {
-#pragma unroll
-            for (int o = LPR >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            s = group_reduce<LPR, false>(s);
             const float mean = s / (float)N;
             float q = 0.f;
 #pragma unroll
@@ -119,8 +181,7 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& p, const float* ep
                     const float d = ((c * LPR + lc) * 4 < BN && n < N) ? v[c][r] - mean : 0.f;
                     q += d * d;
                 }
-#pragma unroll
-            for (int o = LPR >> 1; o > 0; o >>= 1) q += __shfl_xor(q, o);
+            q = group_reduce<LPR, false>(q);
             const float rstd = rsqrtf(q / (float)N + p.ln_eps);
 #pragma unroll
             for (int c = 0; c < NCH; ++c)
@@ -305,7 +366,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
         if (kt + 1 < nk) step(kt + 1, xs1, ws1, xs0, ws0);
     }
 
-    // ---- epilogue: park the f32 tile in LDS (row m, col n), then stream whole rows ----
+    // ---- epilogue: residual rows in flight, park the f32 tile in LDS, stream whole rows ----
+    ResRows<TO, BN, 4, BM> rp;
+    rp.issue(p, m0, n0, 0, wave, lane);
     float* ep = reinterpret_cast<float*>(lds);
 #pragma unroll
     for (int a = 0; a < TN; ++a)
@@ -316,7 +379,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
             *reinterpret_cast<f32x4*>(ep + ml * EPI_LD + nl) = acc[a][b];
         }
     __syncthreads();
-    epilogue_rows<TO, BN, EPI_LD, 4, LN>(p, ep, m0, n0, 0, BM, wave, lane);
+    epilogue_rows<TO, BN, EPI_LD, 4, LN, BM>(p, ep, m0, n0, 0, wave, lane, rp);
 }
 
 // Large-M GEMM / implicit conv: 512 threads (8 waves, WGM x WGN, each wave a (BM/WGM) x 64
@@ -468,6 +531,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const GemmArgs p, cons
     float* ep = reinterpret_cast<float*>(lds);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+        ResRows<TO, BN, 8, HALF> rp;
+        rp.issue(p, m0, n0, h * HALF, wave, lane);
         if (h) __syncthreads();
         if ((wm * WTM) / HALF == h) {
 #pragma unroll
@@ -480,7 +545,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const GemmArgs p, cons
                 }
         }
         __syncthreads();
-        epilogue_rows<TO, BN, EPI_LD, 8, LN>(p, ep, m0, n0, h * HALF, (h + 1) * HALF, wave, lane);
+        epilogue_rows<TO, BN, EPI_LD, 8, LN, HALF>(p, ep, m0, n0, h * HALF, wave, lane, rp);
     }
 }
 

@@ -491,27 +491,6 @@ __device__ __forceinline__ void widen2(uint32_t u, f32x2& x) {
     }
 }
 
-// max / sum over each aligned group of G lanes (G = 2..64), result in every lane: DPP
-// butterflies inside a 16-lane row (quad_perm xor1, xor2, half-mirror, mirror -- each pairs
-// lanes of the two halves of the previous group), cross-row steps by swizzle / bpermute.
-template <bool MAX>
-__device__ __forceinline__ float combine(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
-
-template <int G, bool MAX>
-__device__ __forceinline__ float group_reduce(float x) {
-    static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "group size");
-    auto dpp = [](float v, auto ctrl) {
-        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), decltype(ctrl)::value, 0xf, 0xf, false));
-    };
-    if constexpr (G >= 2) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0xB1>{}));    // quad_perm [1,0,3,2]
-    if constexpr (G >= 4) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0x4E>{}));    // quad_perm [2,3,0,1]
-    if constexpr (G >= 8) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0x141>{}));   // row_half_mirror
-    if constexpr (G >= 16) x = combine<MAX>(x, dpp(x, std::integral_constant<int, 0x140>{}));  // row_mirror
-    if constexpr (G >= 32) x = combine<MAX>(x, __shfl_xor(x, 16));
-    if constexpr (G >= 64) x = combine<MAX>(x, __shfl_xor(x, 32));
-    return x;
-}
-
 template <typename T, int L, int P>
 __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
     const T* __restrict__ value, long vsb, int vss, long vsm, int head_bytes, const int64_t* __restrict__ shapes,
@@ -525,7 +504,22 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
     constexpr unsigned OOB = 0x80000000u;
     __shared__ FastLevels lv;
     __shared__ Tap4 taps[NSB];
-    const int b = blockIdx.y, q0 = blockIdx.x * QT, mh0 = blockIdx.z * MH;
+    // XCD-aware remap (bijective, cdna_hip_programming.md T1): workgroups are dealt to the 8
+    // XCDs round-robin by linear id; give each XCD a contiguous run of query tiles of one
+    // (frame, head group) so neighbouring queries -- which sample overlapping value
+    // neighbourhoods -- share that XCD's L2
+    int b, q0, mh0;
+    {
+        const int gx = gridDim.x, gy = gridDim.y;
+        const int nblk = gx * gy * gridDim.z;
+        const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+        const int qd = nblk >> 3, rm = nblk & 7, xcd = lin & 7;
+        const int nid = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + (lin >> 3);
+        const int bx = nid % gx, rest = nid / gx;
+        b = rest % gy;
+        q0 = bx * QT;
+        mh0 = (rest / gy) * MH;
+    }
     if (threadIdx.x == 0) {
         long long acc = 0;
         for (int l = 0; l < L; ++l) {
