@@ -594,7 +594,9 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
     }
     __syncthreads();
 
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave index made provably uniform: the head-map descriptor below must live in SGPRs,
+    // or hipcc wraps every buffer load in a readfirstlane waterfall loop
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int m = mh0 + wave;
     if (m >= M) return;
     const int qi = lane >> 2, q = q0 + qi;
