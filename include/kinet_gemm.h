@@ -58,10 +58,12 @@ int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, int Hin, int
 /* value_proj for MSDA: C = (A @ B^T + bias) with rows masked, stored HEAD-MAJOR:
  * row r = b*rows_per_batch + s, column n = g*head_dim + d  ->  C[((g*batch + b)*rows_per_batch + s)*head_dim + d]
  * i.e. (N/head_dim, batch, rows_per_batch, head_dim) -- the layout kinet_msda_fused_forward
- * gathers from best (ms_deform_attn.py:64-67 produce the same values in (N, S, M, D)). */
+ * gathers from best (ms_deform_attn.py:64-67 produce the same values in (N, S, M, D)).
+ * out_dtype: in_dtype, or KINET_F16 from KINET_BF16 operands (f16 values feed the sampling
+ * kernel's mixed-precision FMA; post-LayerNorm projections are far inside f16 range). */
 int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
-                         int in_dtype, const float* bias, const uint8_t* row_mask, int rows_per_batch,
-                         int head_dim, kinet_stream_t stream);
+                         int in_dtype, int out_dtype, const float* bias, const uint8_t* row_mask,
+                         int rows_per_batch, int head_dim, kinet_stream_t stream);
 
 /* Diagnostic kernel-selection knob (no reference counterpart; used by the kernel
  * benchmarks to A/B GEMM kernels in one process).  bit 1: allow the 512-thread

@@ -71,12 +71,10 @@ int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num
  *                   head-major layout (M, N, S, D) written by kinet_gemm_headmajor, so a
  *                   wave's gathers for neighbouring queries of one head are contiguous.
  * Launch: one head per wave, 64/(D/vec) consecutive queries per wave.
- * Writes output (N, Lq, M*D) and, when loc_out/attw_out are non-NULL, the f32
- * sampling_loc / attn_weight tensors (needed to run kinet_msda_backward). */
-/* Diagnostic kernel-selection knob (no reference counterpart): bit 0 = never use the
- * specialised 16-bit / head_dim-32 fused kernel.  Returns the previous flags. */
-int kinet_msda_set_flags(int flags);
-
+ * Writes output (N, Lq, M*D) in output_dtype and, when loc_out/attw_out are non-NULL, the
+ * f32 sampling_loc / attn_weight tensors (needed to run kinet_msda_backward).
+ * output_dtype = value_dtype, or KINET_BF16 from KINET_F16 values (f16 values are gathered
+ * and accumulated by mixed f16 x f32 FMAs; head_dim 32, L*P in {16, 32} only). */
 int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_ss, int64_t value_sm,
                              const int64_t* spatial_shapes,
                              const void* offsets_logits, int ld_off,
@@ -85,7 +83,11 @@ int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_
                              void* output, float* loc_out, float* attw_out,
                              int batch, int spatial_size, int num_heads, int channels,
                              int num_levels, int num_query, int num_point,
-                             int value_dtype, kinet_stream_t stream);
+                             int value_dtype, int output_dtype, kinet_stream_t stream);
+
+/* Diagnostic kernel-selection knob (no reference counterpart): bit 0 = never use the
+ * specialised 16-bit / head_dim-32 fused kernel.  Returns the previous flags. */
+int kinet_msda_set_flags(int flags);
 
 #ifdef __cplusplus
 }

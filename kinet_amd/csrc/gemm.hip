@@ -633,6 +633,7 @@ int dispatch(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t s) {
     }
     if (in_dtype == KINET_BF16 && out_dtype == KINET_BF16) return launch<bf16_t, bf16_t, CONV>(a, s);
     if (in_dtype == KINET_BF16 && out_dtype == KINET_F32) return launch<bf16_t, float, CONV>(a, s);
+    if (!CONV && in_dtype == KINET_BF16 && out_dtype == KINET_F16) return launch<bf16_t, f16_t, false>(a, s);
     if (in_dtype == KINET_F16 && out_dtype == KINET_F16) return launch<f16_t, f16_t, CONV>(a, s);
     if (in_dtype == KINET_F16 && out_dtype == KINET_F32) return launch<f16_t, float, CONV>(a, s);
     if (in_dtype == KINET_F32 && out_dtype == KINET_F32) return launch<float, float, CONV>(a, s);
@@ -648,8 +649,8 @@ bool aligned16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
 using namespace kinet;
 
 extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
-                                    int in_dtype, const float* bias, const uint8_t* row_mask, int rows_per_batch,
-                                    int head_dim, kinet_stream_t stream);
+                                    int in_dtype, int out_dtype, const float* bias, const uint8_t* row_mask,
+                                    int rows_per_batch, int head_dim, kinet_stream_t stream);
 
 extern "C" int kinet_gemm_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K, int lda,
                              int ldb, int ldc, int in_dtype, const float* scale, const float* bias, const void* R,
@@ -681,8 +682,10 @@ extern "C" int kinet_gemm_ex(const void* A, const void* A2, const void* B, void*
 }
 
 extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
-                                    int in_dtype, const float* bias, const uint8_t* row_mask, int rows_per_batch,
-                                    int head_dim, kinet_stream_t stream) {
+                                    int in_dtype, int out_dtype, const float* bias, const uint8_t* row_mask,
+                                    int rows_per_batch, int head_dim, kinet_stream_t stream) {
+    KINET_CHECK_ARG(out_dtype == in_dtype || (in_dtype == KINET_BF16 && out_dtype == KINET_F16),
+                    "gemm_headmajor: out_dtype must equal in_dtype (or f16 from bf16)");
     KINET_CHECK_ARG(M >= 0 && N > 0 && K > 0, "gemm_headmajor: invalid sizes");
     KINET_CHECK_ARG(rows_per_batch > 0 && M % rows_per_batch == 0, "gemm_headmajor: M must be batch*rows_per_batch");
     KINET_CHECK_ARG(head_dim > 0 && head_dim % 4 == 0 && N % head_dim == 0, "gemm_headmajor: N must be a multiple of head_dim (%% 4)");
@@ -698,7 +701,7 @@ extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M
     KINET_CHECK_ARG(ab < (1LL << 31) && bb < (1LL << 31), "gemm_headmajor: operand larger than 2 GiB");
     a.a_bytes = (int)ab;
     a.b_bytes = (int)bb;
-    return dispatch<false>(a, in_dtype, in_dtype, (hipStream_t)stream);
+    return dispatch<false>(a, in_dtype, out_dtype, (hipStream_t)stream);
 }
 
 extern "C" int kinet_gemm_set_flags(int flags) {

@@ -372,13 +372,15 @@ bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t strea
     if (a.M < 4096 || (a.K != 64 && a.K != 128 && a.K != 256)) return false;
     if (a.A2 != nullptr && (a.R != nullptr || a.ln_g != nullptr || !al16(a.A2))) return false;
     if (a.N % 8 != 0 || (a.ln_g != nullptr && a.N > 256)) return false;
-    const bool o16 = out_dtype == in_dtype, o32 = out_dtype == KINET_F32;
+    const bool o16 = out_dtype == in_dtype || (in_dtype == KINET_BF16 && out_dtype == KINET_F16);
+    const bool o32 = out_dtype == KINET_F32;
     if (!o16 && !o32) return false;
     if (o16 ? (a.ldc % 8 != 0) : (a.ldc % 4 != 0)) return false;
     if (!al16(a.C) || (a.R != nullptr && (!o16 || a.ldr % 8 != 0 || !al16(a.R)))) return false;
     if (a.hm_rows && a.hm_d % 8 != 0) return false;
     if (in_dtype == KINET_BF16) {
-        if (o16) launch_t<bf16_t, bf16_t>(a, stream);
+        if (out_dtype == KINET_F16) launch_t<bf16_t, f16_t>(a, stream);
+        else if (o16) launch_t<bf16_t, bf16_t>(a, stream);
         else launch_t<bf16_t, float>(a, stream);
     } else {
         if (o16) launch_t<f16_t, f16_t>(a, stream);

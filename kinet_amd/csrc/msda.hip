@@ -482,6 +482,16 @@ struct FastLevels {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
+// acc += f16(lo or hi half of x) * w in f32 -- one v_fma_mix_f32, no separate widening
+__device__ __forceinline__ float fma_mix_lo(float acc, uint32_t x, float w) {
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(x), "v"(w));
+    return acc;
+}
+__device__ __forceinline__ float fma_mix_hi(float acc, uint32_t x, float w) {
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(x), "v"(w));
+    return acc;
+}
+
 template <typename T>
 __device__ __forceinline__ void widen2(uint32_t u, f32x2& x) {
     if constexpr (std::is_same<T, f16_t>::value) {
@@ -491,13 +501,13 @@ __device__ __forceinline__ void widen2(uint32_t u, f32x2& x) {
     }
 }
 
-template <typename T, int L, int P>
+template <typename T, typename TO, int L, int P>
 __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
     const T* __restrict__ value, long vsb, int vss, long vsm, int head_bytes, const int64_t* __restrict__ shapes,
     const float* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
     const uint8_t* __restrict__ qmask, float* __restrict__ loc_out, float* __restrict__ attw_out,
-    T* __restrict__ out, int S, int M, int Lq) {
-    static_assert(sizeof(T) == 2, "16-bit values");
+    TO* __restrict__ out, int S, int M, int Lq) {
+    static_assert(sizeof(T) == 2 && sizeof(TO) == 2, "16-bit values and output");
     constexpr int D = 32, QT = 16, MH = kThreads / 64, LP = L * P;
     static_assert((LP & (LP - 1)) == 0 && LP <= 64 && L <= kMaxLevels, "L*P: power of two <= 64");
     constexpr int NSB = MH * QT * LP;               // samples per workgroup
@@ -621,23 +631,33 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
         for (int g = 0; g < SG; ++g)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const f32x2 w2 = {t[g].w[k], t[g].w[k]};
+                if constexpr (std::is_same<T, f16_t>::value) {
+                    // f16 values: v_fma_mix_f32 reads each half directly (1 VALU per MAC)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    f32x2 x;
-                    widen2<T>(v[g][k][j], x);
-                    acc[j] = __builtin_elementwise_fma(x, w2, acc[j]);
+                    for (int j = 0; j < 4; ++j) {
+                        acc[j][0] = fma_mix_lo(acc[j][0], v[g][k][j], t[g].w[k]);
+                        acc[j][1] = fma_mix_hi(acc[j][1], v[g][k][j], t[g].w[k]);
+                    }
+                } else {
+                    // bf16 values: widen by shift / mask, then v_pk_fma_f32 (1.5 VALU per MAC)
+                    const f32x2 w2 = {t[g].w[k], t[g].w[k]};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        f32x2 x;
+                        widen2<T>(v[g][k][j], x);
+                        acc[j] = __builtin_elementwise_fma(x, w2, acc[j]);
+                    }
                 }
             }
     }
     if (q >= Lq) return;
-    VecT<T, 8> o;
+    VecT<TO, 8> o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        o.v[2 * j] = Cvt<T>::from(acc[j][0]);
-        o.v[2 * j + 1] = Cvt<T>::from(acc[j][1]);
+        o.v[2 * j] = Cvt<TO>::from(acc[j][0]);
+        o.v[2 * j + 1] = Cvt<TO>::from(acc[j][1]);
     }
-    *reinterpret_cast<VecT<T, 8>*>(out + ((long)b * Lq + q) * M * D + (long)m * D + (lane & 3) * 8) = o;
+    *reinterpret_cast<VecT<TO, 8>*>(out + ((long)b * Lq + q) * M * D + (long)m * D + (lane & 3) * 8) = o;
 }
 
 // ---------------------------------------------------------------------------------
@@ -939,7 +959,7 @@ extern "C" int kinet_msda_forward(const void* value, const int64_t* spatial_shap
 
 namespace kinet {
 namespace {
-template <typename T>
+template <typename T, typename TO = T>
 int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* shapes, const float* offlog,
                  int ld_off, const float* ref, int ref_dim, const uint8_t* qmask, void* out, float* loc_out,
                  float* attw_out, int N, int S, int M, int D, int L, int Lq, int P, hipStream_t stream) {
@@ -953,17 +973,19 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
             ((uintptr_t)value % 16) == 0 && head_bytes < (1LL << 31) && !(msda_flags & 1)) {
             dim3 grid((Lq + 15) / 16, N, (M + 3) / 4);
             if (L == 4)
-                hipLaunchKernelGGL((msda_fused_fast_kernel<T, 4, 4>), grid, dim3(kThreads), 0, stream, (const T*)value, vsb,
-                                   vss, vsm, (int)head_bytes, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out,
-                                   attw_out, (T*)out, S, M, Lq);
+                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, 4, 4>), grid, dim3(kThreads), 0, stream, (const T*)value,
+                                   vsb, vss, vsm, (int)head_bytes, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out,
+                                   attw_out, (TO*)out, S, M, Lq);
             else
-                hipLaunchKernelGGL((msda_fused_fast_kernel<T, 8, 4>), grid, dim3(kThreads), 0, stream, (const T*)value, vsb,
-                                   vss, vsm, (int)head_bytes, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out,
-                                   attw_out, (T*)out, S, M, Lq);
+                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, 8, 4>), grid, dim3(kThreads), 0, stream, (const T*)value,
+                                   vsb, vss, vsm, (int)head_bytes, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out,
+                                   attw_out, (TO*)out, S, M, Lq);
             KINET_LAUNCH_CHECK();
             return KINET_OK;
         }
     }
+    KINET_CHECK_ARG((std::is_same<T, TO>::value), "msda fused: output dtype != value dtype needs head_dim 32, "
+                    "L*P in {16, 32}, P = 4 and aligned strides");
     KINET_CHECK_ARG(vsb % c.vec == 0 && vss % c.vec == 0 && vsm % c.vec == 0 && ((uintptr_t)value % 16) == 0,
                     "msda fused: value strides must keep %d-element vectors aligned", c.vec);
     const int QT = 64 / c.lpq;          // queries per wave (= per workgroup)
@@ -974,6 +996,7 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
     const size_t lds = sizeof(LevelInfo) + nsamp * sizeof(Tap4) + (pow2 ? 0 : nsamp * sizeof(float));
     KINET_CHECK_ARG(lds <= 160 * 1024, "msda fused: LDS request %zu too large", lds);
     dim3 grid((Lq + QT - 1) / QT, N, (M + MH - 1) / MH);
+    if constexpr (!std::is_same<T, TO>::value) return KINET_ERR_ARG;   // (rejected above)
 #define KF(VEC)                                                                                                  \
     hipLaunchKernelGGL((msda_fused_kernel<T, VEC>), grid, dim3(kThreads), lds, stream, (const T*)value, vsb, vss, \
                        vsm, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out, attw_out, (T*)out, S, M, D, L,   \
@@ -1002,7 +1025,7 @@ extern "C" int kinet_msda_fused_forward(const void* value, int64_t value_sb, int
                                         const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
                                         void* output, float* loc_out, float* attw_out, int batch, int spatial_size,
                                         int num_heads, int channels, int num_levels, int num_query, int num_point,
-                                        int value_dtype, kinet_stream_t stream) {
+                                        int value_dtype, int output_dtype, kinet_stream_t stream) {
     int rc = common_checks(batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, 1);
     if (rc) return rc;
     KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.", ref_dim);
@@ -1022,6 +1045,9 @@ extern "C" int kinet_msda_fused_forward(const void* value, int64_t value_sb, int
 #define ARGS value, (long)value_sb, (int)value_ss, (long)value_sm, spatial_shapes, (const float*)offsets_logits, ld_off, \
              ref_points, ref_dim, query_attn_mask, output, loc_out, attw_out, batch, spatial_size, num_heads, channels, \
              num_levels, num_query, num_point, s
+    KINET_CHECK_ARG(output_dtype == value_dtype || (value_dtype == KINET_F16 && output_dtype == KINET_BF16),
+                    "msda fused forward: output dtype %d unsupported for value dtype %d", output_dtype, value_dtype);
+    if (value_dtype == KINET_F16 && output_dtype == KINET_BF16) return launch_fused<f16_t, bf16_t>(ARGS);
     if (value_dtype == KINET_F32) return launch_fused<float>(ARGS);
     if (value_dtype == KINET_BF16) return launch_fused<bf16_t>(ARGS);
     if (value_dtype == KINET_F16) return launch_fused<f16_t>(ARGS);

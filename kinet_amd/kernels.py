@@ -133,9 +133,10 @@ def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_d
     return out.view(*lead, Nout) if out.is_contiguous() else out
 
 
-def value_proj_headmajor(x, weight, bias, head_dim, row_mask=None):
+def value_proj_headmajor(x, weight, bias, head_dim, row_mask=None, out_dtype=None):
     """MSDA value projection written head-major: x (B, S, K) -> (Nout/head_dim, B, S, head_dim),
-    padding rows zeroed (ms_deform_attn.py:64-67)."""
+    padding rows zeroed (ms_deform_attn.py:64-67).  out_dtype: x.dtype, or float16 from bf16
+    operands (the sampling kernel's mixed f16 x f32 FMA path)."""
     N.require_gpu(x)
     B, S, K = x.shape
     x2 = x.reshape(B * S, K)
@@ -143,11 +144,12 @@ def value_proj_headmajor(x, weight, bias, head_dim, row_mask=None):
         x2 = x2.contiguous()
     w = weight_as(weight, x.dtype)
     Nout = w.shape[0]
-    out = torch.empty((Nout // head_dim, B, S, head_dim), dtype=x.dtype, device=x.device)
+    od = out_dtype or x.dtype
+    out = torch.empty((Nout // head_dim, B, S, head_dim), dtype=od, device=x.device)
     mask = row_mask.reshape(-1).to(torch.uint8).contiguous() if row_mask is not None else None
     e = x.element_size()
     N.call('kinet_gemm_headmajor', N.ptr(x2), N.ptr(w), N.ptr(out), B * S, Nout, K, x2.stride(0), K,
-           N.dtype_code(x.dtype), N.ptr(f32(bias)), N.ptr(mask), S, head_dim, N.stream(x.device),
+           N.dtype_code(x.dtype), N.dtype_code(od), N.ptr(f32(bias)), N.ptr(mask), S, head_dim, N.stream(x.device),
            work={'family': 'gemm', 'flops': 2.0 * B * S * Nout * K, 'shape': (B * S, Nout, K),
                  'bytes': (B * S * K + Nout * K + B * S * Nout) * e})
     return out
@@ -281,11 +283,12 @@ def box_refine(tmp, ref, valid_ratios=None, want_input=True):
 
 # ------------------------------------------------------------------------------ MSDA
 def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_levels, n_points,
-               query_attn_mask=None, want_loc_attw=False, head_major=False):
+               query_attn_mask=None, want_loc_attw=False, head_major=False, out_dtype=None):
     """Sampling of MSDeformAttn.forward (ms_deform_attn.py:69-87) in one kernel.
     value: projected values, either (B, S, d) row-major (column slices allowed) or, with
     head_major=True, (M, B, S, D) as written by value_proj_headmajor;
     offlog (B, Lq, M*L*P*3) f32 [offsets | logits]; reference_points (B, Lq, L, 2|4) f32.
+    out_dtype: value.dtype, or bfloat16 from float16 values (mixed-precision gather path).
     Returns (B, Lq, d) [, loc, attw]."""
     if head_major:
         M_, B, S, D = value.shape
@@ -306,7 +309,8 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
     ref = reference_points.float().contiguous()
     if ref.shape[2] != n_levels:
         raise RuntimeError(f'reference_points has {ref.shape[2]} levels, module expects {n_levels}')
-    out = torch.empty((B, Lq, d), dtype=value.dtype, device=value.device)
+    od = out_dtype or value.dtype
+    out = torch.empty((B, Lq, d), dtype=od, device=value.device)
     loc = attw = None
     if want_loc_attw:
         loc = torch.empty((B, Lq, n_heads, n_levels, n_points, 2), dtype=torch.float32, device=value.device)
@@ -318,10 +322,10 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
     nsamp = B * Lq * n_heads * n_levels * n_points
     N.call('kinet_msda_fused_forward', N.ptr(value), vsb, vss, vsm, N.ptr(spatial_shapes), N.ptr(offlog),
            offlog.shape[-1], N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), N.ptr(loc), N.ptr(attw), B, S,
-           n_heads, D, n_levels, Lq, n_points, N.dtype_code(value.dtype), N.stream(value.device),
+           n_heads, D, n_levels, Lq, n_points, N.dtype_code(value.dtype), N.dtype_code(od), N.stream(value.device),
            work={'family': 'msda', 'flops': 10.0 * nsamp * D,
                  # compulsory bytes: value once, f32 offsets+logits, refs, output once
-                 'bytes': B * S * d * ev + nsamp * 3 * 4 + ref.numel() * 4 + B * Lq * d * ev
+                 'bytes': B * S * d * ev + nsamp * 3 * 4 + ref.numel() * 4 + B * Lq * d * out.element_size()
                  + (nsamp * 3 * 4 if want_loc_attw else 0),
                  'Lq': Lq, 'S': S, 'shape': (B, Lq, S)})
     if want_loc_attw:

@@ -27,7 +27,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 
 from kinet_amd import kernels as K
 from kinet_amd.models.misc import inverse_sigmoid
-from kinet_amd.msda import MSDeformAttn
+from kinet_amd.msda import MSDeformAttn, value_dtype_for
 
 
 def _get_clones(module, N):
@@ -251,7 +251,8 @@ class DeformableTransformerDecoder(nn.Module):
                             lambda *bs: torch.cat([b.detach() for b in bs], 0).float().contiguous())
         ca0 = self.layers[0].cross_attn
         nh = ca0.n_heads
-        values = K.value_proj_headmajor(src, vw, vb, d // nh, row_mask=src_padding_mask)   # (nl*M, B, S, D)
+        values = K.value_proj_headmajor(src, vw, vb, d // nh, row_mask=src_padding_mask,
+                                        out_dtype=value_dtype_for(src.dtype))                # (nl*M, B, S, D)
         intermediate, intermediate_reference_points = [], []
         for lid, layer in enumerate(self.layers):
             output = layer(output, query_pos, ref_in, src, src_spatial_shapes, src_padding_mask, query_attn_mask,

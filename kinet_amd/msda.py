@@ -20,6 +20,11 @@ from kinet_amd import MultiScaleDeformableAttention as MSDA
 from kinet_amd import kernels as K
 
 
+def value_dtype_for(compute_dtype):
+    """Storage dtype of projected MSDA values: f16 under bf16 compute (see project_value)."""
+    return torch.float16 if compute_dtype == torch.bfloat16 else compute_dtype
+
+
 class MSDeformAttnFunction(Function):
     """ms_deform_attn_func.py:14-31 -- same forward/backward contract."""
 
@@ -97,9 +102,11 @@ class MSDeformAttn(nn.Module):
 
     def project_value(self, input_flatten, input_padding_mask=None):
         """value_proj + padding masked_fill (ms_deform_attn.py:64-66), written head-major
-        (M, N, S, D) for the gather kernel."""
+        (M, N, S, D) for the gather kernel; bf16 compute stores the values as f16 (more
+        mantissa, and the sampling kernel's mixed f16 x f32 FMA reads them directly)."""
         return K.value_proj_headmajor(input_flatten, self.value_proj.weight, self.value_proj.bias,
-                                      self.d_model // self.n_heads, row_mask=input_padding_mask)
+                                      self.d_model // self.n_heads, row_mask=input_padding_mask,
+                                      out_dtype=value_dtype_for(input_flatten.dtype))
 
     # -- pieces used by the fused transformer layers ------------------------------------
     def packed_offsets_weights(self):
@@ -120,7 +127,7 @@ class MSDeformAttn(nn.Module):
         offlog = K.linear(query, w, b, out_dtype=torch.float32, x_add=query_add)
         return K.msda_fused(value, input_spatial_shapes, offlog, reference_points,
                             self.n_heads, self.n_levels, self.n_points, query_attn_mask,
-                            head_major=(value.dim() == 4))
+                            head_major=(value.dim() == 4), out_dtype=query.dtype)
 
     def _forward_autograd(self, query, reference_points, input_flatten, input_spatial_shapes,
                           input_padding_mask, query_attn_mask):

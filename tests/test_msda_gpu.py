@@ -197,3 +197,20 @@ def test_fast_fused_kernel_vs_oracle():
     ref_out = O.fwd(v, ss.cpu().numpy(), loc.cpu().numpy(), aw.cpu().numpy())
     d = (out.float().cpu() - torch.from_numpy(ref_out).reshape(out.shape)).abs()
     assert (d <= 1e-2 * torch.from_numpy(ref_out).reshape(out.shape).abs() + 1e-2).all(), d.max().item()
+
+
+def test_fast_fused_f16_values_bf16_out():
+    """f16 values (v_fma_mix path) with bf16 output vs the same values sampled into f16 output:
+    identical f32 accumulation, so they differ by the output rounding only."""
+    from kinet_amd import kernels as K
+    shapes = ((40, 50), (20, 25), (10, 13), (5, 7))
+    B, M, P, Lq = 2, 8, 4, 1500
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 9, dtype=torch.float16)
+    o_bf = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, head_major=True, out_dtype=torch.bfloat16)
+    o_h = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, head_major=True)
+    torch.cuda.synchronize()
+    assert o_bf.dtype == torch.bfloat16 and o_h.dtype == torch.float16
+    d = (o_bf.float() - o_h.float()).abs()
+    assert (d <= o_h.float().abs() * 2.0 ** -8 + 1e-6).all(), d.max().item()
+    with pytest.raises(RuntimeError):
+        K.msda_fused(value.float(), ss, offlog, ref, M, 4, P, head_major=True, out_dtype=torch.bfloat16)
