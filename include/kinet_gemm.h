@@ -65,6 +65,20 @@ int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, in
                          int in_dtype, int out_dtype, const float* bias, const uint8_t* row_mask,
                          int rows_per_batch, int head_dim, kinet_stream_t stream);
 
+/* Split-K forms for small-M / long-K problems (few output tiles): K is cut into `ksplit`
+ * slices (rounded to whole 64-element K-steps) whose f32 partial tiles go to `workspace`
+ * (ksplit * M * N floats, caller-allocated), then one finalize pass sums the slices and
+ * applies the same epilogue (scale/bias, residual, ReLU, LayerNorm for N <= 1024, row mask)
+ * into C / Y.  Deterministic (no atomics). */
+int kinet_gemm_splitk(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                      int in_dtype, const float* scale, const float* bias, const void* R, int ldr, int relu,
+                      const float* ln_gamma, const float* ln_beta, float ln_eps, int out_dtype,
+                      const uint8_t* row_mask, float* workspace, int ksplit, kinet_stream_t stream);
+int kinet_conv2d_splitk(const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin,
+                        int Hout, int Wout, int Cout, int KH, int KW, int stride, int pad, int in_dtype,
+                        const float* scale, const float* bias, const void* R, int ldr, int relu, int ldy,
+                        float* workspace, int ksplit, kinet_stream_t stream);
+
 /* Diagnostic kernel-selection knob (no reference counterpart; used by the kernel
  * benchmarks to A/B GEMM kernels in one process).  bit 1: allow the 512-thread
  * 256x256-tile LDS-DMA kernel for large-M problems; bit 2: never use the

@@ -29,6 +29,8 @@ _SIGS = {
     'kinet_gemm': [P, P, P] + [I] * 7 + [P, P, P, I, I, I, P, I, P],
     'kinet_gemm_ex': [P, P, P, P] + [I] * 7 + [P, P, P, I, I, P, P, F, I, P, P],
     'kinet_conv2d': [P, P, P] + [I] * 12 + [P, P, P, I, I, I, P],
+    'kinet_conv2d_splitk': [P, P, P] + [I] * 12 + [P, P, P, I, I, I, P, I, P],
+    'kinet_gemm_splitk': [P, P, P] + [I] * 7 + [P, P, P, I, I, P, P, F, I, P, P, I, P],
     'kinet_layernorm': [P] * 5 + [I, I, F, I, I, P],
     'kinet_groupnorm': [P] * 4 + [I] * 5 + [F, I, P, P],
     'kinet_maxpool2d_3x3s2': [P, P] + [I] * 5 + [P],

@@ -118,7 +118,7 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& p, const float* ep
     const int M = p.M, N = p.N;
     constexpr int LPR = RR::LPR, NCH = RR::NCH, RPW = RR::RPW;
     static_assert(64 % LPR == 0, "row mapping");
-    TO* __restrict__ C = (TO*)p.C;
+    TO* __restrict__ C = (TO*)p.C + (long)blockIdx.y * p.c_slice;
     const TO* __restrict__ R = (const TO*)p.R;
     const int lr = lane / LPR, lc = lane - (lane / LPR) * LPR;
     const bool ld_ok = ((p.ldc & 3) == 0) && (R == nullptr || (p.ldr & 3) == 0);
@@ -236,7 +236,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave % WGM, wn = wave / WGM;
     const int sc = tid & 7, sr = tid >> 3;
-    const int M = p.M, N = p.N, K = p.K;
+    const int M = p.M, N = p.N;
+    // K range of this block: the whole K, or slice blockIdx.y of a split-K launch
+    const int kbeg = p.kchunk ? (int)blockIdx.y * p.kchunk : 0;
+    const int K = p.kchunk ? min(p.K, kbeg + p.kchunk) : p.K;
 
     // Buffer descriptors over the whole operands (kernel arguments -> wave-uniform SGPRs).
     // A lane that must contribute zeros (row/col past the edge, K tail, conv padding)
@@ -284,7 +287,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
     u32x4 xs0[XR], ws0[WR], xs1[XR], ws1[WR];
 
     auto load_tile = [&](int k0, u32x4 (&xs)[XR], u32x4 (&ws)[WR]) {
-        const int k = k0 + sc * EPC;
+        const int k = kbeg + k0 + sc * EPC;
         const bool kok = k < K;
         int kh = 0, kw = 0, cc = k;
         if (CONV) {
@@ -329,7 +332,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
 #pragma unroll
         for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = (K + BK - 1) / BK;
+    const int nk = (K - kbeg + BK - 1) / BK;
     auto compute = [&](int buf) {
         const char* xl = lds + buf * STAGE;
         const char* wl = xl + BM * ROWB;
@@ -584,7 +587,7 @@ template <typename T, typename TO, bool CONV>
 int launch(const GemmArgs& a, hipStream_t stream) {
     if (a.M == 0 || a.N == 0) return KINET_OK;
     const bool ln = a.ln_g != nullptr;
-    if (launch_big<T, TO, CONV>(a, stream)) {
+    if (a.kchunk == 0 && launch_big<T, TO, CONV>(a, stream)) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;
     }
@@ -607,7 +610,8 @@ int launch(const GemmArgs& a, hipStream_t stream) {
     const int nMt = (a.M + bm - 1) / bm, nNt = (a.N + bn - 1) / bn;
     const long nblk = (long)nMt * nNt;
     KINET_CHECK_ARG(nblk < (1L << 31), "gemm: too many tiles");
-    dim3 grid((unsigned)nblk), block(256);
+    const int nslice = a.kchunk ? (a.K + a.kchunk - 1) / a.kchunk : 1;
+    dim3 grid((unsigned)nblk, (unsigned)nslice), block(256);
 #define L_(BM_, BN_, WM_, WN_, LN_) \
     hipLaunchKernelGGL((gemm_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0, stream, a, nNt)
     if (ln) {
@@ -627,7 +631,7 @@ int launch(const GemmArgs& a, hipStream_t stream) {
 
 template <bool CONV>
 int dispatch(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t s) {
-    if (!CONV && !(kinet_gemm_flags & 4) && launch_rw(a, in_dtype, out_dtype, s)) {
+    if (!CONV && a.kchunk == 0 && !(kinet_gemm_flags & 4) && launch_rw(a, in_dtype, out_dtype, s)) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;
     }
@@ -639,6 +643,103 @@ int dispatch(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t s) {
     if (in_dtype == KINET_F32 && out_dtype == KINET_F32) return launch<float, float, CONV>(a, s);
     set_error("gemm: unsupported dtypes in=%d out=%d", in_dtype, out_dtype);
     return KINET_ERR_ARG;
+}
+
+// split-K finalize: out[m, n] = epilogue(sum over slices of ws[s][m][n]) -- one wave per row,
+// column n = j*64 + lane (coalesced); the same epilogue as the GEMM kernels (scale/bias,
+// residual, ReLU, LayerNorm over the row, row mask).
+template <typename TO, bool LN>
+__global__ __launch_bounds__(256) void splitk_finalize_kernel(const GemmArgs p, const float* __restrict__ ws,
+                                                              int nslice, long slice) {
+    constexpr int MAXJ = 16;   // LN rows up to 1024 columns
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= p.M) return;
+    const int N = p.N;
+    const int nj = (N + 63) / 64;
+    const TO* __restrict__ R = (const TO*)p.R;
+    TO* __restrict__ C = (TO*)p.C;
+    float v[MAXJ];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        v[j] = 0.f;
+        if (j >= nj) continue;
+        const int n = j * 64 + lane;
+        if (n >= N) continue;
+        float x = 0.f;
+        for (int t = 0; t < nslice; ++t) x += ws[t * slice + (long)row * N + n];
+        x = x * (p.scale ? p.scale[n] : 1.f) + (p.bias ? p.bias[n] : 0.f);
+        if (R) x += IO4<TO>::load1(R + (long)row * p.ldr + n);
+        if (p.relu) x = fmaxf(x, 0.f);
+        v[j] = x;
+        s += x;
+    }
+    if (LN) {
+        s = group_reduce<64, false>(s);
+        const float mean = s / (float)N;
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < MAXJ; ++j)
+            if (j < nj && j * 64 + lane < N) q += (v[j] - mean) * (v[j] - mean);
+        q = group_reduce<64, false>(q);
+        const float rstd = rsqrtf(q / (float)N + p.ln_eps);
+#pragma unroll
+        for (int j = 0; j < MAXJ; ++j) {
+            const int n = j * 64 + lane;
+            if (j < nj && n < N) v[j] = (v[j] - mean) * rstd * p.ln_g[n] + p.ln_b[n];
+        }
+    }
+    const bool masked = p.row_mask && p.row_mask[row];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        const int n = j * 64 + lane;
+        if (j < nj && n < N) IO4<TO>::store1(C + (long)row * p.ldc + n, masked ? 0.f : v[j]);
+    }
+    // columns past 16*64 (non-LN rows wider than 1024)
+    for (int n = MAXJ * 64 + lane; n < N; n += 64) {
+        float x = 0.f;
+        for (int t = 0; t < nslice; ++t) x += ws[t * slice + (long)row * N + n];
+        x = x * (p.scale ? p.scale[n] : 1.f) + (p.bias ? p.bias[n] : 0.f);
+        if (R) x += IO4<TO>::load1(R + (long)row * p.ldr + n);
+        if (p.relu) x = fmaxf(x, 0.f);
+        IO4<TO>::store1(C + (long)row * p.ldc + n, masked ? 0.f : x);
+    }
+}
+
+// Run a GEMM / implicit conv as split-K: partial f32 tiles into ws (nslice x M x N), then the
+// finalize pass applies the caller's epilogue into C.  kchunk is rounded to whole K-steps.
+template <bool CONV>
+int run_splitk(const GemmArgs& user, int in_dtype, int out_dtype, float* ws, int ksplit, hipStream_t s) {
+    KINET_CHECK_ARG(ksplit >= 1 && ws != nullptr, "split-K: need ksplit >= 1 and a workspace");
+    KINET_CHECK_ARG(user.ln_g == nullptr || user.N <= 1024, "split-K: LayerNorm rows up to 1024 columns");
+    const int step = in_dtype == KINET_F32 ? 32 : 64;
+    int kchunk = (user.K + ksplit - 1) / ksplit;
+    kchunk = (kchunk + step - 1) / step * step;
+    const int nslice = (user.K + kchunk - 1) / kchunk;
+    GemmArgs a = user;
+    a.C = ws;
+    a.ldc = user.N;
+    a.R = nullptr;
+    a.scale = nullptr;
+    a.bias = nullptr;
+    a.ln_g = a.ln_b = nullptr;
+    a.row_mask = nullptr;
+    a.relu = 0;
+    a.hm_rows = 0;
+    a.kchunk = kchunk;
+    a.c_slice = (long)user.M * user.N;
+    int rc = dispatch<CONV>(a, in_dtype, KINET_F32, s);
+    if (rc) return rc;
+    dim3 grid((user.M + 3) / 4), block(256);
+#define F_(TO_)                                                                                                 \
+    if (user.ln_g) hipLaunchKernelGGL((splitk_finalize_kernel<TO_, true>), grid, block, 0, s, user, ws, nslice, a.c_slice); \
+    else hipLaunchKernelGGL((splitk_finalize_kernel<TO_, false>), grid, block, 0, s, user, ws, nslice, a.c_slice)
+    if (out_dtype == KINET_BF16) { F_(bf16_t); }
+    else if (out_dtype == KINET_F16) { F_(f16_t); }
+    else { F_(float); }
+#undef F_
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
 }
 
 bool aligned16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
@@ -704,6 +805,31 @@ extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M
     return dispatch<false>(a, in_dtype, out_dtype, (hipStream_t)stream);
 }
 
+extern "C" int kinet_gemm_splitk(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                                 int in_dtype, const float* scale, const float* bias, const void* R, int ldr, int relu,
+                                 const float* ln_gamma, const float* ln_beta, float ln_eps, int out_dtype,
+                                 const uint8_t* row_mask, float* workspace, int ksplit, kinet_stream_t stream) {
+    KINET_CHECK_ARG(M >= 0 && N >= 0 && K > 0, "gemm_splitk: invalid sizes M=%d N=%d K=%d", M, N, K);
+    KINET_CHECK_ARG(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "gemm_splitk: K, lda, ldb must be multiples of 8");
+    KINET_CHECK_ARG(lda >= K && ldb >= K && ldc >= N, "gemm_splitk: leading dims too small");
+    KINET_CHECK_ARG(aligned16(A) && aligned16(B), "gemm_splitk: A and B must be 16-byte aligned");
+    KINET_CHECK_ARG(R == nullptr || ldr >= N, "gemm_splitk: ldr < N");
+    KINET_CHECK_ARG((ln_gamma == nullptr) == (ln_beta == nullptr), "gemm_splitk: LayerNorm needs both gamma and beta");
+    KINET_CHECK_ARG(ln_gamma == nullptr || relu == 0, "gemm_splitk: LayerNorm and ReLU are exclusive");
+    if (M == 0 || N == 0) return KINET_OK;
+    GemmArgs a{};
+    a.A = A; a.B = B; a.C = C; a.R = R; a.scale = scale; a.bias = bias; a.row_mask = row_mask;
+    a.ln_g = ln_gamma; a.ln_b = ln_beta; a.ln_eps = ln_eps;
+    a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldr = ldr; a.relu = relu;
+    const long long es = (long long)dtype_size(in_dtype);
+    const long long ab = ((long long)(M - 1) * lda + K) * es;
+    const long long bb = ((long long)(N - 1) * ldb + K) * es;
+    KINET_CHECK_ARG(ab < (1LL << 31) && bb < (1LL << 31), "gemm_splitk: operand larger than 2 GiB");
+    a.a_bytes = (int)ab;
+    a.b_bytes = (int)bb;
+    return run_splitk<false>(a, in_dtype, out_dtype, workspace, ksplit, (hipStream_t)stream);
+}
+
 extern "C" int kinet_gemm_set_flags(int flags) {
     const int old = kinet_gemm_flags;
     kinet_gemm_flags = flags;
@@ -718,9 +844,9 @@ extern "C" int kinet_gemm(const void* A, const void* B, void* C, int M, int N, i
                          nullptr, 0.f, out_dtype, row_mask, stream);
 }
 
-extern "C" int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin, int Hout,
-                            int Wout, int Cout, int KH, int KW, int stride, int pad, int in_dtype, const float* scale,
-                            const float* bias, const void* R, int ldr, int relu, int ldy, kinet_stream_t stream) {
+static int conv_args(GemmArgs& a, const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin,
+                     int Hout, int Wout, int Cout, int KH, int KW, int stride, int pad, int in_dtype,
+                     const float* scale, const float* bias, const void* R, int ldr, int relu, int ldy) {
     KINET_CHECK_ARG(batch >= 0 && Hin > 0 && Win > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
                     "conv2d: invalid geometry");
     KINET_CHECK_ARG(Cin % 8 == 0, "conv2d: Cin (%d) must be a multiple of 8 (pad channels)", Cin);
@@ -730,7 +856,6 @@ extern "C" int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, i
     KINET_CHECK_ARG(aligned16(X) && aligned16(Wt), "conv2d: X and W must be 16-byte aligned");
     const long M = (long)batch * Hout * Wout;
     KINET_CHECK_ARG(M < (1L << 31) && (long)batch * Hin * Win * Cin < (1L << 40), "conv2d: too large");
-    GemmArgs a{};
     a.A = X; a.B = Wt; a.C = Y; a.R = R; a.scale = scale; a.bias = bias; a.row_mask = nullptr;
     a.M = (int)M; a.N = Cout; a.K = KH * KW * Cin; a.lda = 0; a.ldb = KH * KW * Cin; a.ldc = ldy; a.ldr = ldr;
     a.relu = relu;
@@ -746,10 +871,31 @@ extern "C" int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, i
         KINET_CHECK_ARG(rb < (1LL << 31), "conv2d: residual larger than 2 GiB (split the batch)");
         a.r_bytes = (int)rb;
     }
-    if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
-        // a 1x1 stride-1 convolution over NHWC rows is the plain GEMM Y = X W^T (lda = Cin)
-        a.lda = Cin;
-        return dispatch<false>(a, in_dtype, in_dtype, (hipStream_t)stream);
-    }
+    if (KH == 1 && KW == 1 && stride == 1 && pad == 0) a.lda = Cin;   // plain GEMM over NHWC rows
+    return KINET_OK;
+}
+
+extern "C" int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin, int Hout,
+                            int Wout, int Cout, int KH, int KW, int stride, int pad, int in_dtype, const float* scale,
+                            const float* bias, const void* R, int ldr, int relu, int ldy, kinet_stream_t stream) {
+    GemmArgs a{};
+    int rc = conv_args(a, X, Wt, Y, batch, Hin, Win, Cin, Hout, Wout, Cout, KH, KW, stride, pad, in_dtype, scale, bias,
+                       R, ldr, relu, ldy);
+    if (rc) return rc;
+    // a 1x1 stride-1 convolution over NHWC rows is the plain GEMM Y = X W^T (lda = Cin)
+    if (a.lda) return dispatch<false>(a, in_dtype, in_dtype, (hipStream_t)stream);
     return dispatch<true>(a, in_dtype, in_dtype, (hipStream_t)stream);
+}
+
+extern "C" int kinet_conv2d_splitk(const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin,
+                                   int Hout, int Wout, int Cout, int KH, int KW, int stride, int pad, int in_dtype,
+                                   const float* scale, const float* bias, const void* R, int ldr, int relu, int ldy,
+                                   float* workspace, int ksplit, kinet_stream_t stream) {
+    GemmArgs a{};
+    int rc = conv_args(a, X, Wt, Y, batch, Hin, Win, Cin, Hout, Wout, Cout, KH, KW, stride, pad, in_dtype, scale, bias,
+                       R, ldr, relu, ldy);
+    if (rc) return rc;
+    if (a.M == 0) return KINET_OK;
+    if (a.lda) return run_splitk<false>(a, in_dtype, in_dtype, workspace, ksplit, (hipStream_t)stream);
+    return run_splitk<true>(a, in_dtype, in_dtype, workspace, ksplit, (hipStream_t)stream);
 }

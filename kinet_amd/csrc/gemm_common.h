@@ -28,6 +28,10 @@ struct GemmArgs {
     // C[((g*hm_batch + b)*hm_rows + s)*hm_d + d]  -- the MSDA value layout (heads, B, S, D)
     int hm_rows, hm_d, hm_batch;
     int M, N, K, lda, ldb, ldc, ldr, relu;
+    // split-K (gemm_kernel only): blockIdx.y = K slice of kchunk elements, whose f32 partial
+    // tile goes to C + blockIdx.y * c_slice (no epilogue; splitk_finalize applies it)
+    int kchunk;
+    long c_slice;
     int Hin, Win, Cin, Hout, Wout, KW, stride, pad;
 };
 

@@ -84,6 +84,25 @@ def f32(t):
 
 
 # ----------------------------------------------------------------------------------- GEMM
+def ksplit_for(M, N, K, ln=False):
+    """Split-K factor for long-K problems with too few output tiles to fill the 256 CUs
+    (the tile estimate mirrors launch() in csrc/gemm.hip); 1 = no split."""
+    if K < 1024 or M == 0:
+        return 1
+    if ln:
+        bm, bn = (32 if M <= 8192 else 64), (256 if N <= 256 else 320)
+    elif M <= 4096:
+        bm, bn = 32, 64
+    else:
+        bn = 64 if N <= 64 else 128
+        bm = 64 if ((M + 127) // 128) * ((N + bn - 1) // bn) < 512 else 128
+    tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
+    if tiles >= 256:
+        return 1
+    ks = min(8, max(2, 768 // tiles), K // 256)
+    return ks if ks >= 2 else 1
+
+
 def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_dtype=None,
            scale=None, out=None, x_add=None, ln=None):
     """y = LN?(relu?((x [+ x_add]) @ W^T * scale + bias + residual)); rows with row_mask -> 0.
@@ -125,11 +144,19 @@ def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_d
         mask = row_mask.reshape(-1).to(torch.uint8).contiguous()
     e = x.element_size()
     g, b, eps = (f32(ln[0]), f32(ln[1]), float(ln[2])) if ln is not None else (None, None, 0.0)
+    work = {'family': 'gemm', 'flops': 2.0 * M * Nout * K, 'shape': (M, Nout, K),
+            'bytes': (M * K + Nout * K) * e + M * Nout * out.element_size() * (2 if r is not None else 1)}
+    ks = ksplit_for(M, Nout, K, ln is not None) if a2 is None else 1
+    if ks > 1:
+        ws = torch.empty(ks * M * Nout, dtype=torch.float32, device=x.device)
+        N.call('kinet_gemm_splitk', N.ptr(x2), N.ptr(w), N.ptr(out), M, Nout, K, x2.stride(0), K, ldc,
+               N.dtype_code(x.dtype), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(r), ldr, int(relu),
+               N.ptr(g), N.ptr(b), eps, N.dtype_code(odt), N.ptr(mask), N.ptr(ws), ks, N.stream(x.device),
+               work=work)
+        return out.view(*lead, Nout) if out.is_contiguous() else out
     N.call('kinet_gemm_ex', N.ptr(x2), N.ptr(a2), N.ptr(w), N.ptr(out), M, Nout, K, x2.stride(0), K, ldc,
            N.dtype_code(x.dtype), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(r), ldr, int(relu),
-           N.ptr(g), N.ptr(b), eps, N.dtype_code(odt), N.ptr(mask), N.stream(x.device),
-           work={'family': 'gemm', 'flops': 2.0 * M * Nout * K, 'shape': (M, Nout, K),
-                 'bytes': (M * K + Nout * K) * e + M * Nout * out.element_size() * (2 if r is not None else 1)})
+           N.ptr(g), N.ptr(b), eps, N.dtype_code(odt), N.ptr(mask), N.stream(x.device), work=work)
     return out.view(*lead, Nout) if out.is_contiguous() else out
 
 
@@ -182,12 +209,17 @@ def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, res
     if residual is not None:
         r = residual
     e = x.element_size()
-    N.call('kinet_conv2d', N.ptr(x), N.ptr(w_packed), N.ptr(out), B, H, W, Cin, Ho, Wo, Cout, KH, KW,
-           stride, pad, N.dtype_code(x.dtype), N.ptr(scale), N.ptr(bias), N.ptr(r),
-           Cout if r is not None else 0, int(relu), ldy, N.stream(x.device),
-           work={'family': 'conv', 'flops': 2.0 * B * Ho * Wo * Cout * KH * KW * Cin,
-                 'shape': (B, H, W, Cin, Cout, KH, stride),
-                 'bytes': (B * H * W * Cin + Cout * KH * KW * Cin + B * Ho * Wo * Cout * (2 if r is not None else 1)) * e})
+    work = {'family': 'conv', 'flops': 2.0 * B * Ho * Wo * Cout * KH * KW * Cin,
+            'shape': (B, H, W, Cin, Cout, KH, stride),
+            'bytes': (B * H * W * Cin + Cout * KH * KW * Cin + B * Ho * Wo * Cout * (2 if r is not None else 1)) * e}
+    args = (N.ptr(x), N.ptr(w_packed), N.ptr(out), B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+            N.dtype_code(x.dtype), N.ptr(scale), N.ptr(bias), N.ptr(r), Cout if r is not None else 0, int(relu), ldy)
+    ks = ksplit_for(B * Ho * Wo, Cout, KH * KW * Cin)
+    if ks > 1:
+        ws = torch.empty(ks * B * Ho * Wo * Cout, dtype=torch.float32, device=x.device)
+        N.call('kinet_conv2d_splitk', *args, N.ptr(ws), ks, N.stream(x.device), work=work)
+    else:
+        N.call('kinet_conv2d', *args, N.stream(x.device), work=work)
     return out
 
 

@@ -327,3 +327,39 @@ def test_rw_conv1x1(K, Cin, Cout):
     torch.cuda.synchronize()
     err = (y.permute(0, 3, 1, 2).float().cpu() - ref).abs()
     assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
+
+
+# ---- split-K (few output tiles, long K): f32 slice partials + finalize epilogue ----------------
+
+@pytest.mark.parametrize('M,N,Kd,mode', [(1200, 256, 1024, 'res_ln_mask'), (4200, 256, 2048, 'plain'),
+                                         (1000, 91, 2048, 'relu'), (300, 1100, 1024, 'res')])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_splitk_linear_vs_fp32(K, M, N, Kd, mode, dtype):
+    assert K.ksplit_for(M, N, Kd, 'ln' in mode) > 1
+    x, w, b, kw, ref = _rw_case(M, N, Kd, mode, M + Kd)
+    xx = x.float().to(dtype) if dtype == torch.float32 else x
+    if dtype == torch.float32 and 'res' in mode:
+        kw['residual'] = kw['residual'].float()
+    y = K.linear(xx.cuda(), w.cuda().to(dtype), b.cuda(), **kw)
+    torch.cuda.synchronize()
+    err = (y.float().cpu() - ref).abs()
+    tol = (1e-4 * ref.abs() + 1e-4) if dtype == torch.float32 else (1e-2 * ref.abs() + 2e-2)
+    assert (err <= tol).all(), err.max().item()
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_splitk_conv_vs_fp32(K, dtype):
+    """input_proj of the last level: 3x3 stride-2 conv 2048 -> 256 on a small map (M ~ 1k, K 18k)."""
+    B, H, W, Cin, Cout = 2, 25, 42, 2048, 256
+    assert K.ksplit_for(B * 13 * 21, Cout, 9 * Cin) > 1
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(B, Cin, H, W, generator=g).to(dtype)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * (2.0 / (Cin * 9)) ** 0.5).to(dtype)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    ref = F.conv2d(x.float(), w.float(), stride=2, padding=1) + bias[None, :, None, None]
+    y = K.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().cuda(), K.pack_conv_weight(w.cuda(), dtype), 2, 1,
+                      bias=bias.cuda())
+    torch.cuda.synchronize()
+    err = (y.permute(0, 3, 1, 2).float().cpu() - ref).abs()
+    tol = (1e-4 * ref.abs() + 1e-4) if dtype == torch.float32 else (1e-2 * ref.abs() + 2e-2)
+    assert (err <= tol).all(), err.max().item()
