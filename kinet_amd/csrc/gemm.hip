@@ -833,6 +833,7 @@ extern "C" int kinet_gemm_splitk(const void* A, const void* B, void* C, int M, i
 extern "C" int kinet_gemm_set_flags(int flags) {
     const int old = kinet_gemm_flags;
     kinet_gemm_flags = flags;
+    kinet::rw_min_m = (flags & 8) ? 256 : 4096;
     return old;
 }
 

@@ -37,6 +37,7 @@ struct GemmArgs {
 
 // gemm_rw.hip: resident-weight streaming GEMM; false = problem not eligible
 bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t stream);
+extern int rw_min_m;
 
 namespace {
 

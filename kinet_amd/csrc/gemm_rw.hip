@@ -365,11 +365,13 @@ bool al16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
 
 }  // namespace
 
+int rw_min_m = 4096;   // smallest M routed to the resident-weight kernel (kinet_gemm_set_flags bit 3: 256)
+
 // Entry from gemm.hip's dispatcher: launch the resident-weight kernel when the problem
 // fits it; false leaves the call to the tiled kernel.
 bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t stream) {
     if (in_dtype != KINET_BF16 && in_dtype != KINET_F16) return false;
-    if (a.M < 4096 || (a.K != 64 && a.K != 128 && a.K != 256)) return false;
+    if (a.M < rw_min_m || (a.K != 64 && a.K != 128 && a.K != 256)) return false;
     if (a.A2 != nullptr && (a.R != nullptr || a.ln_g != nullptr || !al16(a.A2))) return false;
     if (a.N % 8 != 0 || (a.ln_g != nullptr && a.N > 256)) return false;
     const bool o16 = out_dtype == in_dtype || (in_dtype == KINET_BF16 && out_dtype == KINET_F16);

@@ -8,7 +8,8 @@ returns the argparse.Namespace build_model expects (util/misc.py:668-674 equival
 from argparse import Namespace
 
 DEFAULTS = dict(
-    lr=0.0002, lr_backbone=0.00002, lr_linear_proj_mult=0.1, lr_track=0.0001, batch_size=2,
+    lr=0.0002, lr_backbone_names=['backbone.0'], lr_backbone=0.00002,
+    lr_linear_proj_names=['reference_points', 'sampling_offsets'], lr_linear_proj_mult=0.1, lr_track=0.0001, batch_size=2,
     weight_decay=0.0001, epochs=50, lr_drop=40, clip_max_norm=0.1,
     deformable=False, kine=False, with_box_refine=False, two_stage=False, freeze_detr=False,
     backbone='resnet50', dilation=False, position_embedding='sine', num_feature_levels=1,

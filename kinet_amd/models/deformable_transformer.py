@@ -44,8 +44,23 @@ def _get_activation_fn(activation):
     raise RuntimeError(F"activation should be relu/gelu, not {activation}.")
 
 
+_FORCE_REFERENCE = [0]
+
+
 def fast_path():
-    return not torch.is_grad_enabled()
+    """HIP inference path: no autograd, and not inside reference_path()."""
+    return not torch.is_grad_enabled() and not _FORCE_REFERENCE[0]
+
+
+class reference_path:
+    """Run the op-for-op module path even without grad (e.g. the no-grad previous-frame
+    pass of training, which the reference runs in train mode -- with dropout)."""
+
+    def __enter__(self):
+        _FORCE_REFERENCE[0] += 1
+
+    def __exit__(self, *exc):
+        _FORCE_REFERENCE[0] -= 1
 
 
 class DeformableTransformerEncoderLayer(nn.Module):

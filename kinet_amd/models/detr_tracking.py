@@ -33,9 +33,12 @@ class DETRTrackingBase(nn.Module):
         self._tracking = True
 
     def forward(self, samples, targets: list = None, prev_features=None):
+        """detr_tracking.py:220-283: with targets and not tracking, training runs the
+        two-pass track-query scheme (kinet_amd.models.training), evaluation adds empty
+        track-query fields."""
         if targets is not None and not self._tracking:
             from kinet_amd.models import training
-            training.prepare_track_queries(self, targets)
+            prev_features = training.prepare_track_queries(self, targets, super().forward, prev_features)
         return super().forward(samples, targets, prev_features)
 
 

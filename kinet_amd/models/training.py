@@ -1,18 +1,28 @@
-"""Host-side training glue of the tracking detector (detr_tracking.py:220-283).
+"""Host-side training glue of the tracking detector: track-query sampling and the
+two-pass forward (src/trackformer/models/detr_tracking.py:39-283).
 
-Evaluation with targets (not tracking): no track queries -- empty track-query fields
-(detr_tracking.py:259-270).  The training two-pass scheme (previous-frame forward without
-grad -> Hungarian matching -> track-query sampling -> current-frame forward with grad)
-lives here as well once the matcher/criterion land.
+Training step of a sample pair (detr_tracking.py:225-265): the previous frame is run
+without grad (the HIP inference path), Hungarian-matched to its targets on the host,
+a random subset of the matched detections becomes the current frame's track queries
+(plus false positives drawn near them), and the current frame runs with grad.
+
+`add_track_queries_to_targets` makes exactly the reference's sequence of torch
+global-RNG calls (randint, randint, then per sample randperm / randperm / multinomial or
+randperm), so a seeded run draws the same track queries as the reference -- pinned by
+tests/golden/train_sampler.npz.  The reference's distance weight uses the x offset twice
+(`box_weights[:, 0] ** 2 + box_weights[:, 0] ** 2`, :128); kept for parity.
 """
+import contextlib
+import math
+
 import torch
+from torch import nn
+
+from kinet_amd.models.deformable_transformer import reference_path
 
 
-def prepare_track_queries(model, targets):
-    if model.training:
-        raise NotImplementedError(
-            'two-pass track-query training (detr_tracking.py:225-255) is not wired yet; '
-            'run tracking mode (model.tracking()) or pass track queries explicitly')
+def empty_track_queries(model, targets):
+    """Evaluation with targets: detection only, no track queries (detr_tracking.py:259-270)."""
     for target in targets:
         device = target['boxes'].device
         target['track_query_hs_embeds'] = torch.zeros(0, model.hidden_dim).float().to(device)
@@ -20,3 +30,108 @@ def prepare_track_queries(model, targets):
         target['track_queries_fal_pos_mask'] = torch.zeros(model.num_queries).bool().to(device)
         target['track_query_boxes'] = torch.zeros(0, 4).to(device)
         target['track_query_match_ids'] = torch.tensor([]).long().to(device)
+
+
+def add_track_queries_to_targets(model, targets, prev_indices, prev_out, add_false_pos=True):
+    """detr_tracking.py:39-218."""
+    device = prev_out['pred_boxes'].device
+    fp_prob = model._track_query_false_positive_prob
+    fn_prob = model._track_query_false_negative_prob
+    min_prev_target_ind = min([len(prev_ind[1]) for prev_ind in prev_indices])
+    num_prev_target_ind = 0
+    if min_prev_target_ind:
+        num_prev_target_ind = torch.randint(0, min_prev_target_ind + 1, (1,)).item()
+    num_prev_target_ind_for_fps = 0
+    if num_prev_target_ind:
+        num_prev_target_ind_for_fps = torch.randint(int(math.ceil(fp_prob * num_prev_target_ind)) + 1, (1,)).item()
+
+    num_q_all = prev_out['pred_boxes'].shape[1]
+    for i, (target, prev_ind) in enumerate(zip(targets, prev_indices)):
+        prev_out_ind, prev_target_ind = prev_ind
+        if fn_prob:
+            # random subset of the matched detections (:62-79)
+            random_subset_mask = torch.randperm(len(prev_target_ind))[:num_prev_target_ind]
+            prev_out_ind = prev_out_ind[random_subset_mask.to(prev_out_ind.device)]
+            prev_target_ind = prev_target_ind[random_subset_mask.to(prev_target_ind.device)]
+
+        # match track ids between frames (:82-94)
+        prev_track_ids = target['prev_target']['track_ids'][prev_target_ind.to(target['prev_target']['track_ids'].device)]
+        match = prev_track_ids.unsqueeze(dim=1).eq(target['track_ids'])
+        target_ind_matching = match.any(dim=1)
+        target['track_query_match_ids'] = match.nonzero()[:, 1]
+
+        if add_false_pos:
+            # random false positives next to matched detections (:97-158)
+            prev_boxes_matched = prev_out['pred_boxes'][i, prev_out_ind[target_ind_matching.to(prev_out_ind.device)]]
+            taken = set(int(v) for v in prev_out_ind.tolist())
+            not_prev_out_ind = [ind for ind in range(num_q_all) if ind not in taken]
+            random_false_out_ind = []
+            prev_target_ind_for_fps = torch.randperm(num_prev_target_ind)[:num_prev_target_ind_for_fps]
+            for j in prev_target_ind_for_fps:
+                prev_boxes_unmatched = prev_out['pred_boxes'][i, not_prev_out_ind]
+                if len(prev_boxes_matched) > j:
+                    prev_box_matched = prev_boxes_matched[j]
+                    box_weights = prev_box_matched.unsqueeze(dim=0)[:, :2] - prev_boxes_unmatched[:, :2]
+                    box_weights = box_weights[:, 0] ** 2 + box_weights[:, 0] ** 2   # (sic, :128)
+                    box_weights = torch.sqrt(box_weights)
+                    random_false_out_idx = not_prev_out_ind.pop(torch.multinomial(box_weights.cpu(), 1).item())
+                else:
+                    random_false_out_idx = not_prev_out_ind.pop(torch.randperm(len(not_prev_out_ind))[0])
+                random_false_out_ind.append(random_false_out_idx)
+            prev_out_ind = torch.tensor(prev_out_ind.tolist() + random_false_out_ind).long()
+            target_ind_matching = torch.cat([target_ind_matching,
+                                             torch.tensor([False, ] * len(random_false_out_ind)).bool().to(device)])
+
+        # track query masks (:174-184); queries are prepended to the object queries
+        track_queries_mask = torch.ones_like(target_ind_matching).bool()
+        track_queries_fal_pos_mask = torch.zeros_like(target_ind_matching).bool()
+        track_queries_fal_pos_mask[~target_ind_matching] = True
+        prev_out_ind = prev_out_ind.to(device)
+        target['track_query_hs_embeds'] = prev_out['hs_embed'][i, prev_out_ind]
+        target['track_query_boxes'] = prev_out['pred_boxes'][i, prev_out_ind].detach()
+        target['track_queries_mask'] = torch.cat([
+            track_queries_mask, torch.tensor([False, ] * model.num_queries).to(device)]).bool()
+        target['track_queries_fal_pos_mask'] = torch.cat([
+            track_queries_fal_pos_mask, torch.tensor([False, ] * model.num_queries).to(device)]).bool()
+
+
+def _has_dropout(model):
+    return any(isinstance(m, (nn.Dropout, nn.MultiheadAttention)) and getattr(m, 'p', getattr(m, 'dropout', 0)) > 0
+               for m in model.modules())
+
+
+def _without_aux(out):
+    return {k: v for k, v in out.items() if 'aux_outputs' not in k}
+
+
+def prepare_track_queries(model, targets, base_forward, prev_features=None):
+    """detr_tracking.py:221-270.  `base_forward` is the plain detector forward
+    (DeformableDETR.forward of `model`).  Returns the prev_features the current-frame
+    forward uses (the previous frame's backbone features in training, else the caller's)."""
+    if not model.training:
+        empty_track_queries(model, targets)
+        return prev_features
+    if model._matcher is None:
+        raise RuntimeError('training the tracking model needs the Hungarian matcher (build_model sets it)')
+    prev_targets = [target['prev_target'] for target in targets]
+    grad_ctx = torch.enable_grad() if model._backprop_prev_frame else torch.no_grad()
+    # the reference runs the previous frame in train mode, so with dropout > 0 it must take
+    # the op-for-op path (dropout included) rather than the HIP inference path
+    path_ctx = reference_path() if _has_dropout(model) else contextlib.nullcontext()
+    with grad_ctx, path_ctx:
+        if 'prev_prev_image' in targets[0]:
+            for target, prev_target in zip(targets, prev_targets):
+                prev_target['prev_target'] = target['prev_prev_target']
+            prev_prev_targets = [target['prev_prev_target'] for target in targets]
+            prev_prev_out, _, prev_prev_features, _, _ = base_forward([t['prev_prev_image'] for t in targets])
+            prev_prev_indices = model._matcher(_without_aux(prev_prev_out), prev_prev_targets)
+            add_track_queries_to_targets(model, prev_targets, prev_prev_indices, prev_prev_out, add_false_pos=False)
+            prev_out, _, prev_features, _, _ = base_forward([t['prev_image'] for t in targets], prev_targets,
+                                                            prev_prev_features)
+        else:
+            prev_out, _, prev_features, _, _ = base_forward([t['prev_image'] for t in targets])
+        prev_indices = model._matcher(_without_aux(prev_out), prev_targets)
+        device = prev_targets[0]['labels'].device
+        prev_indices = [(o.to(device), t.to(device)) for o, t in prev_indices]
+        add_track_queries_to_targets(model, targets, prev_indices, prev_out)
+    return prev_features

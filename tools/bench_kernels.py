@@ -31,7 +31,7 @@ def gemm():
     dt = torch.bfloat16
     print('--- GEMM (bf16 in/out, bias) ---')
     for M, N, Kd in [(4096, 4096, 4096), (8192, 8192, 8192), (88892, 256, 256), (88892, 384, 256),
-                     (88892, 1024, 256), (88892, 256, 1024), (1200, 256, 256), (1200, 512, 256)]:
+                     (88892, 1024, 256), (88892, 256, 1024), (1200, 256, 256), (1200, 512, 256), (1200, 1024, 256), (1200, 384, 256)]:
         x = torch.randn(M, Kd, device='cuda', dtype=dt)
         w = torch.randn(N, Kd, device='cuda') * 0.02
         b = torch.randn(N, device='cuda')
@@ -83,6 +83,10 @@ def model():
 
 if __name__ == '__main__':
     which = sys.argv[1:] or ['gemm', 'model']
+    if 'rwsmall' in which:  # route small-M K<=256 GEMMs to the resident-weight kernel too
+        from kinet_amd import _native
+        _native.lib().kinet_gemm_set_flags(8)
+        print('[bench_kernels] GEMM flags = 8 (resident-weight kernel from M >= 256)')
     if 'norw' in which:    # never use the resident-weight streaming kernel
         from kinet_amd import _native
         _native.lib().kinet_gemm_set_flags(4)
