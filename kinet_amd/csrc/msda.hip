@@ -501,10 +501,10 @@ __device__ __forceinline__ void widen2(uint32_t u, f32x2& x) {
     }
 }
 
-template <typename T, typename TO, int L, int P>
+template <typename T, typename TO, typename TL, int L, int P>
 __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
     const T* __restrict__ value, long vsb, int vss, long vsm, int head_bytes, const int64_t* __restrict__ shapes,
-    const float* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
+    const TL* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
     const uint8_t* __restrict__ qmask, float* __restrict__ loc_out, float* __restrict__ attw_out,
     TO* __restrict__ out, int S, int M, int Lq) {
     static_assert(sizeof(T) == 2 && sizeof(TO) == 2, "16-bit values and output");
@@ -554,9 +554,9 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
         const int ml = s / (QT * LP), qi = (s / LP) % QT, lp = s % LP, l = lp / P;
         const int m = mh0 + ml, q = q0 + qi;
         const bool ok = q < Lq && m < M;
-        const float* orow = offlog + ((long)b * Lq + (ok ? q : 0)) * ld_off;
+        const TL* orow = offlog + ((long)b * Lq + (ok ? q : 0)) * ld_off;
         // softmax over the LP consecutive lanes of one (query, head) (ms_deform_attn.py:71-72)
-        const float logit = ok ? orow[M * LP * 2 + (ok ? m : 0) * LP + lp] : -INFINITY;
+        const float logit = ok ? to_f32(orow[M * LP * 2 + (ok ? m : 0) * LP + lp]) : -INFINITY;
         const float mx = group_reduce<LP, true>(logit);
         const float e = ok ? __expf(logit - mx) : 0.f;
         const float sum = group_reduce<LP, false>(e);
@@ -566,7 +566,14 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
         for (int k = 0; k < 4; ++k) { t4.off[k] = (int)OOB; t4.w[k] = 0.f; }
         if (ok) {
             if (qmask && qmask[(long)b * Lq + q]) a = 0.f;                  // ms_deform_attn.py:73-74
-            const float2 o2 = *reinterpret_cast<const float2*>(orow + (m * LP + lp) * 2);
+            float2 o2;
+            if constexpr (std::is_same<TL, float>::value) {
+                o2 = *reinterpret_cast<const float2*>(orow + (m * LP + lp) * 2);
+            } else {
+                const uint32_t u = *reinterpret_cast<const uint32_t*>(orow + (m * LP + lp) * 2);
+                o2.x = (float)__builtin_bit_cast(f16_t, (uint16_t)(u & 0xffffu));
+                o2.y = (float)__builtin_bit_cast(f16_t, (uint16_t)(u >> 16));
+            }
             const float* rp = ref + (((long)b * Lq + q) * L + l) * ref_dim;
             float x, y;
             if (ref_dim == 2) {   // offsets / spatial_shapes[(H, W)] on (x, y): the reference's quirk (:77-79)
@@ -959,8 +966,8 @@ extern "C" int kinet_msda_forward(const void* value, const int64_t* spatial_shap
 
 namespace kinet {
 namespace {
-template <typename T, typename TO = T>
-int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* shapes, const float* offlog,
+template <typename T, typename TO = T, typename TL = float>
+int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* shapes, const void* offlog_v,
                  int ld_off, const float* ref, int ref_dim, const uint8_t* qmask, void* out, float* loc_out,
                  float* attw_out, int N, int S, int M, int D, int L, int Lq, int P, hipStream_t stream) {
     const Cfg c = pick_cfg(D, M, sizeof(T));
@@ -973,19 +980,23 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
             ((uintptr_t)value % 16) == 0 && head_bytes < (1LL << 31) && !(msda_flags & 1)) {
             dim3 grid((Lq + 15) / 16, N, (M + 3) / 4);
             if (L == 4)
-                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, 4, 4>), grid, dim3(kThreads), 0, stream, (const T*)value,
-                                   vsb, vss, vsm, (int)head_bytes, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out,
+                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 4, 4>), grid, dim3(kThreads), 0, stream,
+                                   (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v, ld_off,
+                                   ref, ref_dim, qmask, loc_out,
                                    attw_out, (TO*)out, S, M, Lq);
             else
-                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, 8, 4>), grid, dim3(kThreads), 0, stream, (const T*)value,
-                                   vsb, vss, vsm, (int)head_bytes, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out,
+                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 8, 4>), grid, dim3(kThreads), 0, stream,
+                                   (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v, ld_off,
+                                   ref, ref_dim, qmask, loc_out,
                                    attw_out, (TO*)out, S, M, Lq);
             KINET_LAUNCH_CHECK();
             return KINET_OK;
         }
     }
-    KINET_CHECK_ARG((std::is_same<T, TO>::value), "msda fused: output dtype != value dtype needs head_dim 32, "
+    KINET_CHECK_ARG((std::is_same<T, TO>::value && std::is_same<TL, float>::value),
+                    "msda fused: output dtype != value dtype or f16 offsets/logits need head_dim 32, "
                     "L*P in {16, 32}, P = 4 and aligned strides");
+    const float* offlog = (const float*)offlog_v;
     KINET_CHECK_ARG(vsb % c.vec == 0 && vss % c.vec == 0 && vsm % c.vec == 0 && ((uintptr_t)value % 16) == 0,
                     "msda fused: value strides must keep %d-element vectors aligned", c.vec);
     const int QT = 64 / c.lpq;          // queries per wave (= per workgroup)
@@ -996,7 +1007,7 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
     const size_t lds = sizeof(LevelInfo) + nsamp * sizeof(Tap4) + (pow2 ? 0 : nsamp * sizeof(float));
     KINET_CHECK_ARG(lds <= 160 * 1024, "msda fused: LDS request %zu too large", lds);
     dim3 grid((Lq + QT - 1) / QT, N, (M + MH - 1) / MH);
-    if constexpr (!std::is_same<T, TO>::value) return KINET_ERR_ARG;   // (rejected above)
+    if constexpr (!std::is_same<T, TO>::value || !std::is_same<TL, float>::value) return KINET_ERR_ARG;   // (rejected above)
 #define KF(VEC)                                                                                                  \
     hipLaunchKernelGGL((msda_fused_kernel<T, VEC>), grid, dim3(kThreads), lds, stream, (const T*)value, vsb, vss, \
                        vsm, shapes, offlog, ld_off, ref, ref_dim, qmask, loc_out, attw_out, (T*)out, S, M, D, L,   \
@@ -1025,7 +1036,7 @@ extern "C" int kinet_msda_fused_forward(const void* value, int64_t value_sb, int
                                         const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
                                         void* output, float* loc_out, float* attw_out, int batch, int spatial_size,
                                         int num_heads, int channels, int num_levels, int num_query, int num_point,
-                                        int value_dtype, int output_dtype, kinet_stream_t stream) {
+                                        int value_dtype, int output_dtype, int offlog_dtype, kinet_stream_t stream) {
     int rc = common_checks(batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, 1);
     if (rc) return rc;
     KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.", ref_dim);
@@ -1042,11 +1053,20 @@ extern "C" int kinet_msda_fused_forward(const void* value, int64_t value_sb, int
     const int vec_el = (int)(16 / (es ? es : 1));
     (void)vec_el;
     hipStream_t s = (hipStream_t)stream;
-#define ARGS value, (long)value_sb, (int)value_ss, (long)value_sm, spatial_shapes, (const float*)offsets_logits, ld_off, \
+#define ARGS value, (long)value_sb, (int)value_ss, (long)value_sm, spatial_shapes, offsets_logits, ld_off, \
              ref_points, ref_dim, query_attn_mask, output, loc_out, attw_out, batch, spatial_size, num_heads, channels, \
              num_levels, num_query, num_point, s
     KINET_CHECK_ARG(output_dtype == value_dtype || (value_dtype == KINET_F16 && output_dtype == KINET_BF16),
                     "msda fused forward: output dtype %d unsupported for value dtype %d", output_dtype, value_dtype);
+    KINET_CHECK_ARG(offlog_dtype == KINET_F32 || offlog_dtype == KINET_F16,
+                    "msda fused forward: offsets/logits must be f32 or f16 (got %d)", offlog_dtype);
+    if (offlog_dtype == KINET_F16) {
+        if (value_dtype == KINET_F16 && output_dtype == KINET_BF16) return launch_fused<f16_t, bf16_t, f16_t>(ARGS);
+        if (value_dtype == KINET_F16 && output_dtype == KINET_F16) return launch_fused<f16_t, f16_t, f16_t>(ARGS);
+        if (value_dtype == KINET_BF16 && output_dtype == KINET_BF16) return launch_fused<bf16_t, bf16_t, f16_t>(ARGS);
+        set_error("msda fused forward: f16 offsets/logits need 16-bit values");
+        return KINET_ERR_ARG;
+    }
     if (value_dtype == KINET_F16 && output_dtype == KINET_BF16) return launch_fused<f16_t, bf16_t>(ARGS);
     if (value_dtype == KINET_F32) return launch_fused<float>(ARGS);
     if (value_dtype == KINET_BF16) return launch_fused<bf16_t>(ARGS);

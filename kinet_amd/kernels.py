@@ -319,7 +319,8 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
     """Sampling of MSDeformAttn.forward (ms_deform_attn.py:69-87) in one kernel.
     value: projected values, either (B, S, d) row-major (column slices allowed) or, with
     head_major=True, (M, B, S, D) as written by value_proj_headmajor;
-    offlog (B, Lq, M*L*P*3) f32 [offsets | logits]; reference_points (B, Lq, L, 2|4) f32.
+    offlog (B, Lq, M*L*P*3) f32 (or f16 with 16-bit values) [offsets | logits];
+    reference_points (B, Lq, L, 2|4) f32.
     out_dtype: value.dtype, or bfloat16 from float16 values (mixed-precision gather path).
     Returns (B, Lq, d) [, loc, attw]."""
     if head_major:
@@ -348,16 +349,18 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
         loc = torch.empty((B, Lq, n_heads, n_levels, n_points, 2), dtype=torch.float32, device=value.device)
         attw = torch.empty((B, Lq, n_heads, n_levels, n_points), dtype=torch.float32, device=value.device)
     qm = query_attn_mask.to(torch.uint8).contiguous() if query_attn_mask is not None else None
-    if offlog.dtype != torch.float32:
-        raise RuntimeError('msda_fused: the offsets/logits projection must be f32')
+    if offlog.dtype not in (torch.float32, torch.float16):
+        raise RuntimeError('msda_fused: the offsets/logits projection must be f32 or f16')
     ev = value.element_size()
     nsamp = B * Lq * n_heads * n_levels * n_points
     N.call('kinet_msda_fused_forward', N.ptr(value), vsb, vss, vsm, N.ptr(spatial_shapes), N.ptr(offlog),
            offlog.shape[-1], N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), N.ptr(loc), N.ptr(attw), B, S,
-           n_heads, D, n_levels, Lq, n_points, N.dtype_code(value.dtype), N.dtype_code(od), N.stream(value.device),
+           n_heads, D, n_levels, Lq, n_points, N.dtype_code(value.dtype), N.dtype_code(od), N.dtype_code(offlog.dtype),
+           N.stream(value.device),
            work={'family': 'msda', 'flops': 10.0 * nsamp * D,
                  # compulsory bytes: value once, f32 offsets+logits, refs, output once
-                 'bytes': B * S * d * ev + nsamp * 3 * 4 + ref.numel() * 4 + B * Lq * d * out.element_size()
+                 'bytes': B * S * d * ev + nsamp * 3 * offlog.element_size() + ref.numel() * 4
+                 + B * Lq * d * out.element_size()
                  + (nsamp * 3 * 4 if want_loc_attw else 0),
                  'Lq': Lq, 'S': S, 'shape': (B, Lq, S)})
     if want_loc_attw:

@@ -124,7 +124,10 @@ class MSDeformAttn(nn.Module):
         (+ query_add, e.g. the position embedding, added at GEMM load time); returns the
         pre-output_proj (N, Lq, d)."""
         w, b = self.packed_offsets_weights()
-        offlog = K.linear(query, w, b, out_dtype=torch.float32, x_add=query_add)
+        # bf16 compute: offsets/logits in f16 (half the bytes of f32 through HBM twice; f16
+        # keeps 11 mantissa bits for the pixel offsets); parity mode stays f32
+        od = torch.float16 if query.dtype == torch.bfloat16 else torch.float32
+        offlog = K.linear(query, w, b, out_dtype=od, x_add=query_add)
         return K.msda_fused(value, input_spatial_shapes, offlog, reference_points,
                             self.n_heads, self.n_levels, self.n_points, query_attn_mask,
                             head_major=(value.dim() == 4), out_dtype=query.dtype)

@@ -214,3 +214,24 @@ def test_fast_fused_f16_values_bf16_out():
     assert (d <= o_h.float().abs() * 2.0 ** -8 + 1e-6).all(), d.max().item()
     with pytest.raises(RuntimeError):
         K.msda_fused(value.float(), ss, offlog, ref, M, 4, P, head_major=True, out_dtype=torch.bfloat16)
+
+
+def test_fast_fused_f16_offsets_logits():
+    """f16 offsets/logits (bf16 compute path) vs the same values in f32: sampling locations
+    differ only by the f16 rounding of the offsets."""
+    from kinet_amd import kernels as K
+    shapes = ((40, 50), (20, 25), (10, 13), (5, 7))
+    B, M, P, Lq = 2, 8, 4, 1500
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 13, dtype=torch.float16)
+    oh = offlog.half()
+    o32, loc32, aw32 = K.msda_fused(value, ss, oh.float(), ref, M, 4, P, qmask, want_loc_attw=True, head_major=True,
+                                    out_dtype=torch.bfloat16)
+    o16, loc16, aw16 = K.msda_fused(value, ss, oh, ref, M, 4, P, qmask, want_loc_attw=True, head_major=True,
+                                    out_dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    # identical input values (the f32 tensor holds the f16 values exactly): the two
+    # instantiations agree up to instruction selection (fma contraction)
+    torch.testing.assert_close(loc16, loc32, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(aw16, aw32, rtol=1e-5, atol=1e-7)
+    d = (o16.float() - o32.float()).abs()
+    assert (d <= o32.float().abs() * 2.0 ** -7 + 1e-4).all(), d.max().item()
