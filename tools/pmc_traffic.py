@@ -13,7 +13,25 @@ import re
 import sys
 
 
+def _mangled_name(name):
+    """Last <len><ident> component of an Itanium nested name (_ZN...<len>name I...): rocprofv3
+    leaves some kernel names mangled in its counter-collection CSVs."""
+    i, last = (3, None) if name.startswith("_ZN") else (2, None)
+    while i < len(name) and name[i].isdigit():
+        j = i
+        while j < len(name) and name[j].isdigit():
+            j += 1
+        n = int(name[i:j])
+        last = name[j:j + n]
+        i = j + n
+    return last
+
+
 def short(name):
+    if name.startswith('_Z'):
+        m = _mangled_name(name)
+        if m:
+            return m
     m = re.search(r'(\w+)<', name) or re.search(r'(\w+)\(', name)
     return m.group(1) if m else name
 
