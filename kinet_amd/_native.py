@@ -31,6 +31,9 @@ _SIGS = {
     'kinet_conv2d': [P, P, P] + [I] * 12 + [P, P, P, I, I, I, P],
     'kinet_conv2d_splitk': [P, P, P] + [I] * 12 + [P, P, P, I, I, I, P, I, P],
     'kinet_gemm_splitk': [P, P, P] + [I] * 7 + [P, P, P, I, I, P, P, F, I, P, P, I, P],
+    'kinet_ffn_pack': [P, P, P, I, I, I, P],
+    'kinet_ffn_set_debug': [I],
+    'kinet_ffn_fused': [P, I, P, P, P, P, P, F, P, I, I, I, I, I, P],
     'kinet_layernorm': [P] * 5 + [I, I, F, I, I, P],
     'kinet_groupnorm': [P] * 4 + [I] * 5 + [F, I, P, P],
     'kinet_maxpool2d_3x3s2': [P, P] + [I] * 5 + [P],

@@ -1,0 +1,476 @@
+// Fused post-norm FFN sub-layer for gfx950: y = LN(x + W2 relu(W1 x + b1) + b2), one launch.
+//
+// Reference: DeformableTransformerEncoderLayer.forward_ffn (deformable_transformer.py:284-288)
+// and the decoder twin (:361-365) -- two GEMMs whose (M, F) hidden tensor (F = 1024, i.e. 4x
+// the activations) is written to and re-read from HBM.  Here it never leaves the CU:
+//
+//  * each wave owns 16*RT rows of x, held for the whole launch in VGPRs as MFMA B-operand
+//    fragments (lane l: row l&15, 8 consecutive k);
+//  * the weights stream through a 2-slot LDS ring, one 32-unit hidden chunk per slot
+//    (W1 rows + W2 columns, pre-packed fragment-major by kinet_ffn_pack so one LDS-DMA
+//    wave-instruction moves one 1-KiB operand fragment and every ds_read_b128 is a linear,
+//    conflict-free 1 KiB); all waves of the workgroup share the ring;
+//  * phase A: H^T(32 x rows) = W1c x^T on v_mfma_f32_16x16x32 -- the accumulator layout
+//    puts 4 consecutive hidden units of one row in each lane;  + b1, ReLU, round to the
+//    16-bit type: that IS the B operand of phase B once W2's hidden index is permuted the
+//    same way (done in the pack), so H goes register -> MFMA with no LDS round trip;
+//  * phase B: out^T(D x rows) += W2c H^T, accumulated over the F/32 chunks in VGPRs;
+//  * epilogue in registers: + b2 + residual x (re-read, L2-hot), LayerNorm over the row
+//    (each row's D outputs live in 4 lanes: in-lane sums + 2 cross-lane steps), 8-byte
+//    stores.
+// One barrier per chunk: wait own DMA -> barrier -> issue the next chunk's DMA into the
+// slot everyone just finished -> compute.  Arithmetic intensity per workgroup = its row
+// count (each weight byte feeds 16*RT*WAVES rows), 256 rows at D = 256.
+#include <hip/hip_runtime.h>
+
+#include "../../include/kinet_ffn.h"
+#include "common.h"
+#include "gemm_common.h"
+
+namespace kinet {
+namespace {
+
+struct FfnArgs {
+    const void* X;
+    const void* W;
+    const float* b1;
+    const float* b2;
+    const float* ln_g;
+    const float* ln_b;
+    void* Y;
+    float eps;
+    int ldx, ldy, M, F;
+    int x_bytes, w_bytes, y_bytes;
+    int dbg;   // diagnostic timing knob (kinet_ffn_set_debug): 1 = no weight DMA after the
+               // prologue (results are garbage)
+};
+
+int ffn_debug = 0;
+
+template <int D>
+struct FfnGeo {
+    static_assert(D % 32 == 0, "D must be a multiple of 32");
+    static constexpr int KS = D / 32;        // 32-deep K steps of linear1
+    static constexpr int NT = D / 16;        // 16-wide output tiles of linear2
+    static constexpr int FR = 2 * KS + NT;   // 1-KiB fragments per 32-unit hidden chunk
+    static constexpr int CHUNK = FR * 1024;
+};
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <typename T>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+    if constexpr (std::is_same<T, bf16_t>::value) {
+        return (uint32_t)f32_to_bf16(a).x | ((uint32_t)f32_to_bf16(b).x << 16);
+    } else {
+        return (uint32_t)__builtin_bit_cast(uint16_t, (f16_t)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (f16_t)b) << 16);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void unpack4(u32x2 u, float* v) {
+    if constexpr (std::is_same<T, bf16_t>::value) {
+        v[0] = __uint_as_float(u[0] << 16); v[1] = __uint_as_float(u[0] & 0xffff0000u);
+        v[2] = __uint_as_float(u[1] << 16); v[3] = __uint_as_float(u[1] & 0xffff0000u);
+    } else {
+        v[0] = (float)__builtin_bit_cast(f16_t, (uint16_t)(u[0] & 0xffffu));
+        v[1] = (float)__builtin_bit_cast(f16_t, (uint16_t)(u[0] >> 16));
+        v[2] = (float)__builtin_bit_cast(f16_t, (uint16_t)(u[1] & 0xffffu));
+        v[3] = (float)__builtin_bit_cast(f16_t, (uint16_t)(u[1] >> 16));
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void ffn_wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// raw workgroup barrier for LDS traffic only: LDS-DMA issued earlier stays in flight
+__device__ __forceinline__ void ffn_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+constexpr int FFN_MAX_F = 2048;
+
+// output column of MFMA row m of phase-B tile nt: lane group g holds, for the tile pair
+// (2kp, 2kp+1), the 8 consecutive columns 32kp + 8g .. +7 -- the same columns its phase-A
+// x fragment xr[kp] holds, so the residual comes from registers and stores are 16 bytes
+__host__ __device__ constexpr int ffn_sigma(int nt, int m) { return 32 * (nt >> 1) + 8 * (m >> 2) + 4 * (nt & 1) + (m & 3); }
+
+template <typename T, int D, int RT, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void ffn_fused_kernel(const FfnArgs p, const int ntiles) {
+    using G = FfnGeo<D>;
+    constexpr int KS = G::KS, NT = G::NT, FR = G::FR;
+    static_assert(FR % WAVES == 0, "whole DMA rounds per chunk");
+    constexpr int FRW = FR / WAVES;          // LDS-DMA instructions per wave per chunk
+    constexpr int XN = RT * KS;              // x-fragment loads per wave per tile
+    constexpr int NST = RT * NT / 2;         // 16-byte stores per wave per tile
+    static_assert(XN == NST, "one extra-count class");
+    constexpr int ROWS = WAVES * 16 * RT;
+    constexpr int NS = 4;                    // ring slots: 2 chunks in flight, the chunk in phase A,
+                                             // the previous chunk in phase B
+    constexpr unsigned OOB = 0x80000000u;
+    constexpr int PAR = (FFN_MAX_F + 3 * D) * 4;
+    __shared__ __attribute__((aligned(16))) char lds[PAR + NS * G::CHUNK];
+    float* const pb1 = reinterpret_cast<float*>(lds);
+    float* const pb2 = pb1 + FFN_MAX_F;
+    float* const pg = pb2 + D;
+    float* const pbe = pg + D;
+    char* const ring = lds + PAR;
+
+    const int P = gridDim.x, bx = blockIdx.x;
+    const int cnt = bx < ntiles ? (ntiles - 1 - bx) / P + 1 : 0;
+    if (cnt == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, c16 = lane & 15;
+    const int nch = p.F / 32, pfi = nch / 2;
+    const bool ln = p.ln_g != nullptr;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, p.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, (short)0, p.w_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(p.Y, (short)0, p.y_bytes, 0x00020000);
+
+    for (int i = threadIdx.x; i < p.F; i += WAVES * 64) pb1[i] = p.b1[i];
+    for (int i = threadIdx.x; i < D; i += WAVES * 64) {
+        pb2[i] = p.b2[i];
+        pg[i] = ln ? p.ln_g[i] : 1.f;
+        pbe[i] = ln ? p.ln_b[i] : 0.f;
+    }
+
+    auto load_x = [&](int tile, u32x4 (&dst)[RT][KS]) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const int r = tile * ROWS + wave * 16 * RT + 16 * rt + c16;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const unsigned off = r < p.M ? ((unsigned)r * (unsigned)p.ldx + (unsigned)(32 * ks + 8 * g)) * 2u : OOB;
+                dst[rt][ks] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+            }
+        }
+    };
+    // global chunk q of this workgroup -> ring slot q % NS; wave w moves fragments w, w+WAVES, ..
+    auto dma_chunk = [&](int q) {
+        const int c = q % nch;
+        char* dst = ring + (q % NS) * G::CHUNK;
+        const unsigned src = (unsigned)c * (unsigned)G::CHUNK + (unsigned)lane * 16u;
+#pragma unroll
+        for (int k = 0; k < FRW; ++k) {
+            const int f = k * WAVES + wave;
+            dma16(rw, dst + f * 1024, src + (unsigned)f * 1024u);
+        }
+    };
+    // VMEM ops a wave issues in chunk iteration q AFTER that iteration's DMA (x prefetch,
+    // epilogue stores): they are younger than the DMA of chunks q+2 and q+1
+    auto extra = [&](int q) {
+        if (q < 0) return 0;
+        const int c = q % nch, ti = q / nch;
+        return ((c == pfi && ti + 1 < cnt) ? XN : 0) + (c == nch - 1 ? NST : 0);
+    };
+
+    u32x4 xr[RT][KS], xn[RT][KS];
+    load_x(bx, xr);
+    __syncthreads();   // parameters in LDS (drains the x loads too: nothing else in flight yet)
+    const int total = cnt * nch;
+    dma_chunk(0);
+    if (total > 1) dma_chunk(1);
+
+    f32x4 acc[RT][NT];
+    constexpr int PB = 4;                      // W2 fragments read ahead of phase B
+    auto fragA = [&](const char* slot, int ks, int h) {
+        return *reinterpret_cast<const u32x4*>(slot + lane * 16 + (h * KS + ks) * 1024);
+    };
+    auto fragB = [&](const char* slot, int nt) {
+        return *reinterpret_cast<const u32x4*>(slot + lane * 16 + (2 * KS + nt) * 1024);
+    };
+    // ReLU + round one 32-bit word (2 hidden units) of row tile w/4's phase-B operand: lane
+    // holds H[row l&15][4g+i] (h0) and [16+4g+i] (h1) = the 8 K slots of the operand in the
+    // order kinet_ffn_pack permuted W2 to
+    auto hword = [&](const f32x4 (&q0)[RT], const f32x4 (&q1)[RT], int w) {
+        const int rt = w >> 2, i = w & 3;
+        const f32x4& src = i < 2 ? q0[rt] : q1[rt];
+        const int e = 2 * (i & 1);
+        return pack2<T>(fmaxf(src[e], 0.f), fmaxf(src[e + 1], 0.f));
+    };
+    // phase B of one chunk: out[row l&15][sigma(nt, 4g+i)] += W2c . H^T; fw[0..PB) preloaded
+    auto phase_b = [&](const char* slot, u32x4 (&fw)[PB + 1], const u32x4 (&hb)[RT]) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            if (nt + PB < NT) fw[(nt + PB) % (PB + 1)] = fragB(slot, nt + PB);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) Mma<T>::run(acc[rt][nt], fw[nt % (PB + 1)], hb[rt]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    for (int ti = 0; ti < cnt; ++ti) {
+    // consume the x fragments HERE (hipcc places the wait for their loads before this
+    // statement, once per tile) so no vmcnt wait of the compiler's lands inside the chunk
+    // loop, where it would retire the ring's DMA early
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(xr[rt][ks]));
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[rt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // Software pipeline over the hidden chunks: iteration c runs phase A of chunk c with the
+    // ReLU/convert of chunk c-1 spread over its steps (VALU beside MFMA), then phase B of
+    // chunk c-1; the tile's last chunk gets its phase B after the loop.  Operand fragments are
+    // read from the ring two steps ahead and the steps are fenced with sched_barrier: with one
+    // wave per SIMD nothing else hides LDS latency, and hipcc otherwise sinks every ds_read
+    // next to its MFMA.
+    f32x4 hp0[RT], hp1[RT];
+    const char* wprev = ring;
+    for (int c = 0; c < nch; ++c) {
+        const int q = ti * nch + c;
+        // retire chunk q: still allowed in flight = everything issued after its DMA
+        if (q + 1 < total) {
+            const int e = extra(q - 2) + extra(q - 1);
+            if (p.dbg & 1) ffn_wait_vmcnt<0>();
+            else if (e == 0) ffn_wait_vmcnt<FRW>();
+            else ffn_wait_vmcnt<FRW + XN>();   // XN == NST; e == 2 XN only waits more
+        } else {
+            ffn_wait_vmcnt<0>();
+        }
+        ffn_lds_barrier();     // chunk q visible to all; slot (q+2)%NS free (chunk q-2 done)
+        if (q + 2 < total && !(p.dbg & 1)) dma_chunk(q + 2);
+        if (c == pfi && ti + 1 < cnt) load_x(bx + (ti + 1) * P, xn);
+        const char* wb = ring + (q % NS) * G::CHUNK;
+        const bool pipe = c > 0;
+        f32x4 h0[RT], h1[RT];
+        {
+            const f32x4 bb0 = *reinterpret_cast<const f32x4*>(pb1 + c * 32 + 4 * g);
+            const f32x4 bb1 = *reinterpret_cast<const f32x4*>(pb1 + c * 32 + 16 + 4 * g);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {   // b1 folded into the accumulator init
+                h0[rt] = bb0;
+                h1[rt] = bb1;
+            }
+        }
+        u32x4 fa[3][2], fw[PB + 1], hb[RT];
+        fa[0][0] = fragA(wb, 0, 0); fa[0][1] = fragA(wb, 0, 1);
+        fa[1][0] = fragA(wb, 1, 0); fa[1][1] = fragA(wb, 1, 1);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            if (ks + 2 < KS) {
+                fa[(ks + 2) % 3][0] = fragA(wb, ks + 2, 0);
+                fa[(ks + 2) % 3][1] = fragA(wb, ks + 2, 1);
+            } else if (pipe) {
+#pragma unroll
+                for (int j = 0; j < PB / 2; ++j) {
+                    const int nt = (ks + 2 - KS) * (PB / 2) + j;
+                    fw[nt] = fragB(wprev, nt);
+                }
+            }
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                Mma<T>::run(h0[rt], fa[ks % 3][0], xr[rt][ks]);
+                Mma<T>::run(h1[rt], fa[ks % 3][1], xr[rt][ks]);
+            }
+            if (pipe && ks < 4 * RT) hb[ks >> 2][ks & 3] = hword(hp0, hp1, ks);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (pipe) {
+#pragma unroll
+            for (int w = KS; w < 4 * RT; ++w) hb[w >> 2][w & 3] = hword(hp0, hp1, w);
+            phase_b(wprev, fw, hb);
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            hp0[rt] = h0[rt];
+            hp1[rt] = h1[rt];
+        }
+        wprev = wb;
+    }
+    {   // phase B of the tile's last chunk (its slot is still held: the next DMA into it is
+        // issued only after the next iteration's barrier)
+        u32x4 fw[PB + 1], hb[RT];
+#pragma unroll
+        for (int j = 0; j < PB; ++j) fw[j] = fragB(wprev, j);
+#pragma unroll
+        for (int w = 0; w < 4 * RT; ++w) hb[w >> 2][w & 3] = hword(hp0, hp1, w);
+        phase_b(wprev, fw, hb);
+    }
+
+        // ---- tile epilogue, registers only: + b2 + residual x (= xr), LayerNorm, store ----
+        const int tile = bx + ti * P;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const int r = tile * ROWS + wave * 16 * RT + 16 * rt + c16;
+            float s = 0.f;
+#pragma unroll
+            for (int kp = 0; kp < KS; ++kp) {
+                float x8[8];
+                unpack4<T>(u32x2{xr[rt][kp][0], xr[rt][kp][1]}, x8);
+                unpack4<T>(u32x2{xr[rt][kp][2], xr[rt][kp][3]}, x8 + 4);
+                const f32x4 b2a = *reinterpret_cast<const f32x4*>(pb2 + 32 * kp + 8 * g);
+                const f32x4 b2b = *reinterpret_cast<const f32x4*>(pb2 + 32 * kp + 8 * g + 4);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float v0 = acc[rt][2 * kp][i] + b2a[i] + x8[i];
+                    const float v1 = acc[rt][2 * kp + 1][i] + b2b[i] + x8[4 + i];
+                    acc[rt][2 * kp][i] = v0;
+                    acc[rt][2 * kp + 1][i] = v1;
+                    s += v0 + v1;
+                }
+            }
+            float mean = 0.f, rstd = 1.f;
+            if (ln) {
+                s += __shfl_xor(s, 16);
+                s += __shfl_xor(s, 32);
+                mean = s * (1.f / (float)D);
+                float qv = 0.f;
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float d = acc[rt][nt][i] - mean;
+                        qv += d * d;
+                    }
+                qv += __shfl_xor(qv, 16);
+                qv += __shfl_xor(qv, 32);
+                rstd = rsqrtf(qv * (1.f / (float)D) + p.eps);
+            }
+#pragma unroll
+            for (int kp = 0; kp < KS; ++kp) {
+                const int n0 = 32 * kp + 8 * g;
+                float o[8];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    o[i] = acc[rt][2 * kp][i];
+                    o[4 + i] = acc[rt][2 * kp + 1][i];
+                }
+                if (ln) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[e] = (o[e] - mean) * rstd * pg[n0 + e] + pbe[n0 + e];
+                }
+                u32x4 w;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) w[e] = pack2<T>(o[2 * e], o[2 * e + 1]);
+                // unconditional (OOB rows dropped by the range check): the store count per
+                // tile is fixed, which the counted vmcnt above relies on
+                const unsigned off = r < p.M ? ((unsigned)r * (unsigned)p.ldy + (unsigned)n0) * 2u : OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), ry, off, 0, 0);
+            }
+        }
+        if (ti + 1 < cnt) {
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) xr[rt][ks] = xn[rt][ks];
+        }
+    }
+}
+
+// packed[c][f][lane][j] (see include/kinet_ffn.h): f < 2KS -> W1 fragment (h-tile f / KS,
+// k-step f % KS); else W2 fragment of output tile f - 2KS with the hidden index permuted to
+// the phase-A accumulator order.
+template <typename T>
+__global__ void ffn_pack_kernel(const T* __restrict__ W1, const T* __restrict__ W2, T* __restrict__ out, int D,
+                                int F) {
+    const int KS = D / 32, NT = D / 16, FR = 2 * KS + NT;
+    const long total = 2L * D * F;
+    for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+        const long per_chunk = (long)FR * 512;
+        const int c = (int)(idx / per_chunk);
+        const int rem = (int)(idx - (long)c * per_chunk);
+        const int f = rem >> 9, e = rem & 511;
+        const int lane = e >> 3, j = e & 7, g = lane >> 4, c16 = lane & 15;
+        T v;
+        if (f < 2 * KS) {
+            const int ht = f / KS, ks = f - ht * KS;
+            v = W1[(long)(32 * c + 16 * ht + c16) * D + 32 * ks + 8 * g + j];
+        } else {
+            const int nt = f - 2 * KS;
+            const int h = 32 * c + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
+            v = W2[(long)ffn_sigma(nt, c16) * F + h];
+        }
+        out[idx] = v;
+    }
+}
+
+template <typename T, int D>
+int launch_ffn(const FfnArgs& a, hipStream_t s) {
+    // persistent: one workgroup per CU walks row tiles.  Many rows: 4 waves x 32 rows (128
+    // rows share each weight byte; the 2 x D/16 output tiles + 2 x D/32 x-fragments (+ the
+    // next tile's prefetch) need > 256 VGPRs, so one wave per SIMD);  few rows (decoder
+    // queries): 4 waves x 16 rows, so the rows spread over more CUs
+    if (a.M >= 16384) {
+        const int nt = (a.M + 127) / 128;
+        if constexpr (FfnGeo<D>::FR % 8 == 0) {
+            // 8 waves x 16 rows: two waves per SIMD hide each other's LDS / VALU latency
+            hipLaunchKernelGGL((ffn_fused_kernel<T, D, 1, 8>), dim3(nt < 256 ? nt : 256), dim3(512), 0, s, a, nt);
+        } else {
+            hipLaunchKernelGGL((ffn_fused_kernel<T, D, 2, 4>), dim3(nt < 256 ? nt : 256), dim3(256), 0, s, a, nt);
+        }
+    } else {
+        const int nt = (a.M + 63) / 64;
+        hipLaunchKernelGGL((ffn_fused_kernel<T, D, 1, 4>), dim3(nt < 256 ? nt : 256), dim3(256), 0, s, a, nt);
+    }
+    return KINET_OK;
+}
+
+bool al16(const void* q) { return (((uintptr_t)q) & 15u) == 0; }
+
+}  // namespace
+}  // namespace kinet
+
+using namespace kinet;
+
+extern "C" int kinet_ffn_set_debug(int flags) {
+    const int old = ffn_debug;
+    ffn_debug = flags;
+    return old;
+}
+
+extern "C" int kinet_ffn_pack(const void* W1, const void* W2, void* packed, int D, int F, int dtype,
+                              kinet_stream_t stream) {
+    KINET_CHECK_ARG(D > 0 && D % 32 == 0 && F > 0 && F % 32 == 0, "ffn_pack: need D %% 32 == 0 and F %% 32 == 0 (D=%d F=%d)", D, F);
+    KINET_CHECK_ARG(dtype == KINET_BF16 || dtype == KINET_F16, "ffn_pack: dtype must be bf16 or f16");
+    const long total = 2L * D * F;
+    const int grid = (int)((total + 255) / 256 < kMaxGridStride ? (total + 255) / 256 : kMaxGridStride);
+    if (dtype == KINET_BF16)
+        hipLaunchKernelGGL(ffn_pack_kernel<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)W1,
+                           (const bf16_t*)W2, (bf16_t*)packed, D, F);
+    else
+        hipLaunchKernelGGL(ffn_pack_kernel<f16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const f16_t*)W1,
+                           (const f16_t*)W2, (f16_t*)packed, D, F);
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_ffn_fused(const void* X, int ldx, const void* packed, const float* b1, const float* b2,
+                               const float* ln_gamma, const float* ln_beta, float ln_eps, void* Y, int ldy, int M,
+                               int D, int F, int dtype, kinet_stream_t stream) {
+    KINET_CHECK_ARG(D == 256 || D == 288, "ffn_fused: D must be 256 or 288 (got %d)", D);
+    KINET_CHECK_ARG(F > 0 && F % 32 == 0 && F <= FFN_MAX_F, "ffn_fused: F must be a multiple of 32 in [32, %d] (got %d)", FFN_MAX_F, F);
+    KINET_CHECK_ARG(M >= 0 && ldx >= D && ldy >= D && ldx % 8 == 0 && ldy % 8 == 0, "ffn_fused: bad M / ldx / ldy");
+    KINET_CHECK_ARG(dtype == KINET_BF16 || dtype == KINET_F16, "ffn_fused: dtype must be bf16 or f16");
+    KINET_CHECK_ARG(b1 != nullptr && b2 != nullptr, "ffn_fused: b1 and b2 are required");
+    KINET_CHECK_ARG((ln_gamma == nullptr) == (ln_beta == nullptr), "ffn_fused: LayerNorm needs both gamma and beta");
+    KINET_CHECK_ARG(al16(X) && al16(Y) && al16(packed) && al16(b1) && al16(b2) &&
+                    (ln_gamma == nullptr || (al16(ln_gamma) && al16(ln_beta))),
+                    "ffn_fused: X, Y, packed weights, biases and LayerNorm params must be 16-byte aligned");
+    if (M == 0) return KINET_OK;
+    const long long xb = ((long long)(M - 1) * ldx + D) * 2;
+    KINET_CHECK_ARG(xb < (1LL << 31), "ffn_fused: X larger than 2 GiB (split the call)");
+    FfnArgs a{};
+    a.X = X; a.W = packed; a.b1 = b1; a.b2 = b2; a.ln_g = ln_gamma; a.ln_b = ln_beta; a.Y = Y; a.eps = ln_eps;
+    a.ldx = ldx; a.ldy = ldy; a.M = M; a.F = F;
+    a.x_bytes = (int)xb;
+    a.w_bytes = (int)(2LL * D * F * 2);
+    const long long yb = ((long long)(M - 1) * ldy + D) * 2;
+    KINET_CHECK_ARG(yb < (1LL << 31), "ffn_fused: Y larger than 2 GiB (split the call)");
+    a.y_bytes = (int)yb;
+    a.dbg = ffn_debug;
+    hipStream_t s = (hipStream_t)stream;
+    int rc;
+    if (dtype == KINET_BF16) rc = D == 256 ? launch_ffn<bf16_t, 256>(a, s) : launch_ffn<bf16_t, 288>(a, s);
+    else rc = D == 256 ? launch_ffn<f16_t, 256>(a, s) : launch_ffn<f16_t, 288>(a, s);
+    if (rc) return rc;
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}

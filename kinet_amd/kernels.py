@@ -160,6 +160,47 @@ def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_d
     return out.view(*lead, Nout) if out.is_contiguous() else out
 
 
+def ffn_supported(x, linear1, linear2):
+    """The fused FFN kernel covers the 16-bit compute modes at d_model 256 / 288."""
+    D = x.shape[-1]
+    F_ = linear1.weight.shape[0]
+    return (x.dtype in (torch.bfloat16, torch.float16) and D in (256, 288) and F_ % 32 == 0
+            and linear1.bias is not None and linear2.bias is not None)
+
+
+def ffn_pack(w1, w2, dtype):
+    """kinet_ffn_pack of (W1 (F, D), W2 (D, F)), cached per parameter version."""
+    def make(a, b):
+        F_, D = a.shape
+        a16 = a.detach().to(dtype).contiguous()
+        b16 = b.detach().to(dtype).contiguous()
+        out = torch.empty(2 * D * F_, dtype=dtype, device=a.device)
+        N.call('kinet_ffn_pack', N.ptr(a16), N.ptr(b16), N.ptr(out), D, F_, N.dtype_code(dtype), N.stream(a.device))
+        return out
+    return cached_multi([w1, w2], ('ffn_pack', dtype), make)
+
+
+def ffn_fused(x, linear1, linear2, norm=None):
+    """y = norm(x + linear2(relu(linear1(x)))) in one launch (deformable_transformer.py:284-288,
+    :361-365); the (M, F) hidden tensor stays on chip.  x (..., D) bf16/f16."""
+    N.require_gpu(x)
+    D = x.shape[-1]
+    F_ = linear1.weight.shape[0]
+    x2 = x.reshape(-1, D)
+    if x2.stride(-1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    M = x2.shape[0]
+    wp = ffn_pack(linear1.weight, linear2.weight, x.dtype)
+    out = torch.empty((M, D), dtype=x.dtype, device=x.device)
+    g, b, eps = (f32(norm.weight), f32(norm.bias), float(norm.eps)) if norm is not None else (None, None, 0.0)
+    e = x.element_size()
+    work = {'family': 'gemm', 'flops': 4.0 * M * D * F_, 'shape': ('ffn', M, D, F_),
+            'bytes': (2 * M * D + 2 * D * F_) * e}
+    N.call('kinet_ffn_fused', N.ptr(x2), x2.stride(0), N.ptr(wp), N.ptr(f32(linear1.bias)), N.ptr(f32(linear2.bias)),
+           N.ptr(g), N.ptr(b), eps, N.ptr(out), D, M, D, F_, N.dtype_code(x.dtype), N.stream(x.device), work=work)
+    return out.view(*x.shape[:-1], D)
+
+
 def value_proj_headmajor(x, weight, bias, head_dim, row_mask=None, out_dtype=None):
     """MSDA value projection written head-major: x (B, S, K) -> (Nout/head_dim, B, S, head_dim),
     padding rows zeroed (ms_deform_attn.py:64-67).  out_dtype: x.dtype, or float16 from bf16

@@ -100,6 +100,8 @@ class DeformableTransformerEncoderLayer(nn.Module):
         samp = a.sample(src, reference_points, value, spatial_shapes, query_add=pos)   # (src+pos) @ W
         n1, n2 = self.norm1, self.norm2
         src = K.linear(samp, a.output_proj.weight, a.output_proj.bias, residual=src, ln=(n1.weight, n1.bias, n1.eps))
+        if K.ffn_supported(src, self.linear1, self.linear2):
+            return K.ffn_fused(src, self.linear1, self.linear2, n2)
         h = K.linear(src, self.linear1.weight, self.linear1.bias, relu=True)
         return K.linear(h, self.linear2.weight, self.linear2.bias, residual=src, ln=(n2.weight, n2.bias, n2.eps))
 
@@ -193,6 +195,8 @@ class DeformableTransformerDecoderLayer(nn.Module):
             value = ca.project_value(src, src_padding_mask)
         samp = ca.sample(tgt, reference_points, value, src_spatial_shapes, query_attn_mask, query_add=query_pos)
         tgt = K.linear(samp, ca.output_proj.weight, ca.output_proj.bias, residual=tgt, ln=(n1.weight, n1.bias, n1.eps))
+        if K.ffn_supported(tgt, self.linear1, self.linear2):
+            return K.ffn_fused(tgt, self.linear1, self.linear2, n3)
         h = K.linear(tgt, self.linear1.weight, self.linear1.bias, relu=True)
         return K.linear(h, self.linear2.weight, self.linear2.bias, residual=tgt, ln=(n3.weight, n3.bias, n3.eps))
 

@@ -363,3 +363,41 @@ def test_splitk_conv_vs_fp32(K, dtype):
     err = (y.permute(0, 3, 1, 2).float().cpu() - ref).abs()
     tol = (1e-4 * ref.abs() + 1e-4) if dtype == torch.float32 else (1e-2 * ref.abs() + 2e-2)
     assert (err <= tol).all(), err.max().item()
+
+
+@pytest.mark.parametrize('M,D', [(1, 256), (200, 256), (2400, 256), (20000, 256), (777, 288), (17000, 288)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_ffn_fused_vs_fp32(K, M, D, dtype):
+    """Fused FFN sub-layer (kinet_ffn_fused) vs fp32 LN(x + W2 relu(W1 x + b1) + b2) on the
+    16-bit inputs/weights, hidden rounded to the 16-bit type like the unfused path stores it."""
+    Fh = 1024
+    g = torch.Generator().manual_seed(M + D)
+    lin1, lin2, norm = torch.nn.Linear(D, Fh), torch.nn.Linear(Fh, D), torch.nn.LayerNorm(D)
+    with torch.no_grad():
+        for p in (norm.weight, norm.bias):
+            p.copy_(torch.randn(p.shape, generator=g) * 0.5 + (1.0 if p is norm.weight else 0.0))
+    x = torch.randn(M, D, generator=g).to(dtype)
+    w1, w2 = lin1.weight.detach().to(dtype).float(), lin2.weight.detach().to(dtype).float()
+    h = F.relu(F.linear(x.float(), w1, lin1.bias.detach())).to(dtype).float()
+    ref = F.layer_norm(x.float() + F.linear(h, w2, lin2.bias.detach()), (D,), norm.weight.detach(), norm.bias.detach())
+    lin1, lin2, norm = lin1.cuda(), lin2.cuda(), norm.cuda()
+    y = K.ffn_fused(x.cuda(), lin1, lin2, norm)
+    torch.cuda.synchronize()
+    assert y.shape == (M, D) and y.dtype == dtype
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err < (6e-2 if dtype == torch.bfloat16 else 8e-3), err
+    # the unfused kinet path (two GEMMs, LN in the second epilogue) agrees to output rounding
+    hk = K.linear(x.cuda(), lin1.weight, lin1.bias, relu=True)
+    yk = K.linear(hk, lin2.weight, lin2.bias, residual=x.cuda(), ln=(norm.weight, norm.bias, norm.eps))
+    assert (y.float() - yk.float()).abs().max().item() < (6e-2 if dtype == torch.bfloat16 else 8e-3)
+
+
+def test_ffn_fused_no_norm_and_errors(K):
+    lin1, lin2 = torch.nn.Linear(256, 1024).cuda(), torch.nn.Linear(1024, 256).cuda()
+    x = torch.randn(300, 256, device='cuda').bfloat16()
+    y = K.ffn_fused(x, lin1, lin2, None)
+    ref = x.float() + lin2(torch.relu(lin1(x.float())).bfloat16().float())
+    assert (y.float() - ref).abs().max().item() < 5e-2
+    lin1b, lin2b = torch.nn.Linear(128, 1024).cuda(), torch.nn.Linear(1024, 128).cuda()
+    with pytest.raises(RuntimeError, match='D must be 256 or 288'):
+        K.ffn_fused(torch.randn(10, 128, device='cuda').bfloat16(), lin1b, lin2b, None)

@@ -51,6 +51,28 @@ def gemm():
         print(f'B{B} {H}x{W} {Cin}->{Cout} k{k}s{s}: {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TF/s')
 
 
+def ffn():
+    from kinet_amd import kernels as K
+    dt = torch.bfloat16
+    print('--- FFN sub-layer: fused kernel vs two GEMMs (bf16, d=256, F=1024, LN) ---')
+    for M in [2400, 88892, 177784]:
+        lin1, lin2, norm = torch.nn.Linear(256, 1024).cuda(), torch.nn.Linear(1024, 256).cuda(), torch.nn.LayerNorm(256).cuda()
+        x = torch.randn(M, 256, device='cuda', dtype=dt)
+        fused = timeit(lambda: K.ffn_fused(x, lin1, lin2, norm))
+        two = timeit(lambda: K.linear(K.linear(x, lin1.weight, lin1.bias, relu=True), lin2.weight, lin2.bias,
+                                      residual=x, ln=(norm.weight, norm.bias, norm.eps)))
+        fl = 4 * M * 256 * 1024
+        if M == 177784:
+            from kinet_amd import _native
+            for dbg in (1,):
+                _native.lib().kinet_ffn_set_debug(dbg)
+                t = timeit(lambda: K.ffn_fused(x, lin1, lin2, norm))
+                print(f'   [debug {dbg}: {"no weight DMA" if dbg == 1 else "no MFMA" if dbg == 2 else "neither"}] {t * 1e3:7.1f} us')
+            _native.lib().kinet_ffn_set_debug(0)
+        print(f'M={M:7d}: fused {fused * 1e3:7.1f} us {fl / fused / 1e9:6.0f} TF/s | two GEMMs {two * 1e3:7.1f} us '
+              f'{fl / two / 1e9:6.0f} TF/s')
+
+
 def model():
     from kinet_amd import _native
     from kinet_amd.models import build_model, nested_tensor_from_tensor_list
@@ -97,5 +119,7 @@ if __name__ == '__main__':
         print('[bench_kernels] GEMM flags = 2 (big-tile kernel allowed)')
     if 'gemm' in which:
         gemm()
+    if 'ffn' in which:
+        ffn()
     if 'model' in which:
         model()
