@@ -40,7 +40,7 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--batch', type=int, default=4, help='frames per GPU per step')
+    ap.add_argument('--batch', type=int, default=8, help='frames per GPU per step')
     ap.add_argument('--height', type=int, default=800)
     ap.add_argument('--width', type=int, default=1333)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'f32'])

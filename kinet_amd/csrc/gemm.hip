@@ -39,6 +39,8 @@ namespace {
 // (measured slower than gemm_kernel on every detector shape, DESIGN.md, so off by default);
 // bit 2 = never use the resident-weight kernel (gemm_rw.hip)
 int kinet_gemm_flags = 0;
+// diagnostic tile override for gemm_kernel (kinet_gemm_force_tile; 0 = heuristic)
+int force_bm = 0, force_bn = 0;
 
 
 template <int BM, int BN>
@@ -596,16 +598,21 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         KINET_CHECK_ARG(a.N <= 320, "gemm: fused LayerNorm needs N <= 320 (got %d)", a.N);
         bm = a.M <= 8192 ? 32 : 64;     // small M (decoder queries): more workgroups
         bn = a.N <= 256 ? 256 : 320;
-    } else if (a.M <= 4096) {
-        bm = 32;
+    } else if (a.kchunk && a.M <= 4096) {
+        bm = bn = 64;                   // split-K slices of a small-M, long-K problem
+    } else if (a.M <= 4096 && a.N <= 1024) {
+        bm = 32;                        // decoder-sized GEMMs: more workgroups
         bn = 64;
     } else {
+        // 64x128 (128x64 for N <= 64): fastest main-loop tile on every 3x3 / K >= 512 conv and
+        // GEMM shape of the detector at batch 8 (tools/sweep_conv.py) -- more tiles per CU-round
+        // than 128x128 and no worse per flop
         bn = a.N <= 64 ? 64 : 128;
-        const long tiles128 = (long)((a.M + 127) / 128) * ((a.N + bn - 1) / bn);
-        bm = tiles128 < 512 ? 64 : 128;
-        // single-K-step problems (1x1 convs with Cin <= 64) are store-bound: the smaller
-        // tile's LDS footprint lets 3 workgroups share a CU and overlap their epilogues
-        if (CONV && a.K <= 128 && bm == 128 && bn == 128) bm = 64;
+        bm = a.N <= 64 ? 128 : 64;
+    }
+    if (force_bm && !ln) {
+        bm = force_bm;
+        bn = force_bn;
     }
     const int nMt = (a.M + bm - 1) / bm, nNt = (a.N + bn - 1) / bn;
     const long nblk = (long)nMt * nNt;
@@ -828,6 +835,14 @@ extern "C" int kinet_gemm_splitk(const void* A, const void* B, void* C, int M, i
     a.a_bytes = (int)ab;
     a.b_bytes = (int)bb;
     return run_splitk<false>(a, in_dtype, out_dtype, workspace, ksplit, (hipStream_t)stream);
+}
+
+extern "C" int kinet_gemm_force_tile(int bm, int bn) {
+    KINET_CHECK_ARG((bm == 0 && bn == 0) || ((bm == 32 && bn == 64) || ((bm == 64 || bm == 128) && (bn == 64 || bn == 128))),
+                    "gemm_force_tile: unsupported tile %dx%d", bm, bn);
+    force_bm = bm;
+    force_bn = bn;
+    return KINET_OK;
 }
 
 extern "C" int kinet_gemm_set_flags(int flags) {

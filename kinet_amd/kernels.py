@@ -84,22 +84,28 @@ def f32(t):
 
 
 # ----------------------------------------------------------------------------------- GEMM
+def _tile(M, N, ln=False, split=False):
+    """The gemm_kernel tile launch() in csrc/gemm.hip picks (bm, bn)."""
+    if ln:
+        return (32 if M <= 8192 else 64), (256 if N <= 256 else 320)
+    if split and M <= 4096:
+        return 64, 64
+    if M <= 4096 and N <= 1024:
+        return 32, 64
+    return (128, 64) if N <= 64 else (64, 128)
+
+
 def ksplit_for(M, N, K, ln=False):
-    """Split-K factor for long-K problems with too few output tiles to fill the 256 CUs
-    (the tile estimate mirrors launch() in csrc/gemm.hip); 1 = no split."""
+    """Split-K factor for long-K problems with too few output tiles to fill the CUs twice
+    over (the tile choice mirrors launch() in csrc/gemm.hip); 1 = no split."""
     if K < 1024 or M == 0:
         return 1
-    if ln:
-        bm, bn = (32 if M <= 8192 else 64), (256 if N <= 256 else 320)
-    elif M <= 4096:
-        bm, bn = 32, 64
-    else:
-        bn = 64 if N <= 64 else 128
-        bm = 64 if ((M + 127) // 128) * ((N + bn - 1) // bn) < 512 else 128
-    tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
-    if tiles >= 256:
+    bm, bn = _tile(M, N, ln)
+    if ((M + bm - 1) // bm) * ((N + bn - 1) // bn) >= 512:
         return 1
-    ks = min(8, max(2, 768 // tiles), K // 256)
+    bm, bn = _tile(M, N, ln, split=True)
+    tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
+    ks = min(4, -(-768 // tiles), K // 256)
     return ks if ks >= 2 else 1
 
 
@@ -235,7 +241,7 @@ def pack_conv_weight(w, dtype, cin_pad=None):
     return cached(w, ('conv', dtype, cin_pad), make)
 
 
-def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, residual=None, out=None):
+def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, residual=None, out=None, ksplit=None):
     """x (B, H, W, Cin) NHWC contiguous; w_packed (Cout, KH, KW, Cin); returns (B, Ho, Wo, Cout)."""
     B, H, W, Cin = x.shape
     Cout, KH, KW, Cin2 = w_packed.shape
@@ -255,7 +261,7 @@ def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, res
             'bytes': (B * H * W * Cin + Cout * KH * KW * Cin + B * Ho * Wo * Cout * (2 if r is not None else 1)) * e}
     args = (N.ptr(x), N.ptr(w_packed), N.ptr(out), B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
             N.dtype_code(x.dtype), N.ptr(scale), N.ptr(bias), N.ptr(r), Cout if r is not None else 0, int(relu), ldy)
-    ks = ksplit_for(B * Ho * Wo, Cout, KH * KW * Cin)
+    ks = ksplit_for(B * Ho * Wo, Cout, KH * KW * Cin) if ksplit is None else ksplit
     if ks > 1:
         ws = torch.empty(ks * B * Ho * Wo * Cout, dtype=torch.float32, device=x.device)
         N.call('kinet_conv2d_splitk', *args, N.ptr(ws), ks, N.stream(x.device), work=work)
