@@ -37,7 +37,7 @@ namespace {
 
 // diagnostic kernel-selection flags (kinet_gemm_set_flags): bit 1 = allow gemm_big_kernel
 // (measured slower than gemm_kernel on every detector shape, DESIGN.md, so off by default);
-// bit 2 = never use the resident-weight kernel (gemm_rw.hip)
+// bit 2 = never use the resident-weight kernel (gemm_rw.hip); bit 4 = LDS-DMA gemm_dma_kernel
 int kinet_gemm_flags = 0;
 // diagnostic tile override for gemm_kernel (kinet_gemm_force_tile; 0 = heuristic)
 int force_bm = 0, force_bn = 0;
@@ -269,7 +269,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
             const int oh = rem / p.Wout, ow = rem - (rem / p.Wout) * p.Wout;
             xih[i] = oh * p.stride - p.pad;
             xiw[i] = ow * p.stride - p.pad;
-            xbase[i] = (unsigned)img * (unsigned)(p.Hin * p.Win * p.Cin);
+            // element offset of the receptive field's (0, 0) tap (may lie outside the image:
+            // only ever used behind the bounds test)
+            xbase[i] = (unsigned)img * (unsigned)(p.Hin * p.Win * p.Cin) +
+                       (unsigned)((xih[i] * p.Win + xiw[i]) * p.Cin);
         } else {
             xih[i] = xiw[i] = 0;
             xbase[i] = (unsigned)m * (unsigned)p.lda;
@@ -288,34 +291,47 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
     // k+1 (issued one step earlier) is written to LDS -- two steps of load latency covered
     u32x4 xs0[XR], ws0[WR], xs1[XR], ws1[WR];
 
+    // when Cin is a multiple of the K-step, one K-step lies inside one filter tap: the tap
+    // (kh, kw) is wave-uniform and computed on the scalar unit, not per lane
+    const bool tap_uniform = CONV && (p.Cin % BK) == 0;
+    // Offsets past the edges / padding taps get bit 31 set: past num_records, so the range
+    // check returns zeros.  Computed arithmetically (no select): hipcc otherwise branches
+    // around the offset math of each load (s_and_saveexec) to skip it for masked lanes.
     auto load_tile = [&](int k0, u32x4 (&xs)[XR], u32x4 (&ws)[WR]) {
         const int k = kbeg + k0 + sc * EPC;
-        const bool kok = k < K;
-        int kh = 0, kw = 0, cc = k;
+        const unsigned kbad = k < K ? 0u : OOB;
+        int kh = 0, kw = 0, dk = 0;
         if (CONV) {
-            const int tap = k / p.Cin;
-            cc = k - tap * p.Cin;
-            kh = tap / p.KW;
-            kw = tap - kh * p.KW;
+            if (tap_uniform) {
+                const int ks0 = __builtin_amdgcn_readfirstlane(kbeg + k0);
+                const int tap = ks0 / p.Cin;
+                kh = tap / p.KW;
+                kw = tap - kh * p.KW;
+                dk = __builtin_amdgcn_readfirstlane((kh * p.Win + kw) * p.Cin + ks0 - tap * p.Cin) + sc * EPC;
+            } else {
+                const int tap = k / p.Cin;
+                kh = tap / p.KW;
+                kw = tap - kh * p.KW;
+                dk = (kh * p.Win + kw) * p.Cin + k - tap * p.Cin;
+            }
         }
 #pragma unroll
         for (int i = 0; i < XR; ++i) {
-            bool ok = xok[i] && kok;
-            unsigned off;
+            unsigned off, bad = kbad | (xok[i] ? 0u : OOB);
             if (CONV) {
-                const int ih = xih[i] + kh, iw = xiw[i] + kw;
-                ok = ok && ih >= 0 && ih < p.Hin && iw >= 0 && iw < p.Win;
-                off = xbase[i] + (unsigned)((ih * p.Win + iw) * p.Cin + cc);
+                const bool in = (unsigned)(xih[i] + kh) < (unsigned)p.Hin && (unsigned)(xiw[i] + kw) < (unsigned)p.Win;
+                bad |= in ? 0u : OOB;
+                off = xbase[i] + (unsigned)dk;
             } else {
                 off = xbase[i] + (unsigned)k;
             }
-            const unsigned boff = ok ? off * (unsigned)sizeof(T) : OOB;
+            const unsigned boff = (off * (unsigned)sizeof(T)) | bad;
             xs[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, boff, 0, 0);
             if (!CONV && has_a2) xs[i] = Mma<T>::add(xs[i], __builtin_amdgcn_raw_buffer_load_b128(ra2, boff, 0, 0));
         }
 #pragma unroll
         for (int i = 0; i < WR; ++i) {
-            const unsigned boff = (wok[i] && kok) ? (wbase[i] + (unsigned)k) * (unsigned)sizeof(T) : OOB;
+            const unsigned boff = ((wbase[i] + (unsigned)k) * (unsigned)sizeof(T)) | kbad | (wok[i] ? 0u : OOB);
             ws[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, boff, 0, 0);
         }
     };
@@ -356,19 +372,23 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
     };
     // step kt: issue K-step kt+2 into the set that held kt (already in LDS), compute kt,
     // write kt+1 (loaded one step ago) into the other LDS buffer, one barrier
+    // the loads of K-steps past the end are issued too (range check -> zeros, no traffic):
+    // a conditional load makes hipcc's vmcnt count assume the short path and drain the
+    // younger prefetch before every LDS write
     auto step = [&](int kt, u32x4 (&xi)[XR], u32x4 (&wi)[WR], const u32x4 (&xn)[XR], const u32x4 (&wn)[WR]) {
-        if (kt + 2 < nk) load_tile((kt + 2) * BK, xi, wi);
+        load_tile((kt + 2) * BK, xi, wi);
         compute(kt & 1);
-        if (kt + 1 < nk) store_tile((kt + 1) & 1, xn, wn);
+        store_tile((kt + 1) & 1, xn, wn);
         __syncthreads();
     };
     load_tile(0, xs0, ws0);
-    if (nk > 1) load_tile(BK, xs1, ws1);
+    load_tile(BK, xs1, ws1);
     store_tile(0, xs0, ws0);
     __syncthreads();
+    // two K-steps per iteration, both unconditional (an odd last step multiplies zeros)
     for (int kt = 0; kt < nk; kt += 2) {
         step(kt, xs0, ws0, xs1, ws1);
-        if (kt + 1 < nk) step(kt + 1, xs1, ws1, xs0, ws0);
+        step(kt + 1, xs1, ws1, xs0, ws0);
     }
 
     // ---- epilogue: residual rows in flight, park the f32 tile in LDS, stream whole rows ----
@@ -386,6 +406,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
     __syncthreads();
     epilogue_rows<TO, BN, EPI_LD, 4, LN, BM>(p, ep, m0, n0, 0, wave, lane, rp);
 }
+
+#include "gemm_dma.h"   // gemm_dma_kernel: the same tiles staged by LDS-DMA through a 3-slot ring
 
 // Large-M GEMM / implicit conv: 512 threads (8 waves, WGM x WGN, each wave a (BM/WGM) x 64
 // output tile), BM x BN tile with BN in {128, 256}, BK = 64 (one 128-byte LDS row).
@@ -609,6 +631,8 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         // than 128x128 and no worse per flop
         bn = a.N <= 64 ? 64 : 128;
         bm = a.N <= 64 ? 128 : 64;
+        // big square-ish problems: the 128x128 tile's lower operand traffic per flop wins
+        if (a.N >= 512 && (long)((a.M + 127) / 128) * ((a.N + 127) / 128) >= 2048) bm = bn = 128;
     }
     if (force_bm && !ln) {
         bm = force_bm;
@@ -619,8 +643,17 @@ int launch(const GemmArgs& a, hipStream_t stream) {
     KINET_CHECK_ARG(nblk < (1L << 31), "gemm: too many tiles");
     const int nslice = a.kchunk ? (a.K + a.kchunk - 1) / a.kchunk : 1;
     dim3 grid((unsigned)nblk, (unsigned)nslice), block(256);
-#define L_(BM_, BN_, WM_, WN_, LN_) \
-    hipLaunchKernelGGL((gemm_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0, stream, a, nNt)
+    // LDS-DMA staging (opt-in, flag 16): measured 0-10 % slower than the register-staged
+    // kernel on the detector's conv / GEMM shapes at batch 8 (tools/sweep_conv.py), so the
+    // register path stays the default; A2 (load-time add) needs the register path anyway
+    const bool dma = a.A2 == nullptr && (kinet_gemm_flags & 16);
+#define L_(BM_, BN_, WM_, WN_, LN_)                                                                             \
+    do {                                                                                                        \
+        if (dma) hipLaunchKernelGGL((gemm_dma_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0,   \
+                                    stream, a, nNt);                                                            \
+        else hipLaunchKernelGGL((gemm_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0, stream, a, \
+                                nNt);                                                                           \
+    } while (0)
     if (ln) {
         if (bm == 32 && bn == 256) L_(32, 256, 1, 4, true);
         else if (bm == 32) L_(32, 320, 1, 4, true);

@@ -1,0 +1,198 @@
+// LDS-DMA staged variant of gemm.hip's gemm_kernel (included by gemm.hip after gemm_kernel,
+// inside its anonymous namespace; uses ResRows / epilogue_rows from there).
+//
+// rocprofv3 on the register-staged kernel (3x3 conv, batch 8): SQ_WAIT_INST_LDS 21 % of wave
+// cycles, MFMA busy 21 % -- the ds_write_b128 staging pass (13 cycles per wave-instruction)
+// costs more LDS time per K-step than the MFMAs take.  Here the DMA writes LDS directly:
+//  * one wave-instruction fills 8 consecutive 128-byte tile rows (1 KiB, lane-linear); the
+//    XOR swizzle that compute() reads with is applied on the SOURCE side (lane l of a row
+//    group loads logical chunk (l & 7) ^ (row & 7));
+//  * a 3-slot ring: K-step kt+2 is issued right after the barrier of step kt into the slot
+//    step kt-1 used; a counted `s_waitcnt vmcnt` (one step's DMA count) retires step kt while
+//    kt+1 stays in flight across the raw s_barrier; the loop holds no VGPR-destination load,
+//    so hipcc adds no vmcnt(0) of its own;
+//  * steps past K are issued too (range check -> zeros): no conditional DMA, exact counts.
+#pragma once
+
+template <int BM, int BN>
+struct DmaSmem {
+    static constexpr int STAGE = (BM + BN) * ROWB;
+    static constexpr int NS = 3;
+    static constexpr int EPI_LD = BN + 4;
+    static constexpr int EPI = BM * EPI_LD * 4;
+    static constexpr int BYTES = (NS * STAGE > EPI) ? NS * STAGE : EPI;
+};
+
+template <int N>
+__device__ __forceinline__ void gemm_wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void gemm_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <typename T, typename TO, int BM, int BN, int WGM, int WGN, bool CONV, bool LN>
+__global__ __launch_bounds__(256, 2) void gemm_dma_kernel(const GemmArgs p, const int nNt) {
+    static_assert(WGM * WGN == 4, "4 waves");
+    constexpr int EPC = Mma<T>::EPC;
+    constexpr int BK = ROWB / (int)sizeof(T);
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;   // wave tile
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int STAGE = DmaSmem<BM, BN>::STAGE;
+    constexpr int NS = DmaSmem<BM, BN>::NS;
+    constexpr int EPI_LD = DmaSmem<BM, BN>::EPI_LD;
+    constexpr int XS = BM / 32, WS = BN / 32;      // DMA wave-instructions per wave per K-step
+    constexpr int SLOTS = XS + WS;
+    static_assert(BM % 32 == 0 && BN % 32 == 0, "whole 8-row groups per wave");
+    __shared__ __attribute__((aligned(16))) char lds[DmaSmem<BM, BN>::BYTES];
+
+    int bid = blockIdx.x;
+    {
+        const int nblk = gridDim.x, q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    }
+    const int mt = bid / nNt, nt = bid - (bid / nNt) * nNt;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WGM, wn = wave / WGM;
+    const int M = p.M, N = p.N;
+    const int kbeg = p.kchunk ? (int)blockIdx.y * p.kchunk : 0;
+    const int K = p.kchunk ? min(p.K, kbeg + p.kchunk) : p.K;
+
+    constexpr unsigned OOB = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
+
+    // this lane's staging rows: A row-group wave + 4i (i < XS), B row-group wave + 4i (i < WS),
+    // row (lane >> 3) of the group, logical 16-byte chunk sch of the row
+    const int rsub = lane >> 3;
+    const int sch = (lane & 7) ^ rsub;            // (row & 7) == rsub: groups are 8-row aligned
+    unsigned xbase[XS];
+    int xih[XS], xiw[XS];
+    bool xok[XS];
+#pragma unroll
+    for (int i = 0; i < XS; ++i) {
+        const int m = m0 + (wave + 4 * i) * 8 + rsub;
+        xok[i] = m < M;
+        if (CONV) {
+            const int hw = p.Hout * p.Wout;
+            const int img = m / hw;
+            const int rem = m - img * hw;
+            const int oh = rem / p.Wout, ow = rem - (rem / p.Wout) * p.Wout;
+            xih[i] = oh * p.stride - p.pad;
+            xiw[i] = ow * p.stride - p.pad;
+            // element offset of the receptive field's (0, 0) tap (used only behind the bounds test)
+            xbase[i] = (unsigned)img * (unsigned)(p.Hin * p.Win * p.Cin) +
+                       (unsigned)((xih[i] * p.Win + xiw[i]) * p.Cin);
+        } else {
+            xih[i] = xiw[i] = 0;
+            xbase[i] = (unsigned)m * (unsigned)p.lda;
+        }
+    }
+    unsigned wbase[WS];
+    bool wok[WS];
+#pragma unroll
+    for (int i = 0; i < WS; ++i) {
+        const int n = n0 + (wave + 4 * i) * 8 + rsub;
+        wok[i] = n < N;
+        wbase[i] = (unsigned)n * (unsigned)p.ldb;
+    }
+    const bool tap_uniform = CONV && (p.Cin % BK) == 0;
+
+    // DMA of K-step kt into ring slot kt % NS (offsets with bit 31 set read zeros)
+    auto stage = [&](int kt) {
+        char* st = lds + (kt % NS) * STAGE;
+        const int k0 = kbeg + kt * BK;
+        const int k = k0 + sch * EPC;
+        const unsigned kbad = k < K ? 0u : OOB;
+        int kh = 0, kw = 0, dk = 0;
+        if (CONV) {
+            if (tap_uniform) {
+                const int ks0 = __builtin_amdgcn_readfirstlane(k0);
+                const int tap = ks0 / p.Cin;
+                kh = tap / p.KW;
+                kw = tap - kh * p.KW;
+                dk = __builtin_amdgcn_readfirstlane((kh * p.Win + kw) * p.Cin + ks0 - tap * p.Cin) + sch * EPC;
+            } else {
+                const int tap = k / p.Cin;
+                kh = tap / p.KW;
+                kw = tap - kh * p.KW;
+                dk = (kh * p.Win + kw) * p.Cin + k - tap * p.Cin;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < XS; ++i) {
+            unsigned off, bad = kbad | (xok[i] ? 0u : OOB);
+            if (CONV) {
+                const bool in = (unsigned)(xih[i] + kh) < (unsigned)p.Hin && (unsigned)(xiw[i] + kw) < (unsigned)p.Win;
+                bad |= in ? 0u : OOB;
+                off = xbase[i] + (unsigned)dk;
+            } else {
+                off = xbase[i] + (unsigned)k;
+            }
+            dma16(ra, st + (wave + 4 * i) * 8 * ROWB, (off * (unsigned)sizeof(T)) | bad);
+        }
+#pragma unroll
+        for (int i = 0; i < WS; ++i)
+            dma16(rb, st + (BM + (wave + 4 * i) * 8) * ROWB,
+                  ((wbase[i] + (unsigned)k) * (unsigned)sizeof(T)) | kbad | (wok[i] ? 0u : OOB));
+    };
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int slot) {
+        const char* xl = lds + slot * STAGE;
+        const char* wl = xl + BM * ROWB;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + (lane >> 4);
+            u32x4 bfr[TM], afr[TN];
+#pragma unroll
+            for (int t = 0; t < TM; ++t)
+                bfr[t] = *reinterpret_cast<const u32x4*>(xl + swz(wm * WTM + t * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int t = 0; t < TN; ++t)
+                afr[t] = *reinterpret_cast<const u32x4*>(wl + swz(wn * WTN + t * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int b = 0; b < TM; ++b) Mma<T>::run(acc[a][b], afr[a], bfr[b]);
+        }
+    };
+
+    const int nk = (K - kbeg + BK - 1) / BK;
+    stage(0);
+    stage(1);
+    for (int kt = 0; kt < nk; ++kt) {
+        gemm_wait_vmcnt<SLOTS>();      // this wave's step-kt DMA landed (kt+1 may fly)
+        gemm_lds_barrier();            // everyone's landed; everyone done with step kt-1's slot
+        stage(kt + 2);
+        compute(kt % NS);
+    }
+    gemm_wait_vmcnt<0>();              // the two zero-filled steps past the end
+    gemm_lds_barrier();
+
+    // ---- epilogue: residual rows in flight, park the f32 tile in LDS, stream whole rows ----
+    ResRows<TO, BN, 4, BM> rp;
+    rp.issue(p, m0, n0, 0, wave, lane);
+    float* ep = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) {
+            const int ml = wm * WTM + b * 16 + (lane & 15);
+            const int nl = wn * WTN + a * 16 + (lane >> 4) * 4;
+            *reinterpret_cast<f32x4*>(ep + ml * EPI_LD + nl) = acc[a][b];
+        }
+    __syncthreads();
+    epilogue_rows<TO, BN, EPI_LD, 4, LN, BM>(p, ep, m0, n0, 0, wave, lane, rp);
+}

@@ -92,6 +92,8 @@ def _tile(M, N, ln=False, split=False):
         return 64, 64
     if M <= 4096 and N <= 1024:
         return 32, 64
+    if N >= 512 and ((M + 127) // 128) * ((N + 127) // 128) >= 2048:
+        return 128, 128
     return (128, 64) if N <= 64 else (64, 128)
 
 

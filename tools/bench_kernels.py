@@ -79,7 +79,8 @@ def model():
     from kinet_amd.models.config import load_args
     m, _, _ = build_model(load_args('train_deformable'))
     m = m.cuda().eval().set_compute_dtype(torch.bfloat16)
-    frames = nested_tensor_from_tensor_list([torch.randn(3, 800, 1333, device='cuda') for _ in range(4)])
+    nb = int(os.environ.get('KINET_BENCH_BATCH', '8'))
+    frames = nested_tensor_from_tensor_list([torch.randn(3, 800, 1333, device='cuda') for _ in range(nb)])
     with torch.no_grad():
         for _ in range(3):
             m(frames)
@@ -97,7 +98,7 @@ def model():
         a[2] += work.get('flops', 0)
         a[3] += work.get('bytes', 0)
     tot = sum(v[1] for v in agg.values())
-    print(f'--- one forward, 4 frames: {tot:.3f} ms device ---')
+    print(f'--- one forward, {nb} frames: {tot:.3f} ms device ---')
     for (f, sh), (n, ms, fl, by) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         print(f'{f:8s} {str(sh):38s} n={n:3d} {ms:7.3f} ms {100 * ms / tot:5.1f}%  '
               f'{fl / ms / 1e9 if ms else 0:7.1f} TF/s  {by / ms / 1e6 if ms else 0:7.1f} GB/s')
