@@ -41,6 +41,8 @@ def parse():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--batch', type=int, default=8, help='frames per GPU per step')
+    ap.add_argument('--streams', type=int, default=2,
+                    help='batches in flight per GPU, each on its own HIP stream (serving-style pipelining)')
     ap.add_argument('--height', type=int, default=800)
     ap.add_argument('--width', type=int, default=1333)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'f32'])
@@ -147,22 +149,31 @@ def main():
     from kinet_amd.models import nested_tensor_from_tensor_list
     model = build(dev, dtype)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    frames = [torch.randn(3, a.height, a.width, generator=g, device=dev) for _ in range(a.batch)]
-    samples = nested_tensor_from_tensor_list(frames)
+    # one independent batch per in-flight slot (distinct requests, all resident in HBM)
+    nst = max(1, a.streams)
+    batches = [nested_tensor_from_tensor_list([torch.randn(3, a.height, a.width, generator=g, device=dev)
+                                               for _ in range(a.batch)]) for _ in range(nst)]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(nst)]
+    samples = batches[0]
 
-    def step():
+    def step(i=0):
         with torch.no_grad():
-            return model(samples)
+            if nst == 1:
+                return model(batches[0])
+            # step i runs batch i % nst on its own stream: the decoder / small-kernel phases of
+            # one batch overlap the backbone of the next (no host syncs anywhere in a forward)
+            with torch.cuda.stream(streams[i % nst]):
+                return model(batches[i % nst])
 
-    for _ in range(max(1, a.warmup)):
-        out = step()
+    for i in range(max(1, a.warmup)):
+        out = step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        out = step()
+    for i in range(a.steps):
+        out = step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -173,10 +184,12 @@ def main():
         elapsed = t.item()
     assert torch.isfinite(out[0]['pred_boxes']).all()
 
-    # roofline pass: HIP events around every launch of 3 more steps (same stream)
+    # roofline pass: HIP events around every launch of 3 more steps, one stream (the traced
+    # kernel durations must not overlap)
     _native.trace_begin()
     for _ in range(3):
-        step()
+        with torch.no_grad():
+            model(samples)
     trace = _native.trace_end()
     torch.cuda.synchronize()
     fam, msda = summarize_trace(trace, 3)
@@ -227,7 +240,8 @@ def main():
             'data': 'synthetic N(0,1) 3x%dx%d frames, random-init weights (reference init)' % (a.height, a.width),
             'config': {'workload': 'config2 cfgs/train_deformable.yaml: R-50 Deformable-DETR inference forward, '
                                    'd=256, 4 levels, 6/6 layers, 300 queries, box refine',
-                       'frames_per_gpu_per_step': a.batch, 'frame': [3, a.height, a.width],
+                       'frames_per_gpu_per_step': a.batch, 'in_flight_batches': nst,
+                       'frame': [3, a.height, a.width],
                        'parallelism': f'replicas x{world}'},
             'roofline': roofline,
             'roofline_mfma': mfma_roof,
