@@ -75,7 +75,11 @@ int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num
  * f32 sampling_loc / attn_weight tensors (needed to run kinet_msda_backward).
  * output_dtype = value_dtype, or KINET_BF16 from KINET_F16 values (f16 values are gathered
  * and accumulated by mixed f16 x f32 FMAs; head_dim 32, L*P in {16, 32} only).
- * offlog_dtype: KINET_F32, or KINET_F16 with 16-bit values (same restrictions). */
+ * offlog_dtype: KINET_F32, or KINET_F16 with 16-bit values (same restrictions).
+ * query_tile_order: optional (NULL = natural order) permutation of the ceil(num_query / 16)
+ *                 16-query tiles giving the order the specialised kernel processes them in
+ *                 (outputs unchanged); the encoder passes its tiles sorted by image row across
+ *                 levels so the value rows they share are fetched into L2 once. */
 int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_ss, int64_t value_sm,
                              const int64_t* spatial_shapes,
                              const void* offsets_logits, int ld_off,
@@ -84,7 +88,8 @@ int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_
                              void* output, float* loc_out, float* attw_out,
                              int batch, int spatial_size, int num_heads, int channels,
                              int num_levels, int num_query, int num_point,
-                             int value_dtype, int output_dtype, int offlog_dtype, kinet_stream_t stream);
+                             int value_dtype, int output_dtype, int offlog_dtype,
+                             const int32_t* query_tile_order, kinet_stream_t stream);
 
 /* Diagnostic kernel-selection knob (no reference counterpart): bit 0 = never use the
  * specialised 16-bit / head_dim-32 fused kernel.  Returns the previous flags. */

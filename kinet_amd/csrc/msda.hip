@@ -506,7 +506,7 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
     const T* __restrict__ value, long vsb, int vss, long vsm, int head_bytes, const int64_t* __restrict__ shapes,
     const TL* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
     const uint8_t* __restrict__ qmask, float* __restrict__ loc_out, float* __restrict__ attw_out,
-    TO* __restrict__ out, int S, int M, int Lq) {
+    TO* __restrict__ out, int S, int M, int Lq, const int* __restrict__ torder) {
     static_assert(sizeof(T) == 2 && sizeof(TO) == 2, "16-bit values and output");
     constexpr int D = 32, QT = 16, MH = kThreads / 64, LP = L * P;
     static_assert((LP & (LP - 1)) == 0 && LP <= 64 && L <= kMaxLevels, "L*P: power of two <= 64");
@@ -525,7 +525,10 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
         const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
         const int qd = nblk >> 3, rm = nblk & 7, xcd = lin & 7;
         const int nid = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + (lin >> 3);
-        const int bx = nid % gx, rest = nid / gx;
+        const int bxl = nid % gx, rest = nid / gx;
+        // optional processing order of the query tiles (results unchanged): the encoder
+        // interleaves the tiles of all levels by image row so one L2 pass serves them all
+        const int bx = torder ? torder[bxl] : bxl;
         b = rest % gy;
         q0 = bx * QT;
         mh0 = (rest / gy) * MH;
@@ -969,7 +972,8 @@ namespace {
 template <typename T, typename TO = T, typename TL = float>
 int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* shapes, const void* offlog_v,
                  int ld_off, const float* ref, int ref_dim, const uint8_t* qmask, void* out, float* loc_out,
-                 float* attw_out, int N, int S, int M, int D, int L, int Lq, int P, hipStream_t stream) {
+                 float* attw_out, int N, int S, int M, int D, int L, int Lq, int P, const int* torder,
+                 hipStream_t stream) {
     const Cfg c = pick_cfg(D, M, sizeof(T));
     KINET_CHECK_ARG(c.lpq <= 64, "msda fused: head_dim/vec (%d) exceeds a wave", c.lpq);
     if (N == 0 || Lq == 0) return KINET_OK;
@@ -983,12 +987,12 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
                 hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 4, 4>), grid, dim3(kThreads), 0, stream,
                                    (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v, ld_off,
                                    ref, ref_dim, qmask, loc_out,
-                                   attw_out, (TO*)out, S, M, Lq);
+                                   attw_out, (TO*)out, S, M, Lq, torder);
             else
                 hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 8, 4>), grid, dim3(kThreads), 0, stream,
                                    (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v, ld_off,
                                    ref, ref_dim, qmask, loc_out,
-                                   attw_out, (TO*)out, S, M, Lq);
+                                   attw_out, (TO*)out, S, M, Lq, torder);
             KINET_LAUNCH_CHECK();
             return KINET_OK;
         }
@@ -1036,7 +1040,8 @@ extern "C" int kinet_msda_fused_forward(const void* value, int64_t value_sb, int
                                         const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
                                         void* output, float* loc_out, float* attw_out, int batch, int spatial_size,
                                         int num_heads, int channels, int num_levels, int num_query, int num_point,
-                                        int value_dtype, int output_dtype, int offlog_dtype, kinet_stream_t stream) {
+                                        int value_dtype, int output_dtype, int offlog_dtype,
+                                        const int32_t* query_tile_order, kinet_stream_t stream) {
     int rc = common_checks(batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, 1);
     if (rc) return rc;
     KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.", ref_dim);
@@ -1055,7 +1060,7 @@ extern "C" int kinet_msda_fused_forward(const void* value, int64_t value_sb, int
     hipStream_t s = (hipStream_t)stream;
 #define ARGS value, (long)value_sb, (int)value_ss, (long)value_sm, spatial_shapes, offsets_logits, ld_off, \
              ref_points, ref_dim, query_attn_mask, output, loc_out, attw_out, batch, spatial_size, num_heads, channels, \
-             num_levels, num_query, num_point, s
+             num_levels, num_query, num_point, (const int*)query_tile_order, s
     KINET_CHECK_ARG(output_dtype == value_dtype || (value_dtype == KINET_F16 && output_dtype == KINET_BF16),
                     "msda fused forward: output dtype %d unsupported for value dtype %d", output_dtype, value_dtype);
     KINET_CHECK_ARG(offlog_dtype == KINET_F32 || offlog_dtype == KINET_F16,

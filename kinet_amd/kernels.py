@@ -363,8 +363,34 @@ def box_refine(tmp, ref, valid_ratios=None, want_input=True):
 
 
 # ------------------------------------------------------------------------------ MSDA
+_tile_orders = {}
+
+
+def encoder_tile_order(shapes, device, qt=16):
+    """Processing order of the encoder's 16-query tiles for msda_fused: sorted by the
+    normalised image row of each tile's first query, so the tiles of all levels that sample
+    the same image band run together and share the value rows in L2 (the natural order
+    sweeps the image once per level).  Cached per (shapes, device)."""
+    key = (tuple(tuple(int(v) for v in s) for s in shapes), str(device), qt)
+    o = _tile_orders.get(key)
+    if o is None:
+        import numpy as np
+        hw = np.array([h * w for h, w in key[0]], dtype=np.int64)
+        starts = np.concatenate([[0], np.cumsum(hw)[:-1]])
+        lq = int(hw.sum())
+        q = np.arange((lq + qt - 1) // qt, dtype=np.int64) * qt
+        lvl = np.searchsorted(starts, q, side='right') - 1
+        H = np.array([h for h, _ in key[0]], dtype=np.float64)[lvl]
+        W = np.array([w for _, w in key[0]], dtype=np.int64)[lvl]
+        y = ((q - starts[lvl]) // W + 0.5) / H
+        o = torch.as_tensor(np.argsort(y, kind='stable').astype(np.int32), device=device)
+        _tile_orders[key] = o
+    return o
+
+
 def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_levels, n_points,
-               query_attn_mask=None, want_loc_attw=False, head_major=False, out_dtype=None):
+               query_attn_mask=None, want_loc_attw=False, head_major=False, out_dtype=None,
+               query_tile_order=None):
     """Sampling of MSDeformAttn.forward (ms_deform_attn.py:69-87) in one kernel.
     value: projected values, either (B, S, d) row-major (column slices allowed) or, with
     head_major=True, (M, B, S, D) as written by value_proj_headmajor;
@@ -405,7 +431,7 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
     N.call('kinet_msda_fused_forward', N.ptr(value), vsb, vss, vsm, N.ptr(spatial_shapes), N.ptr(offlog),
            offlog.shape[-1], N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), N.ptr(loc), N.ptr(attw), B, S,
            n_heads, D, n_levels, Lq, n_points, N.dtype_code(value.dtype), N.dtype_code(od), N.dtype_code(offlog.dtype),
-           N.stream(value.device),
+           N.ptr(query_tile_order), N.stream(value.device),
            work={'family': 'msda', 'flops': 10.0 * nsamp * D,
                  # compulsory bytes: value once, f32 offsets+logits, refs, output once
                  'bytes': B * S * d * ev + nsamp * 3 * offlog.element_size() + ref.numel() * 4

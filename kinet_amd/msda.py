@@ -118,7 +118,8 @@ class MSDeformAttn(nn.Module):
                            lambda a, b: torch.cat([a.detach(), b.detach()], 0).float().contiguous())
         return w, b
 
-    def sample(self, query, reference_points, value, input_spatial_shapes, query_attn_mask=None, query_add=None):
+    def sample(self, query, reference_points, value, input_spatial_shapes, query_attn_mask=None, query_add=None,
+               query_order=None):
         """value already projected: head-major (M, N, S, D) from project_value (or a
         row-major (N, S, d) tensor); the offsets/weights projection input is query
         (+ query_add, e.g. the position embedding, added at GEMM load time); returns the
@@ -130,7 +131,7 @@ class MSDeformAttn(nn.Module):
         offlog = K.linear(query, w, b, out_dtype=od, x_add=query_add)
         return K.msda_fused(value, input_spatial_shapes, offlog, reference_points,
                             self.n_heads, self.n_levels, self.n_points, query_attn_mask,
-                            head_major=(value.dim() == 4), out_dtype=query.dtype)
+                            head_major=(value.dim() == 4), out_dtype=query.dtype, query_tile_order=query_order)
 
     def _forward_autograd(self, query, reference_points, input_flatten, input_spatial_shapes,
                           input_padding_mask, query_attn_mask):

@@ -235,3 +235,21 @@ def test_fast_fused_f16_offsets_logits():
     torch.testing.assert_close(aw16, aw32, rtol=1e-5, atol=1e-7)
     d = (o16.float() - o32.float()).abs()
     assert (d <= o32.float().abs() * 2.0 ** -7 + 1e-4).all(), d.max().item()
+
+
+def test_fast_fused_query_tile_order_invariant():
+    """The encoder's tile processing order (kinet_amd.kernels.encoder_tile_order) changes only
+    WHEN each 16-query tile runs: every output / loc / attw is bit-identical to natural order."""
+    from kinet_amd import kernels as K
+    shapes = ((40, 50), (20, 25), (10, 13), (5, 7))
+    B, M, P = 2, 8, 4
+    Lq = sum(h * w for h, w in shapes)
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 21, dtype=torch.float16)
+    order = K.encoder_tile_order(shapes, value.device)
+    assert sorted(order.tolist()) == list(range((Lq + 15) // 16)) and order.tolist() != sorted(order.tolist())
+    o0, l0, a0 = K.msda_fused(value, ss, offlog.half(), ref, M, 4, P, qmask, want_loc_attw=True, head_major=True,
+                              out_dtype=torch.bfloat16)
+    o1, l1, a1 = K.msda_fused(value, ss, offlog.half(), ref, M, 4, P, qmask, want_loc_attw=True, head_major=True,
+                              out_dtype=torch.bfloat16, query_tile_order=order)
+    torch.cuda.synchronize()
+    assert torch.equal(o0, o1) and torch.equal(l0, l1) and torch.equal(a0, a1)

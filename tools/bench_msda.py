@@ -68,9 +68,15 @@ def main():
     ap.add_argument('--noise', type=float, default=0.0)
     ap.add_argument('--iters', type=int, default=50)
     ap.add_argument('--decoder', action='store_true')
+    ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--order', action='store_true', help='encoder tile order (kernels.encoder_tile_order)')
     a = ap.parse_args()
-    value, ss, offlog, ref, (M, L, P) = make_inputs(noise=a.noise, decoder=a.decoder)
-    fn = lambda: K.msda_fused(value, ss, offlog, ref, M, L, P, head_major=True)   # noqa: E731
+    value, ss, offlog, ref, (M, L, P) = make_inputs(B=a.batch, noise=a.noise, decoder=a.decoder,
+                                                    dtype=torch.float16)
+    offlog = offlog.half()
+    order = K.encoder_tile_order(ss.tolist(), value.device) if a.order and not a.decoder else None
+    fn = lambda: K.msda_fused(value, ss, offlog, ref, M, L, P, head_major=True, out_dtype=torch.bfloat16,   # noqa: E731
+                              query_tile_order=order)
     ms = time_call(fn, a.iters)
     B, Lq = offlog.shape[:2]
     S = value.shape[2]
