@@ -55,6 +55,14 @@ int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, int Hin, int
                  int in_dtype, const float* scale, const float* bias, const void* R, int ldr,
                  int relu, int ldy, kinet_stream_t stream);
 
+/* kinet_conv2d with separate vertical / horizontal stride and padding
+ * (Hout = (Hin + 2*pad_h - KH)/stride_h + 1, Wout = (Win + 2*pad_w - KW)/stride_w + 1);
+ * used for the tap-folded ResNet stem (kinet_pack_image_kwfold). */
+int kinet_conv2d_ex(const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin,
+                    int Hout, int Wout, int Cout, int KH, int KW, int stride_h, int stride_w, int pad_h,
+                    int pad_w, int in_dtype, const float* scale, const float* bias, const void* R, int ldr,
+                    int relu, int ldy, kinet_stream_t stream);
+
 /* value_proj for MSDA: C = (A @ B^T + bias) with rows masked, stored HEAD-MAJOR:
  * row r = b*rows_per_batch + s, column n = g*head_dim + d  ->  C[((g*batch + b)*rows_per_batch + s)*head_dim + d]
  * i.e. (N/head_dim, batch, rows_per_batch, head_dim) -- the layout kinet_msda_fused_forward

@@ -32,6 +32,15 @@ int kinet_maxpool2d_3x3s2(const void* x, void* y, int N, int H, int W, int C, in
 int kinet_pack_image_nhwc(const float* x, void* y, int N, int H, int W, int Cpad, int dtype,
                           kinet_stream_t stream);
 
+/* Stem input with the horizontal taps of a KW-wide, stride-s filter folded into channels:
+ * (N, 3, H, W) f32 NCHW -> (N, H, Wo, Cg) in bf16/f16/f32 with y[n][h][ow][kw*3 + c] =
+ * x[n][c][h][ow*stride - pad + kw] (0 outside the image and for channels >= 3*KW),
+ * Wo = (W + 2*pad - KW)/stride + 1, Cg % 8 == 0.  The KHxKW stride-s convolution of the image
+ * (ResNet conv1, backbone.py) is then the KHx1 convolution of y with strides (s, 1), pads
+ * (pad, 0) and weights w'[o][kh][0][kw*3 + c] = w[o][c][kh][kw] (kinet_conv2d_ex). */
+int kinet_pack_image_kwfold(const float* x, void* y, int N, int H, int W, int KW, int stride, int pad,
+                            int Cg, int dtype, kinet_stream_t stream);
+
 /* y = a + b, n elements. */
 int kinet_add(const void* a, const void* b, void* y, int64_t n_lo, int dtype, kinet_stream_t stream);
 

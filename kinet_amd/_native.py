@@ -30,6 +30,7 @@ _SIGS = {
     'kinet_gemm': [P, P, P] + [I] * 7 + [P, P, P, I, I, I, P, I, P],
     'kinet_gemm_ex': [P, P, P, P] + [I] * 7 + [P, P, P, I, I, P, P, F, I, P, P],
     'kinet_conv2d': [P, P, P] + [I] * 12 + [P, P, P, I, I, I, P],
+    'kinet_conv2d_ex': [P, P, P] + [I] * 14 + [P, P, P, I, I, I, P],
     'kinet_conv2d_splitk': [P, P, P] + [I] * 12 + [P, P, P, I, I, I, P, I, P],
     'kinet_gemm_splitk': [P, P, P] + [I] * 7 + [P, P, P, I, I, P, P, F, I, P, P, I, P],
     'kinet_ffn_pack': [P, P, P, I, I, I, P],
@@ -39,6 +40,7 @@ _SIGS = {
     'kinet_groupnorm': [P] * 4 + [I] * 5 + [F, I, P, P],
     'kinet_maxpool2d_3x3s2': [P, P] + [I] * 5 + [P],
     'kinet_pack_image_nhwc': [P, P] + [I] * 5 + [P],
+    'kinet_pack_image_kwfold': [P, P] + [I] * 8 + [P],
     'kinet_mha_core': [P, I, P, I, P, I, P, I] + [I] * 5 + [F, I, P, P],
     'kinet_add': [P, P, P, I64, I, P],
     'kinet_box_refine': [P, P, I, P, P, P, I, I, I, P],

@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
             const int rem = m - img * hw;
             const int oh = rem / p.Wout, ow = rem - (rem / p.Wout) * p.Wout;
             xih[i] = oh * p.stride - p.pad;
-            xiw[i] = ow * p.stride - p.pad;
+            xiw[i] = ow * p.stride_w - p.pad_w;
             // element offset of the receptive field's (0, 0) tap (may lie outside the image:
             // only ever used behind the bounds test)
             xbase[i] = (unsigned)img * (unsigned)(p.Hin * p.Win * p.Cin) +
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const GemmArgs p, cons
             const int rem = m - img * hw;
             const int oh = rem / p.Wout, ow = rem - (rem / p.Wout) * p.Wout;
             xih[i] = oh * p.stride - p.pad;
-            xiw[i] = ow * p.stride - p.pad;
+            xiw[i] = ow * p.stride_w - p.pad_w;
             xbase[i] = (unsigned)img * (unsigned)(p.Hin * p.Win * p.Cin);
         } else {
             xih[i] = xiw[i] = 0;
@@ -672,6 +672,10 @@ int launch(const GemmArgs& a, hipStream_t stream) {
 template <bool CONV>
 int dispatch(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t s) {
     if (!CONV && a.kchunk == 0 && !(kinet_gemm_flags & 4) && launch_rw(a, in_dtype, out_dtype, s)) {
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
+    if (CONV && a.kchunk == 0 && !(kinet_gemm_flags & 4) && out_dtype == in_dtype && launch_rw_conv(a, in_dtype, s)) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;
     }
@@ -894,12 +898,12 @@ extern "C" int kinet_gemm(const void* A, const void* B, void* C, int M, int N, i
 }
 
 static int conv_args(GemmArgs& a, const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin,
-                     int Hout, int Wout, int Cout, int KH, int KW, int stride, int pad, int in_dtype,
+                     int Hout, int Wout, int Cout, int KH, int KW, int stride, int pad, int stride_w, int pad_w, int in_dtype,
                      const float* scale, const float* bias, const void* R, int ldr, int relu, int ldy) {
-    KINET_CHECK_ARG(batch >= 0 && Hin > 0 && Win > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
+    KINET_CHECK_ARG(batch >= 0 && Hin > 0 && Win > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0 && stride_w > 0 && pad_w >= 0,
                     "conv2d: invalid geometry");
     KINET_CHECK_ARG(Cin % 8 == 0, "conv2d: Cin (%d) must be a multiple of 8 (pad channels)", Cin);
-    KINET_CHECK_ARG(Hout == (Hin + 2 * pad - KH) / stride + 1 && Wout == (Win + 2 * pad - KW) / stride + 1,
+    KINET_CHECK_ARG(Hout == (Hin + 2 * pad - KH) / stride + 1 && Wout == (Win + 2 * pad_w - KW) / stride_w + 1,
                     "conv2d: output size mismatch");
     KINET_CHECK_ARG(ldy >= Cout && (R == nullptr || ldr >= Cout), "conv2d: ldy/ldr < Cout");
     KINET_CHECK_ARG(aligned16(X) && aligned16(Wt), "conv2d: X and W must be 16-byte aligned");
@@ -909,6 +913,7 @@ static int conv_args(GemmArgs& a, const void* X, const void* Wt, void* Y, int ba
     a.M = (int)M; a.N = Cout; a.K = KH * KW * Cin; a.lda = 0; a.ldb = KH * KW * Cin; a.ldc = ldy; a.ldr = ldr;
     a.relu = relu;
     a.Hin = Hin; a.Win = Win; a.Cin = Cin; a.Hout = Hout; a.Wout = Wout; a.KW = KW; a.stride = stride; a.pad = pad;
+    a.stride_w = stride_w; a.pad_w = pad_w;
     const long long es = (long long)dtype_size(in_dtype);
     const long long ab = (long long)batch * Hin * Win * Cin * es;
     const long long bb = (long long)Cout * KH * KW * Cin * es;
@@ -920,20 +925,28 @@ static int conv_args(GemmArgs& a, const void* X, const void* Wt, void* Y, int ba
         KINET_CHECK_ARG(rb < (1LL << 31), "conv2d: residual larger than 2 GiB (split the batch)");
         a.r_bytes = (int)rb;
     }
-    if (KH == 1 && KW == 1 && stride == 1 && pad == 0) a.lda = Cin;   // plain GEMM over NHWC rows
+    if (KH == 1 && KW == 1 && stride == 1 && pad == 0 && stride_w == 1 && pad_w == 0) a.lda = Cin;   // plain GEMM over NHWC rows
     return KINET_OK;
+}
+
+extern "C" int kinet_conv2d_ex(const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin,
+                               int Hout, int Wout, int Cout, int KH, int KW, int stride_h, int stride_w, int pad_h,
+                               int pad_w, int in_dtype, const float* scale, const float* bias, const void* R, int ldr,
+                               int relu, int ldy, kinet_stream_t stream) {
+    GemmArgs a{};
+    int rc = conv_args(a, X, Wt, Y, batch, Hin, Win, Cin, Hout, Wout, Cout, KH, KW, stride_h, pad_h, stride_w, pad_w,
+                       in_dtype, scale, bias, R, ldr, relu, ldy);
+    if (rc) return rc;
+    // a 1x1 stride-1 convolution over NHWC rows is the plain GEMM Y = X W^T (lda = Cin)
+    if (a.lda) return dispatch<false>(a, in_dtype, in_dtype, (hipStream_t)stream);
+    return dispatch<true>(a, in_dtype, in_dtype, (hipStream_t)stream);
 }
 
 extern "C" int kinet_conv2d(const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin, int Hout,
                             int Wout, int Cout, int KH, int KW, int stride, int pad, int in_dtype, const float* scale,
                             const float* bias, const void* R, int ldr, int relu, int ldy, kinet_stream_t stream) {
-    GemmArgs a{};
-    int rc = conv_args(a, X, Wt, Y, batch, Hin, Win, Cin, Hout, Wout, Cout, KH, KW, stride, pad, in_dtype, scale, bias,
-                       R, ldr, relu, ldy);
-    if (rc) return rc;
-    // a 1x1 stride-1 convolution over NHWC rows is the plain GEMM Y = X W^T (lda = Cin)
-    if (a.lda) return dispatch<false>(a, in_dtype, in_dtype, (hipStream_t)stream);
-    return dispatch<true>(a, in_dtype, in_dtype, (hipStream_t)stream);
+    return kinet_conv2d_ex(X, Wt, Y, batch, Hin, Win, Cin, Hout, Wout, Cout, KH, KW, stride, stride, pad, pad, in_dtype,
+                           scale, bias, R, ldr, relu, ldy, stream);
 }
 
 extern "C" int kinet_conv2d_splitk(const void* X, const void* Wt, void* Y, int batch, int Hin, int Win, int Cin,
@@ -941,8 +954,8 @@ extern "C" int kinet_conv2d_splitk(const void* X, const void* Wt, void* Y, int b
                                    const float* scale, const float* bias, const void* R, int ldr, int relu, int ldy,
                                    float* workspace, int ksplit, kinet_stream_t stream) {
     GemmArgs a{};
-    int rc = conv_args(a, X, Wt, Y, batch, Hin, Win, Cin, Hout, Wout, Cout, KH, KW, stride, pad, in_dtype, scale, bias,
-                       R, ldr, relu, ldy);
+    int rc = conv_args(a, X, Wt, Y, batch, Hin, Win, Cin, Hout, Wout, Cout, KH, KW, stride, pad, stride, pad, in_dtype,
+                       scale, bias, R, ldr, relu, ldy);
     if (rc) return rc;
     if (a.M == 0) return KINET_OK;
     if (a.lda) return run_splitk<false>(a, in_dtype, in_dtype, workspace, ksplit, (hipStream_t)stream);

@@ -24,6 +24,7 @@ struct GemmArgs {
     float ln_eps;
     int a_bytes, b_bytes;   // buffer-descriptor extents (bytes, < 2^31)
     int r_bytes;            // residual extent (gemm_rw.hip stages R by LDS-DMA)
+    int c_bytes;            // output extent (gemm_rw.hip writes C by buffer stores)
     // head-major store (hm_rows > 0): row r = b*hm_rows + s, column n = g*hm_d + d goes to
     // C[((g*hm_batch + b)*hm_rows + s)*hm_d + d]  -- the MSDA value layout (heads, B, S, D)
     int hm_rows, hm_d, hm_batch;
@@ -33,10 +34,13 @@ struct GemmArgs {
     int kchunk;
     long c_slice;
     int Hin, Win, Cin, Hout, Wout, KW, stride, pad;
+    int stride_w, pad_w;   // horizontal stride / padding (== stride / pad for square convs)
 };
 
 // gemm_rw.hip: resident-weight streaming GEMM; false = problem not eligible
 bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t stream);
+// gemm_rw.hip: the tap-folded stem convolution (conv-row gather); false = not eligible
+bool launch_rw_conv(const GemmArgs& a, int in_dtype, hipStream_t stream);
 extern int rw_min_m;
 
 namespace {

@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dma_kernel(const GemmArgs p, cons
             const int rem = m - img * hw;
             const int oh = rem / p.Wout, ow = rem - (rem / p.Wout) * p.Wout;
             xih[i] = oh * p.stride - p.pad;
-            xiw[i] = ow * p.stride - p.pad;
+            xiw[i] = ow * p.stride_w - p.pad_w;
             // element offset of the receptive field's (0, 0) tap (used only behind the bounds test)
             xbase[i] = (unsigned)img * (unsigned)(p.Hin * p.Win * p.Cin) +
                        (unsigned)((xih[i] * p.Win + xiw[i]) * p.Cin);

@@ -108,7 +108,11 @@ __device__ __forceinline__ void unpack8(const u32x4& u, float* v, bool f16) {
     }
 }
 
-template <typename T, typename TO, int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2>
+// CR (conv-row mode): A row m is output pixel (img, oh, ow) of a KH x 1, horizontally
+// stride-1 unpadded NHWC convolution (the tap-folded ResNet stem, ops.hip
+// pack_image_kwfold_kernel): K = KH*Cin, logical chunk q of the row = 8 channels of tap
+// kh = q / (Cin/8) read from input row oh*stride - pad + kh (zeros outside the image and past K)
+template <typename T, typename TO, int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2, bool CR>
 __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const int n_mtiles) {
     using C_ = RwCfg<KC, NT, BMR, NS, HAS_R, LN, HAS_A2>;
     constexpr int TMR = BMR / 16;             // 16-row MFMA tiles per row tile
@@ -149,7 +153,8 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
             const int n = ncol0 + wave * NC * 4 + (i >> 2) * NC + a * 4 + (i & 3);
 #pragma unroll
             for (int c = 0; c < KC; ++c) {
-                const unsigned off = n < N ? ((unsigned)n * (unsigned)p.ldb + (unsigned)(c * 32 + (lane >> 4) * 8)) * 2u : OOB;
+                const int k = c * 32 + (lane >> 4) * 8;
+                const unsigned off = (n < N && k < p.K) ? ((unsigned)n * (unsigned)p.ldb + (unsigned)k) * 2u : OOB;
                 wf[a][c] = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0);
             }
         }
@@ -164,26 +169,68 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
         __builtin_amdgcn_make_buffer_rsrc((void*)(p.row_mask ? (const void*)p.row_mask : p.A), (short)0,
                                           p.row_mask ? M : 0, 0x00020000);
 
+    // per-thread DMA offsets, split into a scalar tile base (m0 * ld) and lane constants
+    unsigned a_lo[C_::A_OPS];
+    int a_row[C_::A_OPS];
+    int cr_kh[C_::A_OPS];
+#pragma unroll
+    for (int j = 0; j < C_::A_OPS; ++j) {
+        const int idx = j * 256 + tid;
+        const int row = idx / C_::CPR, s = idx % C_::CPR;
+        a_row[j] = row;
+        a_lo[j] = ((unsigned)row * (unsigned)p.lda + (unsigned)((s ^ (row & C_::SWM)) * 8)) * 2u;
+        cr_kh[j] = 0;
+        if (CR) {
+            // tap and in-tap channel offset of logical chunk q (lane constants); chunks past K
+            // get a tap index that never lands inside the image
+            const int q = s ^ (row & C_::SWM), cpt = p.Cin >> 3;
+            const int kh = q / cpt;
+            cr_kh[j] = q * 8 < p.K ? kh : (1 << 28);
+            a_lo[j] = (unsigned)((q - kh * cpt) * 8);
+        }
+    }
+    unsigned r_lo[C_::R_OPS > 0 ? C_::R_OPS : 1];
+    int r_row[C_::R_OPS > 0 ? C_::R_OPS : 1];
+#pragma unroll
+    for (int j = 0; j < C_::R_OPS; ++j) {
+        const int idx = j * 256 + tid;
+        const int row = idx / C_::R_CPR, s = idx % C_::R_CPR;
+        const int n = ncol0 + (s ^ (row & C_::R_SWM)) * 8;
+        r_row[j] = n < N ? row : (1 << 30);   // columns past N: never in range
+        r_lo[j] = ((unsigned)row * (unsigned)p.ldr + (unsigned)n) * 2u;
+    }
     auto issue = [&](int i) {
         const int m0 = (bx + i * P) * BMR;
         char* st = stages + (i % NS) * C_::STAGE;
+        const unsigned abase = (unsigned)m0 * (unsigned)p.lda * 2u;
+        // conv-row mode: the tile's first pixel on the scalar unit, then row r of the tile is
+        // that pixel + r with at most one carry into the next output row (host: Wout >= BMR)
+        const int hw = p.Hout * p.Wout;
+        const int img0 = CR ? m0 / hw : 0;
+        const int oh0 = CR ? (m0 - img0 * hw) / p.Wout : 0;
+        const int ow0 = CR ? m0 - img0 * hw - oh0 * p.Wout : 0;
 #pragma unroll
         for (int j = 0; j < C_::A_OPS; ++j) {
-            const int idx = j * 256 + tid;
-            const int row = idx / C_::CPR, s = idx % C_::CPR;
-            const int q = s ^ (row & C_::SWM);
-            const int m = m0 + row;
-            const unsigned off = m < M ? ((unsigned)m * (unsigned)p.lda + (unsigned)(q * 8)) * 2u : OOB;
+            unsigned off = m0 + a_row[j] < M ? abase + a_lo[j] : OOB;
+            if (CR) {
+                int ow = ow0 + a_row[j], oh = oh0, img = img0;
+                const bool c1 = ow >= p.Wout;
+                ow = c1 ? ow - p.Wout : ow;
+                oh = c1 ? oh + 1 : oh;
+                const bool c2 = oh >= p.Hout;
+                oh = c2 ? 0 : oh;
+                img = c2 ? img + 1 : img;
+                const int ih = oh * p.stride - p.pad + cr_kh[j];
+                const bool ok = m0 + a_row[j] < M && (unsigned)ih < (unsigned)p.Hin;
+                off = ok ? ((unsigned)((img * p.Hin + ih) * p.Win + ow) * (unsigned)p.Cin + a_lo[j]) * 2u : OOB;
+            }
             dma16(ra, st + (j * 256 + wave * 64) * 16, off);
             if (HAS_A2) dma16(ra2, st + C_::A_BYTES + (j * 256 + wave * 64) * 16, off);
         }
+        const unsigned rbase = (unsigned)m0 * (unsigned)p.ldr * 2u;
 #pragma unroll
         for (int j = 0; j < C_::R_OPS; ++j) {
-            const int idx = j * 256 + tid;
-            const int row = idx / C_::R_CPR, s = idx % C_::R_CPR;
-            const int q = s ^ (row & C_::R_SWM);
-            const int m = m0 + row, n = ncol0 + q * 8;
-            const unsigned off = (m < M && n < N) ? ((unsigned)m * (unsigned)p.ldr + (unsigned)n) * 2u : OOB;
+            const unsigned off = m0 + r_row[j] < M ? rbase + r_lo[j] : OOB;
             dma16(rr, st + C_::R_OFF + (j * 256 + wave * 64) * 16, off);
         }
         // row-mask bytes m0 .. m0+BMR (every wave writes the same 1 KiB; bytes past M read 0)
@@ -196,39 +243,65 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
         if (s < cnt) issue(s);
 
     const int cl0 = wave * NC * 4 + (lane >> 4) * NC;   // this lane's first column in the group
-    uint32_t pend[TMR][PW];
+    uint32_t pend[TMR][PW] = {};
     int pend_m0 = 0;
-    auto store_pending = [&]() {
-        TO* __restrict__ C = (TO*)p.C;
-        constexpr int EPC16 = 16 / (int)sizeof(TO);     // elements per 16-byte store
+    // packed outputs of one row tile: ALWAYS S buffer stores per lane (offsets past the
+    // descriptor for rows / columns outside C and for the dummy call of iteration 0), so the
+    // counted waits below know exactly how many vector-memory ops are younger than a DMA
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, p.c_bytes, 0x00020000);
+    constexpr int EPC16 = 16 / (int)sizeof(TO);     // elements per 16-byte store
+    constexpr int S = TMR * (NC / EPC16);           // stores per lane per row tile
+    static_assert(NS >= 2 && NS <= 4 && (NS - 2) * (C_::D + S) <= 63, "ring depth / vmcnt range");
+    // element offset of (row m, column n): m * rs + colpart(n); head-major (hm_rows > 0):
+    // ((g*hm_batch + b)*hm_rows + s)*hm_d + d = g*M*hm_d + m*hm_d + d for m = b*hm_rows + s
+    const int rs = p.hm_rows ? p.hm_d : p.ldc;
+    unsigned s_lo[TMR][NC / EPC16];
+    bool s_nok[NC / EPC16];
+#pragma unroll
+    for (int h = 0; h < NC / EPC16; ++h) {
+        const int n = ncol0 + cl0 + h * EPC16;
+        s_nok[h] = n >= N;
+        const int g = p.hm_rows ? n / p.hm_d : 0;
+        const unsigned colpart = p.hm_rows ? (unsigned)g * (unsigned)M * (unsigned)p.hm_d + (unsigned)(n - g * p.hm_d)
+                                           : (unsigned)n;
+#pragma unroll
+        for (int t = 0; t < TMR; ++t)
+            s_lo[t][h] = ((unsigned)(t * 16 + (lane & 15)) * (unsigned)rs + colpart) * (unsigned)sizeof(TO);
+    }
+    auto store_pending = [&](bool valid) {
+        const unsigned base = (unsigned)pend_m0 * (unsigned)rs * (unsigned)sizeof(TO);
 #pragma unroll
         for (int t = 0; t < TMR; ++t) {
-            const int m = pend_m0 + t * 16 + (lane & 15);
-            if (m >= M) continue;
+            const bool mok = valid && pend_m0 + t * 16 + (lane & 15) < M;
 #pragma unroll
             for (int h = 0; h < NC / EPC16; ++h) {
-                const int n = ncol0 + cl0 + h * EPC16;
-                if (n >= N) continue;
-                TO* dst;
-                if (p.hm_rows) {
-                    const int bb = m / p.hm_rows, ss = m - bb * p.hm_rows;
-                    const int g = n / p.hm_d, dd = n - g * p.hm_d;
-                    dst = C + (((long)g * p.hm_batch + bb) * p.hm_rows + ss) * p.hm_d + dd;
-                } else {
-                    dst = C + (long)m * p.ldc + n;
-                }
-                *reinterpret_cast<u32x4*>(dst) =
-                    u32x4{pend[t][4 * h], pend[t][4 * h + 1], pend[t][4 * h + 2], pend[t][4 * h + 3]};
+                const unsigned off = (mok && !s_nok[h]) ? base + s_lo[t][h] : OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u32x4{pend[t][4 * h], pend[t][4 * h + 1], pend[t][4 * h + 2], pend[t][4 * h + 3]}, rc, off, 0, 0);
             }
         }
     };
 
     for (int i = 0; i < cnt; ++i) {
-        // retire tile i's DMA: loads issued after it are the (NS-2) later tiles' D each
-        if (i + NS - 2 < cnt) wait_vmcnt<(NS - 2) * C_::D>();
-        else wait_vmcnt<0>();
+        // retire tile i's DMA.  Younger vector-memory ops: the DMA of the (NS-2) later tiles
+        // (D each) and the stores (S each) of the min(i, NS-2) iterations issued after it
+        if (i + NS - 2 >= cnt) wait_vmcnt<0>();
+        else if (NS <= 2 || i >= NS - 2) wait_vmcnt<(NS - 2) * (C_::D + S)>();
+        else if (i == 0) wait_vmcnt<(NS - 2) * C_::D>();
+        else wait_vmcnt<(NS - 2) * C_::D + S>();   // i == 1 (NS == 4)
+        if (HAS_A2) {
+            // q = src + pos rounded to the operand type, exactly as gemm.hip's load-time add:
+            // each thread sums the chunks its own DMA delivered (landed: the wait above), once
+            // per tile instead of once per wave; the barrier publishes the sums
+            char* st = stages + (i % NS) * C_::STAGE;
+#pragma unroll
+            for (int j = 0; j < C_::A_OPS; ++j) {
+                u32x4* pa = reinterpret_cast<u32x4*>(st + (j * 256 + tid) * 16);
+                *pa = Mma<T>::add(*pa, *reinterpret_cast<const u32x4*>(st + C_::A_BYTES + (j * 256 + tid) * 16));
+            }
+        }
         lds_barrier();
-        if (i > 0) store_pending();
+        store_pending(i > 0);
         if (i + NS - 1 < cnt) issue(i + NS - 1);
 
         const char* st = stages + (i % NS) * C_::STAGE;
@@ -245,9 +318,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
                 const int row = t * 16 + (lane & 15);
                 const int q = c * 4 + (lane >> 4);
                 const int xo = row * C_::ROW + ((q ^ (row & C_::SWM)) << 4);
-                u32x4 xf = *reinterpret_cast<const u32x4*>(st + xo);
-                // q = src + pos rounded to the operand type, exactly as gemm.hip's load-time add
-                if (HAS_A2) xf = Mma<T>::add(xf, *reinterpret_cast<const u32x4*>(st + C_::A_BYTES + xo));
+                const u32x4 xf = *reinterpret_cast<const u32x4*>(st + xo);
 #pragma unroll
                 for (int a = 0; a < NT; ++a) Mma<T>::run(acc[a][t], wf[a][c], xf);
             }
@@ -324,34 +395,56 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
         }
         pend_m0 = m0;
     }
-    if (cnt > 0) store_pending();
+    if (cnt > 0) store_pending(true);
 }
 
-template <typename T, typename TO, int KC, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2 = false>
+template <typename T, typename TO, int KC, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2 = false, int NT = 4,
+          bool CR = false>
 void launch_cfg(const GemmArgs& a, hipStream_t stream) {
-    constexpr int GW = 256;
+    constexpr int GW = 4 * NT * 16;
     const int n_mtiles = (a.M + BMR - 1) / BMR;
     const int ng = (a.N + GW - 1) / GW;
-    int P = (512 / ng + 7) / 8 * 8;           // 2 resident workgroups per CU over all groups
+    // 2 resident workgroups per CU over all groups: never more than the 512 slots (a second
+    // round of workgroups would double the launch), and a multiple of 8 so the column groups
+    // of one row tile land on one XCD (linear id bx + y*P) and share its L2 copy of the tile
+    int P = 512 / ng >= 8 ? 512 / ng / 8 * 8 : 512 / ng;
     if (P > n_mtiles) P = n_mtiles;
     dim3 grid(P, ng), block(256);
-    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, 4, BMR, NS, HAS_R, LN, HAS_A2>), grid, block, 0, stream, a, n_mtiles);
+    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR>), grid, block, 0, stream, a,
+                       n_mtiles);
+}
+
+// deepest DMA ring (<= 4 row tiles) that keeps the workgroup within 80 KiB of LDS (two per CU)
+template <int KC, int BMR, bool HAS_R, bool LN, bool HAS_A2>
+constexpr int ring_depth() {
+    constexpr int base = RwCfg<KC, 4, BMR, 1, HAS_R, LN, HAS_A2>::BYTES -
+                         RwCfg<KC, 4, BMR, 1, HAS_R, LN, HAS_A2>::STAGE;
+    constexpr int stage = RwCfg<KC, 4, BMR, 1, HAS_R, LN, HAS_A2>::STAGE;
+    return (80 * 1024 - base) / stage >= 4 ? 4 : (80 * 1024 - base) / stage;
+}
+
+template <typename T, typename TO, int KC, bool HAS_R, bool LN, bool HAS_A2>
+void launch_ring(const GemmArgs& a, hipStream_t stream) {
+    // 16-row tiles when a tile carries a second operand (residual / A2) or the LayerNorm
+    // epilogue (which needs them at K = 256 to stay in 256 VGPRs): a 4-deep ring then fits;
+    // K = 64 rows (128 B) need 32-row tiles for whole 4 KiB DMA rounds
+    constexpr int BMR = (KC == 2 || (!HAS_R && !LN && !HAS_A2)) ? 32 : 16;
+    constexpr int NS = ring_depth<KC, BMR, HAS_R, LN, HAS_A2>();
+    static_assert(NS >= 2, "LDS budget");
+    launch_cfg<T, TO, KC, BMR, NS, HAS_R, LN, HAS_A2>(a, stream);
 }
 
 template <typename T, typename TO, int KC>
 void launch_k(const GemmArgs& a, hipStream_t stream) {
     const bool r = a.R != nullptr, ln = a.ln_g != nullptr;
-    // LDS per workgroup <= 80 KiB (two per CU): A 16 KiB + R 16 KiB per 32-row tile at
-    // K = 256; the LayerNorm epilogue at K = 256 needs 16-row tiles to stay in 256 VGPRs
-    constexpr int BL = KC == 8 ? 16 : 32;
     if (a.A2 != nullptr) {
         // the query + position-embedding projections (no residual / LayerNorm there)
         if (r || ln) return;
-        launch_cfg<T, TO, KC, 32, 2, false, false, true>(a, stream);
-    } else if (r && ln) launch_cfg<T, TO, KC, BL, 4, true, true>(a, stream);
-    else if (r) launch_cfg<T, TO, KC, 32, 2, true, false>(a, stream);
-    else if (ln) launch_cfg<T, TO, KC, BL, 4, false, true>(a, stream);
-    else launch_cfg<T, TO, KC, 32, 4, false, false>(a, stream);
+        launch_ring<T, TO, KC, false, false, true>(a, stream);
+    } else if (r && ln) launch_ring<T, TO, KC, true, true, false>(a, stream);
+    else if (r) launch_ring<T, TO, KC, true, false, false>(a, stream);
+    else if (ln) launch_ring<T, TO, KC, false, true, false>(a, stream);
+    else launch_ring<T, TO, KC, false, false, false>(a, stream);
 }
 
 template <typename T, typename TO>
@@ -380,14 +473,40 @@ bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t strea
     if (o16 ? (a.ldc % 8 != 0) : (a.ldc % 4 != 0)) return false;
     if (!al16(a.C) || (a.R != nullptr && (!o16 || a.ldr % 8 != 0 || !al16(a.R)))) return false;
     if (a.hm_rows && a.hm_d % 8 != 0) return false;
+    // output descriptor extent (buffer stores; offsets must stay below 2^31)
+    const long long osz = out_dtype == KINET_F32 ? 4 : 2;
+    const long long cb = a.hm_rows ? (long long)a.M * a.N * osz
+                                   : (a.M > 0 ? ((long long)(a.M - 1) * a.ldc + a.N) * osz : 0);
+    if (cb >= (1LL << 31)) return false;
+    GemmArgs ac = a;
+    ac.c_bytes = (int)cb;
     if (in_dtype == KINET_BF16) {
-        if (out_dtype == KINET_F16) launch_t<bf16_t, f16_t>(a, stream);
-        else if (o16) launch_t<bf16_t, bf16_t>(a, stream);
-        else launch_t<bf16_t, float>(a, stream);
+        if (out_dtype == KINET_F16) launch_t<bf16_t, f16_t>(ac, stream);
+        else if (o16) launch_t<bf16_t, bf16_t>(ac, stream);
+        else launch_t<bf16_t, float>(ac, stream);
     } else {
-        if (o16) launch_t<f16_t, f16_t>(a, stream);
-        else launch_t<f16_t, float>(a, stream);
+        if (o16) launch_t<f16_t, f16_t>(ac, stream);
+        else launch_t<f16_t, float>(ac, stream);
     }
+    return true;
+}
+
+// Entry from gemm.hip's conv dispatcher: the KH x 1, horizontally stride-1 unpadded conv of
+// the tap-folded stem (K = KH*Cin <= 256) as a resident-weight stream with the conv-row gather
+// (a short-K conv in the tiled kernel exposes a full load latency per 3-step tile); false
+// leaves the call to the tiled kernel.
+bool launch_rw_conv(const GemmArgs& a, int in_dtype, hipStream_t stream) {
+    if (in_dtype != KINET_BF16 && in_dtype != KINET_F16) return false;
+    if (a.M < rw_min_m || a.K > 256 || a.KW != 1 || a.stride_w != 1 || a.pad_w != 0 || a.Win != a.Wout) return false;
+    if (a.Cin % 8 != 0 || a.Wout < 32 || a.N > 128 || a.N % 8 != 0 || a.R != nullptr || a.ln_g != nullptr) return false;
+    if (a.ldc % 8 != 0 || !al16(a.C) || a.row_mask != nullptr) return false;
+    const long long cb = ((long long)(a.M - 1) * a.ldc + a.N) * 2;
+    if (cb >= (1LL << 31)) return false;
+    GemmArgs ac = a;
+    ac.c_bytes = (int)cb;
+    constexpr int NS = ring_depth<8, 32, false, false, false>();
+    if (in_dtype == KINET_BF16) launch_cfg<bf16_t, bf16_t, 8, 32, NS, false, false, false, 2, true>(ac, stream);
+    else launch_cfg<f16_t, f16_t, 8, 32, NS, false, false, false, 2, true>(ac, stream);
     return true;
 }
 

@@ -243,14 +243,28 @@ def pack_conv_weight(w, dtype, cin_pad=None):
     return cached(w, ('conv', dtype, cin_pad), make)
 
 
+def pack_stem_weight(w, dtype, cg):
+    """OIHW (Cout, 3, KH, KW) -> (Cout, KH, 1, cg) with w'[o][kh][0][kw*3 + c] = w[o][c][kh][kw]:
+    the weights of the tap-folded stem convolution over pack_image_kwfold's layout."""
+    def make(t):
+        o, i, kh, kw = t.shape
+        p = t.detach().permute(0, 2, 3, 1).reshape(o, kh, 1, kw * i)
+        p = torch.nn.functional.pad(p, (0, cg - kw * i))
+        return p.to(dtype).contiguous()
+    return cached(w, ('stem', dtype, cg), make)
+
+
 def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, residual=None, out=None, ksplit=None):
-    """x (B, H, W, Cin) NHWC contiguous; w_packed (Cout, KH, KW, Cin); returns (B, Ho, Wo, Cout)."""
+    """x (B, H, W, Cin) NHWC contiguous; w_packed (Cout, KH, KW, Cin); returns (B, Ho, Wo, Cout).
+    stride / pad: int or (vertical, horizontal)."""
     B, H, W, Cin = x.shape
     Cout, KH, KW, Cin2 = w_packed.shape
     if Cin2 != Cin:
         raise RuntimeError(f'conv2d: weight Cin {Cin2} != input Cin {Cin}')
-    Ho = (H + 2 * pad - KH) // stride + 1
-    Wo = (W + 2 * pad - KW) // stride + 1
+    sh, sw = (stride, stride) if isinstance(stride, int) else stride
+    ph, pw = (pad, pad) if isinstance(pad, int) else pad
+    Ho = (H + 2 * ph - KH) // sh + 1
+    Wo = (W + 2 * pw - KW) // sw + 1
     if out is None:
         out = torch.empty((B, Ho, Wo, Cout), dtype=x.dtype, device=x.device)
     ldy = out.stride(2) if out.dim() == 4 else out.stride(-2)
@@ -259,10 +273,16 @@ def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, res
         r = residual
     e = x.element_size()
     work = {'family': 'conv', 'flops': 2.0 * B * Ho * Wo * Cout * KH * KW * Cin,
-            'shape': (B, H, W, Cin, Cout, KH, stride),
+            'shape': (B, H, W, Cin, Cout, KH, sh),
             'bytes': (B * H * W * Cin + Cout * KH * KW * Cin + B * Ho * Wo * Cout * (2 if r is not None else 1)) * e}
-    args = (N.ptr(x), N.ptr(w_packed), N.ptr(out), B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-            N.dtype_code(x.dtype), N.ptr(scale), N.ptr(bias), N.ptr(r), Cout if r is not None else 0, int(relu), ldy)
+    tail = (N.dtype_code(x.dtype), N.ptr(scale), N.ptr(bias), N.ptr(r), Cout if r is not None else 0, int(relu), ldy)
+    if sh != sw or ph != pw:
+        if ksplit not in (None, 1):
+            raise RuntimeError('conv2d: split-K needs equal strides / pads')
+        N.call('kinet_conv2d_ex', N.ptr(x), N.ptr(w_packed), N.ptr(out), B, H, W, Cin, Ho, Wo, Cout, KH, KW,
+               sh, sw, ph, pw, *tail, N.stream(x.device), work=work)
+        return out
+    args = (N.ptr(x), N.ptr(w_packed), N.ptr(out), B, H, W, Cin, Ho, Wo, Cout, KH, KW, sh, ph) + tail
     ks = ksplit_for(B * Ho * Wo, Cout, KH * KW * Cin) if ksplit is None else ksplit
     if ks > 1:
         ws = torch.empty(ks * B * Ho * Wo * Cout, dtype=torch.float32, device=x.device)
@@ -288,6 +308,20 @@ def pack_image(img, dtype, cpad=8):
         raise RuntimeError('pack_image expects 3-channel images')
     y = torch.empty((B, H, W, cpad), dtype=dtype, device=img.device)
     N.call('kinet_pack_image_nhwc', N.ptr(img), N.ptr(y), B, H, W, cpad, N.dtype_code(dtype), N.stream(img.device))
+    return y
+
+
+def pack_image_kwfold(img, dtype, kw, stride, pad, cg):
+    """(B, 3, H, W) f32 NCHW -> (B, H, Wo, cg) with the kw horizontal taps of a stride-`stride`
+    filter folded into channels (kinet_pack_image_kwfold)."""
+    img = img.float().contiguous()
+    B, C, H, W = img.shape
+    if C != 3:
+        raise RuntimeError('pack_image_kwfold expects 3-channel images')
+    Wo = (W + 2 * pad - kw) // stride + 1
+    y = torch.empty((B, H, Wo, cg), dtype=dtype, device=img.device)
+    N.call('kinet_pack_image_kwfold', N.ptr(img), N.ptr(y), B, H, W, kw, stride, pad, cg, N.dtype_code(dtype),
+           N.stream(img.device), work={'family': 'kinet_pack_image_kwfold'})
     return y
 
 

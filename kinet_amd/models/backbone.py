@@ -120,8 +120,16 @@ class ResNetBody(nn.Module):
 
     def forward_nhwc(self, img_nchw, dtype):
         """img (B, 3, H, W) f32 -> [layer1, layer2, layer3, layer4] NHWC in dtype."""
-        x = K.pack_image(img_nchw, dtype, 8)
-        x = conv_bn(x, self.conv1, self.bn1, True, cin_pad=8)
+        # stem (torchvision conv1 7x7/2 + FrozenBN + ReLU): the 7 horizontal taps are folded
+        # into 24 channels while packing the image, so the conv runs as 7x1 with strides
+        # (2, 1): K = 7*24 = 168 instead of 7*7*8 = 392 (kinet_pack_image_kwfold)
+        c1 = self.conv1
+        kh, kw = c1.kernel_size
+        cg = (3 * kw + 7) // 8 * 8
+        x = K.pack_image_kwfold(img_nchw, dtype, kw, c1.stride[1], c1.padding[1], cg)
+        scale, bias = self.bn1.folded()
+        x = K.conv2d_nhwc(x, K.pack_stem_weight(c1.weight, dtype, cg), (c1.stride[0], 1), (c1.padding[0], 0),
+                          scale=scale, bias=bias, relu=True)
         x = K.maxpool_3x3s2(x)
         outs = []
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):

@@ -78,6 +78,46 @@ def test_stem_packed_image(K):
     assert _rel(mp.permute(0, 3, 1, 2), F.max_pool2d(ref, 3, 2, 1)) < 1e-6
 
 
+@pytest.mark.parametrize('H,W', [(50, 66), (37, 41), (800, 1333)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16, torch.float32])
+def test_stem_kwfold(K, H, W, dtype):
+    """Tap-folded stem: the packed layout is exactly the strided horizontal unfold of the
+    image, and the 7x1 (2, 1)-strided conv over it equals torchvision's 7x7/2 conv1."""
+    g = torch.Generator().manual_seed(H + W)
+    B = 2 if H < 800 else 1
+    img = torch.randn(B, 3, H, W, generator=g)
+    w = torch.randn(64, 3, 7, 7, generator=g) * 0.1
+    scale = torch.rand(64, generator=g) + 0.5
+    bias = torch.randn(64, generator=g) * 0.1
+    xp = K.pack_image_kwfold(img.cuda(), dtype, 7, 2, 3, 24)
+    Wo = (W + 6 - 7) // 2 + 1
+    assert xp.shape == (B, H, Wo, 24)
+    # expected fold: column ow holds x[c][h][2*ow - 3 + kw] at channel kw*3 + c
+    pad = F.pad(img, (3, 3))
+    cols = torch.stack([pad[..., kw: kw + 2 * (Wo - 1) + 1: 2] for kw in range(7)], -1)   # (B, 3, H, Wo, 7)
+    exp = torch.zeros(B, H, Wo, 24)
+    exp[..., :21] = cols.permute(0, 2, 3, 4, 1).reshape(B, H, Wo, 21)
+    assert torch.equal(xp.cpu(), exp.to(dtype))
+    y = K.conv2d_nhwc(xp, K.pack_stem_weight(w.cuda(), dtype, 24), (2, 1), (3, 0), scale=scale.cuda(),
+                      bias=bias.cuda(), relu=True)
+    ref = F.relu(F.conv2d(img, w, stride=2, padding=3) * scale[None, :, None, None] + bias[None, :, None, None])
+    torch.cuda.synchronize()
+    assert y.shape == (B, (H - 1) // 2 + 1, Wo, 64)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < (2e-5 if dtype == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize('k,s,p', [((3, 1), (2, 1), (1, 0)), ((5, 1), (1, 1), (2, 0)), ((1, 3), (1, 2), (0, 1))])
+def test_conv2d_asymmetric_stride_pad(K, k, s, p):
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 16, 23, 29, generator=g)
+    w = torch.randn(48, 16, k[0], k[1], generator=g) * 0.2
+    ref = F.conv2d(x, w, stride=s, padding=p)
+    y = K.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().cuda().bfloat16(), K.pack_conv_weight(w.cuda(), torch.bfloat16),
+                      s, p)
+    torch.cuda.synchronize()
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 2e-2
+
+
 @pytest.mark.parametrize('d', [256, 288])
 def test_layernorm(K, d):
     x = torch.randn(777, d)
