@@ -150,9 +150,10 @@ __global__ __launch_bounds__(WAVES * 64) void ffn_fused_kernel(const FfnArgs p, 
             }
         }
     };
-    // global chunk q of this workgroup -> ring slot q % NS; wave w moves fragments w, w+WAVES, ..
-    auto dma_chunk = [&](int q) {
-        const int c = q % nch;
+    // global chunk q of this workgroup (hidden chunk c = q mod nch, passed in: a runtime
+    // modulo is a ~20-instruction scalar division) -> ring slot q % NS; wave w moves
+    // fragments w, w+WAVES, ..
+    auto dma_chunk = [&](int q, int c) {
         char* dst = ring + (q % NS) * G::CHUNK;
         const unsigned src = (unsigned)c * (unsigned)G::CHUNK + (unsigned)lane * 16u;
 #pragma unroll
@@ -161,20 +162,21 @@ __global__ __launch_bounds__(WAVES * 64) void ffn_fused_kernel(const FfnArgs p, 
             dma16(rw, dst + f * 1024, src + (unsigned)f * 1024u);
         }
     };
-    // VMEM ops a wave issues in chunk iteration q AFTER that iteration's DMA (x prefetch,
-    // epilogue stores): they are younger than the DMA of chunks q+2 and q+1
-    auto extra = [&](int q) {
-        if (q < 0) return 0;
-        const int c = q % nch, ti = q / nch;
-        return ((c == pfi && ti + 1 < cnt) ? XN : 0) + (c == nch - 1 ? NST : 0);
+    // VMEM ops a wave issues in chunk iteration (tile t, chunk c) AFTER that iteration's DMA
+    // (x prefetch, epilogue stores): they are younger than the DMA of the next two chunks.
+    // Every per-chunk index here is wave-uniform scalar work shared by all waves of the CU
+    // (one SALU issue per cycle per CU), so no divisions: the caller steps (t, c) back itself.
+    auto extra = [&](int c, int t) {
+        if (t < 0) return 0;
+        return ((c == pfi && t + 1 < cnt) ? XN : 0) + (c == nch - 1 ? NST : 0);
     };
 
     u32x4 xr[RT][KS], xn[RT][KS];
     load_x(bx, xr);
     __syncthreads();   // parameters in LDS (drains the x loads too: nothing else in flight yet)
     const int total = cnt * nch;
-    dma_chunk(0);
-    if (total > 1) dma_chunk(1);
+    dma_chunk(0, 0);
+    if (total > 1) dma_chunk(1, nch > 1 ? 1 : 0);
 
     f32x4 acc[RT][NT];
     constexpr int PB = 4;                      // W2 fragments read ahead of phase B
@@ -228,7 +230,11 @@ __global__ __launch_bounds__(WAVES * 64) void ffn_fused_kernel(const FfnArgs p, 
         const int q = ti * nch + c;
         // retire chunk q: still allowed in flight = everything issued after its DMA
         if (q + 1 < total) {
-            const int e = extra(q - 2) + extra(q - 1);
+            int c1 = c - 1, t1 = ti, c2 = c - 2, t2 = ti;
+            if (c1 < 0) { c1 += nch; --t1; }
+            if (c2 < 0) { c2 += nch; --t2; }
+            if (c2 < 0) { c2 += nch; --t2; }   // nch == 1
+            const int e = extra(c2, t2) + extra(c1, t1);
             if (p.dbg & 1) ffn_wait_vmcnt<0>();
             else if (e == 0) ffn_wait_vmcnt<FRW>();
             else ffn_wait_vmcnt<FRW + XN>();   // XN == NST; e == 2 XN only waits more
@@ -236,7 +242,12 @@ __global__ __launch_bounds__(WAVES * 64) void ffn_fused_kernel(const FfnArgs p, 
             ffn_wait_vmcnt<0>();
         }
         ffn_lds_barrier();     // chunk q visible to all; slot (q+2)%NS free (chunk q-2 done)
-        if (q + 2 < total && !(p.dbg & 1)) dma_chunk(q + 2);
+        if (q + 2 < total && !(p.dbg & 1)) {
+            int cn = c + 2;
+            if (cn >= nch) cn -= nch;
+            if (cn >= nch) cn -= nch;       // nch == 1
+            dma_chunk(q + 2, cn);
+        }
         if (c == pfi && ti + 1 < cnt) load_x(bx + (ti + 1) * P, xn);
         const char* wb = ring + (q % NS) * G::CHUNK;
         const bool pipe = c > 0;

@@ -37,7 +37,8 @@ namespace {
 
 // diagnostic kernel-selection flags (kinet_gemm_set_flags): bit 1 = allow gemm_big_kernel
 // (measured slower than gemm_kernel on every detector shape, DESIGN.md, so off by default);
-// bit 2 = never use the resident-weight kernel (gemm_rw.hip); bit 4 = LDS-DMA gemm_dma_kernel
+// bit 2 = never use the resident-weight kernel (gemm_rw.hip); bit 4 = LDS-DMA gemm_dma_kernel;
+// bit 32 = never use the dedicated stem convolution (stem.hip)
 int kinet_gemm_flags = 0;
 // diagnostic tile override for gemm_kernel (kinet_gemm_force_tile; 0 = heuristic)
 int force_bm = 0, force_bn = 0;
@@ -672,6 +673,10 @@ int launch(const GemmArgs& a, hipStream_t stream) {
 template <bool CONV>
 int dispatch(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t s) {
     if (!CONV && a.kchunk == 0 && !(kinet_gemm_flags & 4) && launch_rw(a, in_dtype, out_dtype, s)) {
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
+    if (CONV && !(kinet_gemm_flags & 32) && out_dtype == in_dtype && launch_stem_conv(a, in_dtype, s)) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;
     }

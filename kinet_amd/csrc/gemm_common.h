@@ -41,6 +41,9 @@ struct GemmArgs {
 bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t stream);
 // gemm_rw.hip: the tap-folded stem convolution (conv-row gather); false = not eligible
 bool launch_rw_conv(const GemmArgs& a, int in_dtype, hipStream_t stream);
+// stem.hip: the tap-folded ResNet stem convolution (7x1, strides (2, 1), 24 -> 64 channels)
+// with its input rows shared through LDS; false = not that geometry
+bool launch_stem_conv(const GemmArgs& a, int dtype, hipStream_t stream);
 extern int rw_min_m;
 
 namespace {

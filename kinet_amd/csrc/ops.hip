@@ -197,7 +197,7 @@ __global__ void pack_image_kernel(const float* __restrict__ x, T* __restrict__ y
 // with stride (s, 1) over Cg channels: K = KH*Cg (7*24 = 168) instead of KH*KW*8 = 392 for
 // the 8-channel-padded image -- 2.3x fewer MFMA flops in ResNet's 7x7 stem (backbone.py:
 // torchvision conv1).
-constexpr int kFoldPx = 128;    // output pixels per workgroup of pack_image_kwfold_kernel
+constexpr int kFoldPx = 672;    // output pixels per workgroup of pack_image_kwfold_kernel (a 1333-wide image row)
 
 template <typename T>
 __global__ __launch_bounds__(256) void pack_image_kwfold_kernel(const float* __restrict__ x, T* __restrict__ y, int H,

@@ -23,9 +23,11 @@ def main():
     t = timeit(lambda: K.pack_image(img, dt, 8), iters=10)
     print(f'pack_image (8 ch): {t * 1e3:.1f} us')
     wp = K.pack_stem_weight(w, dt, 24)
-    t = timeit(lambda: K.conv2d_nhwc(xp, wp, (2, 1), (3, 0), scale=scale, bias=bias, relu=True), iters=10)
-    print(f'folded conv, default dispatch (resident-weight conv-row kernel): {t * 1e3:.1f} us')
-    L.kinet_gemm_set_flags(4)   # tiled kernel only
+    for flags, what in [(0, 'stem kernel (stem.hip)'), (32, 'resident-weight conv-row kernel')]:
+        L.kinet_gemm_set_flags(flags)
+        t = timeit(lambda: K.conv2d_nhwc(xp, wp, (2, 1), (3, 0), scale=scale, bias=bias, relu=True), iters=10)
+        print(f'folded conv, {what}: {t * 1e3:.1f} us')
+    L.kinet_gemm_set_flags(32 | 4)   # tiled kernel only
     for bm, bn in [(0, 0), (128, 64), (64, 64)]:
         L.kinet_gemm_force_tile(bm, bn)
         t = timeit(lambda: K.conv2d_nhwc(xp, wp, (2, 1), (3, 0), scale=scale, bias=bias, relu=True), iters=10)
