@@ -113,6 +113,69 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, 
     }
 }
 
+// 16-byte vector forms (C and C/groups multiples of V = 16/sizeof(T)): a thread owns V
+// consecutive channels (one group), 16-byte loads and stores, 32-bit index math.
+template <typename T>
+__global__ __launch_bounds__(256) void gn_stats_vec_kernel(const T* __restrict__ x, float* __restrict__ stats, int HW,
+                                                           int C, int groups, int pix_per_block) {
+    constexpr int V = 16 / (int)sizeof(T);
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    extern __shared__ float red[];   // [groups][2]
+    const int n = blockIdx.y;
+    const int p0 = blockIdx.x * pix_per_block;
+    const int p1 = min(HW, p0 + pix_per_block);
+    for (int i = threadIdx.x; i < 2 * groups; i += blockDim.x) red[i] = 0.f;
+    __syncthreads();
+    const int CV = C / V, nslot = 256 / CV;
+    const int cv = threadIdx.x % CV, slot = threadIdx.x / CV;
+    if (slot < nslot) {
+        float s = 0.f, q = 0.f;
+        const T* xb = x + (long)n * HW * C + cv * V;
+        for (int p = p0 + slot; p < p1; p += nslot) {
+            const u4 v = *reinterpret_cast<const u4*>(xb + (long)p * C);
+            const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const float t = to_f32(e[j]);
+                s += t;
+                q += t * t;
+            }
+        }
+        const int grp = cv * V / (C / groups);
+        atomicAdd(&red[2 * grp], s);
+        atomicAdd(&red[2 * grp + 1], q);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * groups; i += blockDim.x) atomicAdd(&stats[(long)n * 2 * groups + i], red[i]);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gn_apply_vec_kernel(const T* __restrict__ x, const float* __restrict__ stats,
+                                                           const float* __restrict__ g, const float* __restrict__ b,
+                                                           T* __restrict__ y, int HW, int C, int groups, long y_bs,
+                                                           float eps) {
+    // grid (ceil(HW*C/V / 256), N)
+    constexpr int V = 16 / (int)sizeof(T);
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const int n = blockIdx.y;
+    const int CV = C / V;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= HW * CV) return;
+    const int p = i / CV, c0 = (i - p * CV) * V;
+    const int cpg = C / groups, grp = c0 / cpg;
+    const float cnt = (float)HW * cpg;
+    const float mean = stats[(long)n * 2 * groups + 2 * grp] / cnt;
+    const float var = fmaxf(stats[(long)n * 2 * groups + 2 * grp + 1] / cnt - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + eps);
+    const u4 v = *reinterpret_cast<const u4*>(x + ((long)n * HW + p) * C + c0);
+    const T* e = reinterpret_cast<const T*>(&v);
+    u4 o;
+    T* oe = reinterpret_cast<T*>(&o);
+#pragma unroll
+    for (int j = 0; j < V; ++j) st(oe + j, (to_f32(e[j]) - mean) * rstd * g[c0 + j] + b[c0 + j]);
+    *reinterpret_cast<u4*>(y + (long)n * y_bs + (long)p * C + c0) = o;
+}
+
 // ---------------------------------------------------------------------------------
 // max-pool 3x3 stride 2 pad 1 (NHWC)
 // ---------------------------------------------------------------------------------
@@ -407,6 +470,28 @@ extern "C" int kinet_groupnorm(const void* x, const float* gamma, const float* b
     if (N == 0) return KINET_OK;
     hipStream_t s = (hipStream_t)stream;
     KINET_CHECK_HIP(hipMemsetAsync(stats, 0, (size_t)2 * N * groups * sizeof(float), s));
+    // 16-byte vector path: bf16 / f16 / f32, whole vectors per group, aligned rows
+    const int V = dtype == KINET_F32 ? 4 : 8;
+    const bool vec = dtype != KINET_F64 && C % V == 0 && (C / groups) % V == 0 && C / V <= 256 &&
+                     y_batch_stride % V == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0 &&
+                     (long)HW * (C / V) < (1L << 31) && N <= 65535;
+    if (vec) {
+        const int ppb = 128;
+        const dim3 g1((HW + ppb - 1) / ppb, N), g2((unsigned)(((long)HW * (C / V) + 255) / 256), N);
+#define GNV(TT)                                                                                                  \
+    do {                                                                                                         \
+        hipLaunchKernelGGL((gn_stats_vec_kernel<TT>), g1, dim3(256), 2 * groups * sizeof(float), s, (const TT*)x, \
+                           stats, HW, C, groups, ppb);                                                           \
+        hipLaunchKernelGGL((gn_apply_vec_kernel<TT>), g2, dim3(256), 0, s, (const TT*)x, stats, gamma, beta,     \
+                           (TT*)y, HW, C, groups, (long)y_batch_stride, eps);                                    \
+    } while (0)
+        if (dtype == KINET_BF16) GNV(bf16_t);
+        else if (dtype == KINET_F16) GNV(f16_t);
+        else GNV(float);
+#undef GNV
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
     const int ppb = 64;
     dim3 g1((HW + ppb - 1) / ppb, N);
     DISPATCH_T(dtype, hipLaunchKernelGGL((gn_stats_kernel<T>), g1, dim3(256), 2 * groups * sizeof(float), s,
