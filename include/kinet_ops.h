@@ -51,6 +51,11 @@ int kinet_mha_core(const void* Q, int ldq, const void* Kt, int ldk, const void* 
                    void* O, int ldo, int batch, int Lq, int Lk, int heads, int head_dim,
                    float scale, int dtype, const uint8_t* key_mask, kinet_stream_t stream);
 
+/* Diagnostic knob (no reference counterpart): 1 (default) = kinet_mha_core runs head_dim 32,
+ * bf16/f16, Lk <= 384 on the MFMA kernel (attn.hip), 0 = always the FMA kernel.  Returns the
+ * previous setting. */
+int kinet_mha_set_mfma(int enable);
+
 /* Iterative box refinement (deformable_transformer.py:414-425) fused with the next
  * layer's reference input (:406-411):
  *   new_ref = sigmoid(tmp + inverse_sigmoid(ref))        (ref_dim 4)

@@ -41,6 +41,7 @@ _SIGS = {
     'kinet_maxpool2d_3x3s2': [P, P] + [I] * 5 + [P],
     'kinet_pack_image_nhwc': [P, P] + [I] * 5 + [P],
     'kinet_pack_image_kwfold': [P, P] + [I] * 8 + [P],
+    'kinet_mha_set_mfma': [I],
     'kinet_mha_core': [P, I, P, I, P, I, P, I] + [I] * 5 + [F, I, P, P],
     'kinet_add': [P, P, P, I64, I, P],
     'kinet_box_refine': [P, P, I, P, P, P, I, I, I, P],

@@ -572,6 +572,20 @@ extern "C" int kinet_add(const void* a, const void* b, void* y, int64_t n, int d
     return KINET_OK;
 }
 
+namespace kinet {
+// attn.hip: the MFMA kernel for head_dim 32, 16-bit, Lk <= 384 (false = not covered)
+bool launch_mha_mfma(const void* Q, int ldq, const void* Kt, int ldk, const void* V, int ldv, void* O, int ldo,
+                     int batch, int Lq, int Lk, int heads, int head_dim, float scale, int dtype,
+                     const uint8_t* key_mask, hipStream_t stream);
+int mha_use_mfma = 1;
+}  // namespace kinet
+
+extern "C" int kinet_mha_set_mfma(int enable) {
+    const int old = kinet::mha_use_mfma;
+    kinet::mha_use_mfma = enable;
+    return old;
+}
+
 extern "C" int kinet_mha_core(const void* Q, int ldq, const void* Kt, int ldk, const void* V, int ldv, void* O, int ldo,
                               int batch, int Lq, int Lk, int heads, int head_dim, float scale, int dtype,
                               const uint8_t* key_mask, kinet_stream_t stream) {
@@ -579,8 +593,13 @@ extern "C" int kinet_mha_core(const void* Q, int ldq, const void* Kt, int ldk, c
     KINET_CHECK_ARG(head_dim == 32 || head_dim == 36 || head_dim == 16 || head_dim == 64,
                     "mha: head_dim %d not instantiated (16/32/36/64)", head_dim);
     if (batch == 0 || Lq == 0) return KINET_OK;
-    dim3 grid((Lq + 15) / 16, heads, batch);
     hipStream_t s = (hipStream_t)stream;
+    if (kinet::mha_use_mfma && kinet::launch_mha_mfma(Q, ldq, Kt, ldk, V, ldv, O, ldo, batch, Lq, Lk, heads, head_dim,
+                                                      scale, dtype, key_mask, s)) {
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
+    dim3 grid((Lq + 15) / 16, heads, batch);
 #define MH(DD) DISPATCH_T(dtype, hipLaunchKernelGGL((mha_kernel<T, DD>), grid, dim3(256), 0, s, (const T*)Q, ldq, \
                                                    (const T*)Kt, ldk, (const T*)V, ldv, (T*)O, ldo, Lq, Lk, heads, \
                                                    scale, key_mask))

@@ -156,6 +156,36 @@ def test_mha_core(K, D, Lq):
     assert _rel(y, ref) < 1e-5
 
 
+@pytest.mark.parametrize('Lq,Lk', [(300, 300), (57, 333), (130, 37)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_mha_core_mfma(K, Lq, Lk, dtype):
+    """head_dim 32, 16-bit: the MFMA kernel (attn.hip) vs fp32 SDPA with a key padding mask,
+    and vs the FMA kernel on the same 16-bit inputs."""
+    from kinet_amd import _native
+    heads, B, D = 8, 3, 32
+    E = heads * D
+    g = torch.Generator().manual_seed(Lq + Lk)
+    q, k, v = (torch.randn(B, n, E, generator=g).to(dtype) for n in (Lq, Lk, Lk))
+    mask = torch.rand(B, Lk, generator=g) < 0.2
+    mask[:, 0] = False
+
+    def split(t, n):
+        return t.float().view(B, n, heads, D).transpose(1, 2)
+    ref = F.scaled_dot_product_attention(split(q, Lq), split(k, Lk), split(v, Lk),
+                                         attn_mask=~mask[:, None, None, :]).transpose(1, 2).reshape(B, Lq, E)
+    y = K.mha_core(q.cuda(), k.cuda(), v.cuda(), heads, D ** -0.5, key_mask=mask.cuda())
+    lib = _native.lib()
+    old = lib.kinet_mha_set_mfma(0)
+    try:
+        y_fma = K.mha_core(q.cuda(), k.cuda(), v.cuda(), heads, D ** -0.5, key_mask=mask.cuda())
+    finally:
+        lib.kinet_mha_set_mfma(old)
+    torch.cuda.synchronize()
+    tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
+    assert _rel(y, ref) < tol
+    assert _rel(y, y_fma) < tol
+
+
 # ---- the 512-thread LDS-DMA kernel (M >= 16384, N >= 128, 16-bit operands) ----------------
 
 @pytest.fixture
