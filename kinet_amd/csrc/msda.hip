@@ -482,6 +482,27 @@ struct FastLevels {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
+// acc += f16(half of x) * f16(half of w) in f32 (both multiplicands 16-bit sources)
+__device__ __forceinline__ float fma_mix16_lo_lo(float acc, uint32_t x, uint32_t w) {
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(x), "v"(w));
+    return acc;
+}
+__device__ __forceinline__ float fma_mix16_lo_hi(float acc, uint32_t x, uint32_t w) {
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(x), "v"(w));
+    return acc;
+}
+__device__ __forceinline__ float fma_mix16_hi_lo(float acc, uint32_t x, uint32_t w) {
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(x), "v"(w));
+    return acc;
+}
+__device__ __forceinline__ float fma_mix16_hi_hi(float acc, uint32_t x, uint32_t w) {
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(x), "v"(w));
+    return acc;
+}
+__device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (f16_t)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (f16_t)b) << 16);
+}
+
 // acc += f16(lo or hi half of x) * w in f32 -- one v_fma_mix_f32, no separate widening
 __device__ __forceinline__ float fma_mix_lo(float acc, uint32_t x, float w) {
     asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(x), "v"(w));
@@ -513,7 +534,12 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
     constexpr int NSB = MH * QT * LP;               // samples per workgroup
     constexpr unsigned OOB = 0x80000000u;
     __shared__ FastLevels lv;
-    __shared__ Tap4 taps[NSB];
+    // per-sample tap records, split so phase 2 reads the offsets before its gathers and the
+    // weights only after them: 4 byte offsets (16 B) + 4 weights as f16 (8 B; v_fma_mix takes
+    // them as a 16-bit source directly) -- 24 KiB per workgroup instead of 32, so the LDS no
+    // longer caps residency below the register limit
+    __shared__ int4 toff[NSB];
+    __shared__ uint2 twt[NSB];
     // XCD-aware remap (bijective, cdna_hip_programming.md T1): workgroups are dealt to the 8
     // XCDs round-robin by linear id; give each XCD a contiguous run of query tiles of one
     // (frame, head group) so neighbouring queries -- which sample overlapping value
@@ -610,7 +636,8 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
                 t4.w[3] = lh * lw * a;
             }
         }
-        taps[s] = t4;
+        toff[s] = make_int4(t4.off[0], t4.off[1], t4.off[2], t4.off[3]);
+        twt[s] = make_uint2(pack_f16x2(t4.w[0], t4.w[1]), pack_f16x2(t4.w[2], t4.w[3]));
     }
     __syncthreads();
 
@@ -623,34 +650,40 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
     const unsigned cb = (unsigned)(lane & 3) * 16u;   // this lane's 8 channels, bytes
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(value + (long)b * vsb + (long)m * vsm), (short)0, head_bytes, 0x00020000);
-    const Tap4* tp = taps + (wave * QT + qi) * LP;
+    const int4* tpo = toff + (wave * QT + qi) * LP;
+    const uint2* tpw = twt + (wave * QT + qi) * LP;
     f32x2 acc[4] = {};
     constexpr int SG = 4;   // 4 samples x 4 corners = 16 gathers in flight per lane
 #pragma unroll 1
     for (int s = 0; s < LP; s += SG) {
-        Tap4 t[SG];
-#pragma unroll
-        for (int g = 0; g < SG; ++g) t[g] = tp[s + g];
         u32x4v v[SG][4];
 #pragma unroll
-        for (int g = 0; g < SG; ++g)
+        for (int g = 0; g < SG; ++g) {
+            const int4 o = tpo[s + g];
+            v[g][0] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.x + cb, 0, 0));
+            v[g][1] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.y + cb, 0, 0));
+            v[g][2] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.z + cb, 0, 0));
+            v[g][3] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.w + cb, 0, 0));
+        }
+        uint2 wq[SG];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                v[g][k] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)t[g].off[k] + cb, 0, 0));
+        for (int g = 0; g < SG; ++g) wq[g] = tpw[s + g];
 #pragma unroll
         for (int g = 0; g < SG; ++g)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
+                const uint32_t wp = k < 2 ? wq[g].x : wq[g].y;   // f16 weights of corners (k & ~1, k | 1)
                 if constexpr (std::is_same<T, f16_t>::value) {
-                    // f16 values: v_fma_mix_f32 reads each half directly (1 VALU per MAC)
+                    // f16 values x f16 weights, f32 accumulate: one v_fma_mix_f32 per MAC
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        acc[j][0] = fma_mix_lo(acc[j][0], v[g][k][j], t[g].w[k]);
-                        acc[j][1] = fma_mix_hi(acc[j][1], v[g][k][j], t[g].w[k]);
+                        acc[j][0] = (k & 1) ? fma_mix16_lo_hi(acc[j][0], v[g][k][j], wp) : fma_mix16_lo_lo(acc[j][0], v[g][k][j], wp);
+                        acc[j][1] = (k & 1) ? fma_mix16_hi_hi(acc[j][1], v[g][k][j], wp) : fma_mix16_hi_lo(acc[j][1], v[g][k][j], wp);
                     }
                 } else {
                     // bf16 values: widen by shift / mask, then v_pk_fma_f32 (1.5 VALU per MAC)
-                    const f32x2 w2 = {t[g].w[k], t[g].w[k]};
+                    const float wk = (float)__builtin_bit_cast(f16_t, (uint16_t)((k & 1) ? (wp >> 16) : (wp & 0xffffu)));
+                    const f32x2 w2 = {wk, wk};
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         f32x2 x;
