@@ -33,7 +33,8 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxLevels = 16;
 
-// diagnostic flags (kinet_msda_set_flags): bit 0 = never use msda_fused_fast_kernel
+// diagnostic flags (kinet_msda_set_flags): bit 0 = never use msda_fused_fast_kernel; bit 1 = its
+// 4-head x 4-sample-group variant, bit 2 = 4 heads x 2 (the default is 2 heads x 2; timing studies)
 int msda_flags = 0;
 
 template <typename T, int VEC>
@@ -522,14 +523,15 @@ __device__ __forceinline__ void widen2(uint32_t u, f32x2& x) {
     }
 }
 
-template <typename T, typename TO, typename TL, int L, int P>
-__global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
+// MH heads (waves) per workgroup, SG samples gathered per group (SG x 4 loads in flight per lane)
+template <typename T, typename TO, typename TL, int L, int P, int MH = kThreads / 64, int SG = 4>
+__global__ __launch_bounds__(MH * 64) void msda_fused_fast_kernel(
     const T* __restrict__ value, long vsb, int vss, long vsm, int head_bytes, const int64_t* __restrict__ shapes,
     const TL* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
     const uint8_t* __restrict__ qmask, float* __restrict__ loc_out, float* __restrict__ attw_out,
     TO* __restrict__ out, int S, int M, int Lq, const int* __restrict__ torder) {
     static_assert(sizeof(T) == 2 && sizeof(TO) == 2, "16-bit values and output");
-    constexpr int D = 32, QT = 16, MH = kThreads / 64, LP = L * P;
+    constexpr int D = 32, QT = 16, LP = L * P, NT = MH * 64;
     static_assert((LP & (LP - 1)) == 0 && LP <= 64 && L <= kMaxLevels, "L*P: power of two <= 64");
     constexpr int NSB = MH * QT * LP;               // samples per workgroup
     constexpr unsigned OOB = 0x80000000u;
@@ -578,8 +580,8 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
 
     const int rowb = vss * (int)sizeof(T);           // bytes between pixels of one head map
 #pragma unroll
-    for (int i = 0; i < NSB / kThreads; ++i) {
-        const int s = threadIdx.x + kThreads * i;
+    for (int i = 0; i < NSB / NT; ++i) {
+        const int s = threadIdx.x + NT * i;
         const int ml = s / (QT * LP), qi = (s / LP) % QT, lp = s % LP, l = lp / P;
         const int m = mh0 + ml, q = q0 + qi;
         const bool ok = q < Lq && m < M;
@@ -653,7 +655,6 @@ __global__ __launch_bounds__(kThreads) void msda_fused_fast_kernel(
     const int4* tpo = toff + (wave * QT + qi) * LP;
     const uint2* tpw = twt + (wave * QT + qi) * LP;
     f32x2 acc[4] = {};
-    constexpr int SG = 4;   // 4 samples x 4 corners = 16 gathers in flight per lane
 #pragma unroll 1
     for (int s = 0; s < LP; s += SG) {
         u32x4v v[SG][4];
@@ -1016,7 +1017,19 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
         if (D == 32 && P == 4 && (L == 4 || L == 8) && vss % 8 == 0 && vsb % 8 == 0 && vsm % 8 == 0 &&
             ((uintptr_t)value % 16) == 0 && head_bytes < (1LL << 31) && !(msda_flags & 1)) {
             dim3 grid((Lq + 15) / 16, N, (M + 3) / 4);
-            if (L == 4)
+            if (L == 4 && !(msda_flags & 6)) {
+                // 2 heads (waves) per workgroup, 2 samples per gather group: 12.5 KiB LDS and
+                // 52 VGPRs, 12 workgroups per CU (encoder call 271 -> 258 us vs 4 heads x 4)
+                dim3 g2((Lq + 15) / 16, N, (M + 1) / 2);
+                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 4, 4, 2, 2>), g2, dim3(128), 0, stream,
+                                   (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v,
+                                   ld_off, ref, ref_dim, qmask, loc_out, attw_out, (TO*)out, S, M, Lq, torder);
+            } else if (L == 4 && (msda_flags & 4)) {
+                dim3 g2((Lq + 15) / 16, N, (M + 3) / 4);
+                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 4, 4, 4, 2>), g2, dim3(256), 0, stream,
+                                   (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v,
+                                   ld_off, ref, ref_dim, qmask, loc_out, attw_out, (TO*)out, S, M, Lq, torder);
+            } else if (L == 4)
                 hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 4, 4>), grid, dim3(kThreads), 0, stream,
                                    (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v, ld_off,
                                    ref, ref_dim, qmask, loc_out,
