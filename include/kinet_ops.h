@@ -19,7 +19,10 @@ int kinet_layernorm(const void* x, const void* r, const float* gamma, const floa
 /* nn.GroupNorm(groups, C) on NHWC input (deformable_detr.py:64, :70):
  * x (N, HW, C) contiguous; y written at y + n*y_batch_stride + p*C + c (so a level can land
  * inside the flattened multi-level src buffer, deformable_transformer.py:145-153).
- * `stats`: caller-provided scratch of 2*N*groups floats (zeroed by the call). */
+ * `stats`: caller-provided scratch of kinet_groupnorm_workspace(N, HW, C, groups, dtype) floats;
+ * its first 2*N*groups floats hold (sum, sumsq) per image x group on return.  Every reduction
+ * runs in a fixed order (no float atomics): reruns are bit-identical. */
+long kinet_groupnorm_workspace(int N, int HW, int C, int groups, int dtype);
 int kinet_groupnorm(const void* x, const float* gamma, const float* beta, void* y,
                     int N, int HW, int C, int groups, int y_batch_stride, float eps, int dtype,
                     float* stats, kinet_stream_t stream);

@@ -38,6 +38,7 @@ _SIGS = {
     'kinet_ffn_fused': [P, I, P, P, P, P, P, F, P, I, I, I, I, I, P],
     'kinet_layernorm': [P] * 5 + [I, I, F, I, I, P],
     'kinet_groupnorm': [P] * 4 + [I] * 5 + [F, I, P, P],
+    'kinet_groupnorm_workspace': [I] * 5,
     'kinet_maxpool2d_3x3s2': [P, P] + [I] * 5 + [P],
     'kinet_pack_image_nhwc': [P, P] + [I] * 5 + [P],
     'kinet_pack_image_kwfold': [P, P] + [I] * 8 + [P],
@@ -49,7 +50,8 @@ _SIGS = {
     'kinet_version': [],
 }
 _RESTYPES = {'kinet_last_error': ctypes.c_char_p, 'kinet_version': ctypes.c_char_p,
-             'kinet_msda_backward_workspace_bytes': ctypes.c_int64}
+             'kinet_msda_backward_workspace_bytes': ctypes.c_int64,
+             'kinet_groupnorm_workspace': ctypes.c_long}
 
 DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
 

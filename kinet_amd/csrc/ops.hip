@@ -65,19 +65,20 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const T* __restrict__ x,
 }
 
 // ---------------------------------------------------------------------------------
-// GroupNorm on NHWC: stats (sum, sumsq per image x group) then apply
+// GroupNorm on NHWC: per-block partial (sum, sumsq) per image x group, a fixed-order
+// finalize, then apply.  No float atomics anywhere: every reduction runs in a fixed order, so
+// reruns (and graph replays, and two batches in flight) are bit-identical.
+// Workspace (floats): stats [N][2*groups] then partials [N][nblk][2*groups].
 // ---------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x, float* __restrict__ stats, int HW,
+__global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x, float* __restrict__ part, int HW,
                                                        int C, int groups, int pix_per_block) {
-    // thread t sums channels t, t+256, ... over this block's pixel range (coalesced rows)
-    extern __shared__ float red[];   // [groups][2]
+    // thread t sums channels t, t+256, ... over this block's pixel range (coalesced rows); the
+    // per-channel sums are parked in LDS and each group summed in channel order
+    extern __shared__ float red[];   // [2][C]
     const int n = blockIdx.y;
     const int p0 = blockIdx.x * pix_per_block;
     const int p1 = min(HW, p0 + pix_per_block);
-    for (int i = threadIdx.x; i < 2 * groups; i += blockDim.x) red[i] = 0.f;
-    __syncthreads();
-    const int cpg = C / groups;
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
         float s = 0.f, q = 0.f;
         for (int p = p0; p < p1; ++p) {
@@ -85,11 +86,34 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x, 
             s += t;
             q += t * t;
         }
-        atomicAdd(&red[2 * (c / cpg)], s);
-        atomicAdd(&red[2 * (c / cpg) + 1], q);
+        red[c] = s;
+        red[C + c] = q;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 2 * groups; i += blockDim.x) atomicAdd(&stats[(long)n * 2 * groups + i], red[i]);
+    const int cpg = C / groups;
+    float* out = part + ((long)n * gridDim.x + blockIdx.x) * 2 * groups;
+    for (int g = threadIdx.x; g < groups; g += blockDim.x) {
+        float s = 0.f, q = 0.f;
+        for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+            s += red[c];
+            q += red[C + c];
+        }
+        out[2 * g] = s;
+        out[2 * g + 1] = q;
+    }
+}
+
+// stats[n][i] = sum over the nblk block partials of image n, in block order
+__global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restrict__ part, float* __restrict__ stats,
+                                                          int nblk, int groups) {
+    const int n = blockIdx.x;
+    const int w = 2 * groups;
+    for (int i = threadIdx.x; i < w; i += blockDim.x) {
+        const float* pp = part + (long)n * nblk * w + i;
+        float a = 0.f;
+        for (int b = 0; b < nblk; ++b) a += pp[(long)b * w];
+        stats[(long)n * w + i] = a;
+    }
 }
 
 template <typename T>
@@ -116,20 +140,18 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, 
 // 16-byte vector forms (C and C/groups multiples of V = 16/sizeof(T)): a thread owns V
 // consecutive channels (one group), 16-byte loads and stores, 32-bit index math.
 template <typename T>
-__global__ __launch_bounds__(256) void gn_stats_vec_kernel(const T* __restrict__ x, float* __restrict__ stats, int HW,
+__global__ __launch_bounds__(256) void gn_stats_vec_kernel(const T* __restrict__ x, float* __restrict__ part, int HW,
                                                            int C, int groups, int pix_per_block) {
     constexpr int V = 16 / (int)sizeof(T);
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    extern __shared__ float red[];   // [groups][2]
+    __shared__ float red[2][256];   // per-thread partials, summed per group in a fixed order
     const int n = blockIdx.y;
     const int p0 = blockIdx.x * pix_per_block;
     const int p1 = min(HW, p0 + pix_per_block);
-    for (int i = threadIdx.x; i < 2 * groups; i += blockDim.x) red[i] = 0.f;
-    __syncthreads();
     const int CV = C / V, nslot = 256 / CV;
     const int cv = threadIdx.x % CV, slot = threadIdx.x / CV;
+    float s = 0.f, q = 0.f;
     if (slot < nslot) {
-        float s = 0.f, q = 0.f;
         const T* xb = x + (long)n * HW * C + cv * V;
         for (int p = p0 + slot; p < p1; p += nslot) {
             const u4 v = *reinterpret_cast<const u4*>(xb + (long)p * C);
@@ -141,12 +163,22 @@ __global__ __launch_bounds__(256) void gn_stats_vec_kernel(const T* __restrict__
                 q += t * t;
             }
         }
-        const int grp = cv * V / (C / groups);
-        atomicAdd(&red[2 * grp], s);
-        atomicAdd(&red[2 * grp + 1], q);
     }
+    red[0][threadIdx.x] = s;
+    red[1][threadIdx.x] = q;
     __syncthreads();
-    for (int i = threadIdx.x; i < 2 * groups; i += blockDim.x) atomicAdd(&stats[(long)n * 2 * groups + i], red[i]);
+    const int vpg = C / groups / V;   // channel vectors per group
+    float* out = part + ((long)n * gridDim.x + blockIdx.x) * 2 * groups;
+    for (int g = threadIdx.x; g < groups; g += blockDim.x) {
+        float gs = 0.f, gq = 0.f;
+        for (int sl = 0; sl < nslot; ++sl)
+            for (int k = g * vpg; k < (g + 1) * vpg; ++k) {
+                gs += red[0][sl * CV + k];
+                gq += red[1][sl * CV + k];
+            }
+        out[2 * g] = gs;
+        out[2 * g + 1] = gq;
+    }
 }
 
 template <typename T>
@@ -461,27 +493,46 @@ extern "C" int kinet_layernorm(const void* x, const void* r, const float* gamma,
     return KINET_OK;
 }
 
+namespace {
+// pixels per stats block: 128 on the vector path, 64 on the scalar path
+bool gn_vec_ok(const void* x, const void* y, int HW, int C, int groups, int y_batch_stride, int N, int dtype) {
+    const int V = dtype == KINET_F32 ? 4 : 8;
+    return dtype != KINET_F64 && C % V == 0 && (C / groups) % V == 0 && C / V <= 256 && y_batch_stride % V == 0 &&
+           (((uintptr_t)x | (uintptr_t)y) & 15) == 0 && (long)HW * (C / V) < (1L << 31) && N <= 65535;
+}
+long gn_workspace(int N, int HW, int groups, int ppb) {
+    const long nblk = (HW + ppb - 1) / ppb;
+    return 2L * N * groups * (1 + nblk);
+}
+}  // namespace
+
+extern "C" long kinet_groupnorm_workspace(int N, int HW, int C, int groups, int dtype) {
+    (void)C;
+    (void)dtype;
+    if (N <= 0 || HW <= 0 || groups <= 0) return 0;
+    return gn_workspace(N, HW, groups, 64);   // the larger of the two paths' needs
+}
+
 extern "C" int kinet_groupnorm(const void* x, const float* gamma, const float* beta, void* y, int N, int HW, int C,
                                int groups, int y_batch_stride, float eps, int dtype, float* stats,
                                kinet_stream_t stream) {
     KINET_CHECK_ARG(N >= 0 && HW > 0 && C > 0 && groups > 0 && C % groups == 0, "groupnorm: bad geometry");
     KINET_CHECK_ARG(y_batch_stride >= HW * C, "groupnorm: y_batch_stride < HW*C");
-    KINET_CHECK_ARG(stats != nullptr, "groupnorm: stats workspace (2*N*groups floats) required");
+    KINET_CHECK_ARG(stats != nullptr, "groupnorm: workspace of kinet_groupnorm_workspace() floats required");
     if (N == 0) return KINET_OK;
     hipStream_t s = (hipStream_t)stream;
-    KINET_CHECK_HIP(hipMemsetAsync(stats, 0, (size_t)2 * N * groups * sizeof(float), s));
-    // 16-byte vector path: bf16 / f16 / f32, whole vectors per group, aligned rows
-    const int V = dtype == KINET_F32 ? 4 : 8;
-    const bool vec = dtype != KINET_F64 && C % V == 0 && (C / groups) % V == 0 && C / V <= 256 &&
-                     y_batch_stride % V == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0 &&
-                     (long)HW * (C / V) < (1L << 31) && N <= 65535;
+    const bool vec = gn_vec_ok(x, y, HW, C, groups, y_batch_stride, N, dtype);
+    const int ppb = vec ? 128 : 64;
+    const int nblk = (HW + ppb - 1) / ppb;
+    float* part = stats + 2L * N * groups;
+    const dim3 g1(nblk, N);
     if (vec) {
-        const int ppb = 128;
-        const dim3 g1((HW + ppb - 1) / ppb, N), g2((unsigned)(((long)HW * (C / V) + 255) / 256), N);
+        const int V = dtype == KINET_F32 ? 4 : 8;
+        const dim3 g2((unsigned)(((long)HW * (C / V) + 255) / 256), N);
 #define GNV(TT)                                                                                                  \
     do {                                                                                                         \
-        hipLaunchKernelGGL((gn_stats_vec_kernel<TT>), g1, dim3(256), 2 * groups * sizeof(float), s, (const TT*)x, \
-                           stats, HW, C, groups, ppb);                                                           \
+        hipLaunchKernelGGL((gn_stats_vec_kernel<TT>), g1, dim3(256), 0, s, (const TT*)x, part, HW, C, groups, ppb); \
+        hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(64), 0, s, (const float*)part, stats, nblk, groups); \
         hipLaunchKernelGGL((gn_apply_vec_kernel<TT>), g2, dim3(256), 0, s, (const TT*)x, stats, gamma, beta,     \
                            (TT*)y, HW, C, groups, (long)y_batch_stride, eps);                                    \
     } while (0)
@@ -492,10 +543,10 @@ extern "C" int kinet_groupnorm(const void* x, const float* gamma, const float* b
         KINET_LAUNCH_CHECK();
         return KINET_OK;
     }
-    const int ppb = 64;
-    dim3 g1((HW + ppb - 1) / ppb, N);
-    DISPATCH_T(dtype, hipLaunchKernelGGL((gn_stats_kernel<T>), g1, dim3(256), 2 * groups * sizeof(float), s,
-                                         (const T*)x, stats, HW, C, groups, ppb));
+    KINET_CHECK_ARG(C <= 8192, "groupnorm: C up to 8192 on the scalar path");
+    DISPATCH_T(dtype, hipLaunchKernelGGL((gn_stats_kernel<T>), g1, dim3(256), 2 * C * sizeof(float), s,
+                                         (const T*)x, part, HW, C, groups, ppb));
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(64), 0, s, (const float*)part, stats, nblk, groups);
     KINET_LAUNCH_CHECK();
     const long total = (long)N * HW * C;
     DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T>), dim3(grid_for(total)), dim3(256), 0, s, (const T*)x,

@@ -344,7 +344,8 @@ def groupnorm_nhwc(x, weight, bias, groups, eps=1e-5, out=None, out_batch_stride
     if out is None:
         out = torch.empty_like(x)
         out_batch_stride = HW * C
-    stats = torch.empty(2 * B * groups, dtype=torch.float32, device=x.device)
+    nws = N.lib().kinet_groupnorm_workspace(B, HW, C, groups, N.dtype_code(x.dtype))
+    stats = torch.empty(max(1, nws), dtype=torch.float32, device=x.device)
     N.call('kinet_groupnorm', N.ptr(x), N.ptr(f32(weight)), N.ptr(f32(bias)), N.ptr(out), B, HW, C, groups,
            int(out_batch_stride), float(eps), N.dtype_code(x.dtype), N.ptr(stats), N.stream(x.device),
            work={'family': 'norm', 'bytes': 2 * x.numel() * x.element_size()})

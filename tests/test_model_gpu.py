@@ -95,6 +95,35 @@ def test_config2_bf16_close(config2):
         model.set_compute_dtype(torch.float32)
 
 
+def test_config2_bf16_deterministic(config2):
+    """Every kernel of the inference path reduces in a fixed order: reruns of the bf16 forward,
+    and two batches in flight on two HIP streams, give bit-identical outputs."""
+    d, model = config2
+    model.set_compute_dtype(torch.bfloat16)
+    try:
+        imgs = [torch.from_numpy(d['img0']).cuda(), torch.from_numpy(d['img1']).cuda()]
+        imgs2 = [i.flip(-1).contiguous() for i in imgs]
+        with torch.no_grad():
+            a = model(imgs)[0]
+            torch.cuda.synchronize()
+            a = {k: a[k].clone() for k in ('pred_logits', 'pred_boxes', 'hs_embed')}
+            b = model(imgs2)[0]
+            torch.cuda.synchronize()
+            b = {k: b[k].clone() for k in ('pred_logits', 'pred_boxes', 'hs_embed')}
+            s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+            for _ in range(2):
+                with torch.cuda.stream(s1):
+                    a2 = model(imgs)[0]
+                with torch.cuda.stream(s2):
+                    b2 = model(imgs2)[0]
+            torch.cuda.synchronize()
+        for k in a:
+            assert torch.equal(a2[k], a[k]), k
+            assert torch.equal(b2[k], b[k]), k
+    finally:
+        model.set_compute_dtype(torch.float32)
+
+
 def test_tracking_multiframe_parity(golden_dir):
     d = dict(np.load(os.path.join(golden_dir, 'detr_tracking_mf_small.npz')))
     model = _build(golden_dir, 'detr_tracking_mf_small.keys.txt', 31, 'train_deformable', 'train_multi_frame',
