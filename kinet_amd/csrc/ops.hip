@@ -103,16 +103,36 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x, 
     }
 }
 
-// stats[n][i] = sum over the nblk block partials of image n, in block order
+// stats[n][i] = sum over the nblk block partials of image n in a fixed order: with w = 2*groups
+// outputs, 256/w threads share one output (strided over the blocks, loads unrolled so they are
+// all in flight), then their sums are combined in thread order
 __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restrict__ part, float* __restrict__ stats,
                                                           int nblk, int groups) {
+    __shared__ float red[256];
     const int n = blockIdx.x;
     const int w = 2 * groups;
-    for (int i = threadIdx.x; i < w; i += blockDim.x) {
-        const float* pp = part + (long)n * nblk * w + i;
+    const int tpo = w <= 256 ? 256 / w : 1;   // threads per output
+    const int i0 = threadIdx.x % w, k = threadIdx.x / w;
+    for (int base = 0; base < w; base += 256) {
+        const int i = base + (tpo > 1 ? i0 : (int)threadIdx.x);
         float a = 0.f;
-        for (int b = 0; b < nblk; ++b) a += pp[(long)b * w];
-        stats[(long)n * w + i] = a;
+        if (i < w && k < tpo) {
+            const float* pp = part + (long)n * nblk * w + i;
+#pragma unroll 8
+            for (int b = k; b < nblk; b += tpo) a += pp[(long)b * w];
+        }
+        if (tpo == 1) {
+            if (i < w) stats[(long)n * w + i] = a;
+            continue;
+        }
+        red[threadIdx.x] = a;
+        __syncthreads();
+        if (k == 0 && i < w) {
+            float t = 0.f;
+            for (int j = 0; j < tpo; ++j) t += red[j * w + i0];
+            stats[(long)n * w + i] = t;
+        }
+        break;   // tpo > 1 means w <= 256: one pass covers every output
     }
 }
 
@@ -532,7 +552,7 @@ extern "C" int kinet_groupnorm(const void* x, const float* gamma, const float* b
 #define GNV(TT)                                                                                                  \
     do {                                                                                                         \
         hipLaunchKernelGGL((gn_stats_vec_kernel<TT>), g1, dim3(256), 0, s, (const TT*)x, part, HW, C, groups, ppb); \
-        hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(64), 0, s, (const float*)part, stats, nblk, groups); \
+        hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, (const float*)part, stats, nblk, groups); \
         hipLaunchKernelGGL((gn_apply_vec_kernel<TT>), g2, dim3(256), 0, s, (const TT*)x, stats, gamma, beta,     \
                            (TT*)y, HW, C, groups, (long)y_batch_stride, eps);                                    \
     } while (0)
@@ -546,7 +566,7 @@ extern "C" int kinet_groupnorm(const void* x, const float* gamma, const float* b
     KINET_CHECK_ARG(C <= 8192, "groupnorm: C up to 8192 on the scalar path");
     DISPATCH_T(dtype, hipLaunchKernelGGL((gn_stats_kernel<T>), g1, dim3(256), 2 * C * sizeof(float), s,
                                          (const T*)x, part, HW, C, groups, ppb));
-    hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(64), 0, s, (const float*)part, stats, nblk, groups);
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, (const float*)part, stats, nblk, groups);
     KINET_LAUNCH_CHECK();
     const long total = (long)N * HW * C;
     DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T>), dim3(grid_for(total)), dim3(256), 0, s, (const T*)x,
