@@ -40,8 +40,8 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--batch', type=int, default=8, help='frames per GPU per step')
-    ap.add_argument('--streams', type=int, default=2,
+    ap.add_argument('--batch', type=int, default=16, help='frames per GPU per step')
+    ap.add_argument('--streams', type=int, default=3,
                     help='batches in flight per GPU, each on its own HIP stream (serving-style pipelining)')
     ap.add_argument('--height', type=int, default=800)
     ap.add_argument('--width', type=int, default=1333)
