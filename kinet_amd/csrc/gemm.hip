@@ -633,7 +633,11 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         bn = a.N <= 64 ? 64 : 128;
         bm = a.N <= 64 ? 128 : 64;
         // big square-ish problems: the 128x128 tile's lower operand traffic per flop wins
-        if (a.N >= 512 && (long)((a.M + 127) / 128) * ((a.N + 127) / 128) >= 2048) bm = bn = 128;
+        const long t128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128);
+        if (a.N >= 512 && t128 >= 2048) bm = bn = 128;
+        // 3x3 convs (K >= 9*128) with >= ~2 rounds of 128x128 tiles over the 512 resident
+        // slots: 3-6 % faster than 64x128 at batch 16 (tools/sweep_conv.py 16), neutral at 8
+        if (CONV && a.K >= 1152 && a.N >= 128 && t128 >= 1000) bm = bn = 128;
     }
     if (force_bm && !ln) {
         bm = force_bm;
