@@ -1,0 +1,34 @@
+"""Probe: which host ops of one batch-8 forward issue device-to-device memcpys
+(rocprof shows them as __amd_rocclr_copyBuffer).  python tools/copy_probe.py"""
+import os
+import sys
+
+import torch
+from torch.profiler import ProfilerActivity, profile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import bench
+    from kinet_amd.models import nested_tensor_from_tensor_list
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(0)
+    model = bench.build(dev, torch.bfloat16)
+    x = nested_tensor_from_tensor_list([torch.randn(3, 800, 1333, device=dev) for _ in range(8)])
+    with torch.no_grad():
+        for _ in range(2):
+            model(x)
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CPU], with_stack=True, record_shapes=True) as prof:
+            model(x)
+            torch.cuda.synchronize()
+    names = ('aten::copy_', 'aten::clone', 'aten::contiguous', 'aten::cat', 'aten::stack', 'aten::to',
+             'aten::_to_copy', 'aten::index', 'aten::repeat', 'aten::expand', 'aten::zeros', 'aten::fill_')
+    print(prof.key_averages(group_by_input_shape=True).table(sort_by='count', row_limit=40))
+    print(prof.key_averages(group_by_stack_n=6).table(sort_by='count', row_limit=25))
+    del names
+
+
+if __name__ == '__main__':
+    main()
