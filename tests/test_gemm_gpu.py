@@ -78,6 +78,17 @@ def test_stem_packed_image(K):
     assert _rel(mp.permute(0, 3, 1, 2), F.max_pool2d(ref, 3, 2, 1)) < 1e-6
 
 
+@pytest.mark.parametrize('N,C,H,W', [(3, 64, 101, 167), (1, 64, 5, 7), (2, 32, 400, 667)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_maxpool_exact(K, N, C, H, W, dtype):
+    """3x3/2 max-pool (XCD-banded row kernel, incl. fewer rows than XCDs): bit-exact."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, C, H, W, generator=g).to(dtype)
+    ref = F.max_pool2d(x.float(), 3, 2, 1).to(dtype)
+    got = K.maxpool_3x3s2(x.permute(0, 2, 3, 1).contiguous().cuda()).permute(0, 3, 1, 2).cpu()
+    assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize('H,W', [(50, 66), (37, 41), (800, 1333)])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16, torch.float32])
 def test_stem_kwfold(K, H, W, dtype):
