@@ -25,9 +25,14 @@ def main():
             torch.cuda.synchronize()
     names = ('aten::copy_', 'aten::clone', 'aten::contiguous', 'aten::cat', 'aten::stack', 'aten::to',
              'aten::_to_copy', 'aten::index', 'aten::repeat', 'aten::expand', 'aten::zeros', 'aten::fill_')
-    print(prof.key_averages(group_by_input_shape=True).table(sort_by='count', row_limit=40))
-    print(prof.key_averages(group_by_stack_n=6).table(sort_by='count', row_limit=25))
-    del names
+    from collections import Counter
+    cnt = Counter()
+    for e in prof.events():
+        if e.name in names:
+            st = [f for f in (e.stack or []) if 'kinet_amd' in f][:2]
+            cnt[(e.name, str(e.input_shapes)[:60], ' <- '.join(st))] += 1
+    for (n, shp, st), c in sorted(cnt.items(), key=lambda kv: -kv[1]):
+        print(f'{c:3d}  {n:18s} {shp:60s} {st}')
 
 
 if __name__ == '__main__':
