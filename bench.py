@@ -154,6 +154,8 @@ def main():
     batches = [nested_tensor_from_tensor_list([torch.randn(3, a.height, a.width, generator=g, device=dev)
                                                for _ in range(a.batch)]) for _ in range(nst)]
     streams = [torch.cuda.Stream(device=dev) for _ in range(nst)]
+    for st in streams:   # the input batches were written on the default stream
+        st.wait_stream(torch.cuda.current_stream(dev))
     samples = batches[0]
 
     def step(i=0):
@@ -167,6 +169,10 @@ def main():
 
     for i in range(max(1, a.warmup)):
         out = step(i)
+        if i == 0:
+            # step 0 fills the weight-pack / geometry caches on its stream; the other
+            # streams read them from step 1 on
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -35,7 +35,8 @@ enum kinet_status {
 /* Text of the last error raised on this host thread ("" if none). */
 const char* kinet_last_error(void);
 
-/* Library build identifier (gfx target + git-free build stamp). */
+/* Library build identifier: "kinet_amd <version> gfx950 src <hash>", where <hash> is the
+ * sha256 prefix of the kernel sources + headers it was compiled from (kinet_amd/build.py). */
 const char* kinet_version(void);
 
 #ifdef __cplusplus

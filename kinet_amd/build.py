@@ -7,6 +7,7 @@ shared object: include/*.h).  The .so travels to the GPU box with the repo snaps
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -30,15 +31,44 @@ def _headers():
     return glob.glob(os.path.join(CSRC, '*.h')) + glob.glob(os.path.join(HERE, '..', 'include', '*.h'))
 
 
-def _compile(src, force):
+def source_hash():
+    """sha256 over every kernel source and header (csrc/*.hip, csrc/*.h, include/*.h), by
+    relative path and content.  Embedded in the library (kinet_version()) so a test on the
+    GPU box can prove the .so it loaded was built from the sources it shipped with."""
+    files = sorted(_sources() + _headers(), key=lambda p: os.path.relpath(p, os.path.dirname(HERE)))
+    h = hashlib.sha256()
+    for p in files:
+        h.update(os.path.relpath(os.path.realpath(p), os.path.dirname(HERE)).encode() + b'\0')
+        with open(p, 'rb') as f:
+            h.update(f.read())
+        h.update(b'\0')
+    return h.hexdigest()[:16]
+
+
+def _file_key(src):
+    """Hash of one translation unit's inputs: its source + every header + the flags."""
+    h = hashlib.sha256(' '.join(FLAGS).encode())
+    for p in [src] + sorted(_headers()):
+        with open(p, 'rb') as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _compile(src, force, src_hash):
+    """Content-addressed: an object is rebuilt unless its stamp matches the hash of its
+    inputs (mtimes are not trusted -- a snapshot copy or checkout can reorder them).
+    status.hip carries the whole-library hash, so it is keyed on that."""
     obj = os.path.join(OBJ_DIR, os.path.basename(src) + '.o')
-    newest_dep = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _headers()])
-    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
+    stamp = obj + '.hash'
+    key = src_hash if os.path.basename(src) == 'status.hip' else _file_key(src)
+    if not force and os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read().strip() == key:
         return obj, False
-    cmd = [HIPCC] + FLAGS + ['-c', src, '-o', obj]
+    cmd = [HIPCC] + FLAGS + [f'-DKINET_SRC_HASH="{src_hash}"', '-c', src, '-o', obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'hipcc failed for {src}:\n{r.stdout}\n{r.stderr}')
+    with open(stamp, 'w') as f:
+        f.write(key + '\n')
     return obj, True
 
 
@@ -46,8 +76,9 @@ def build(force=False, jobs=None, verbose=True):
     os.makedirs(OBJ_DIR, exist_ok=True)
     srcs = _sources()
     jobs = jobs or min(8, len(srcs)) or 1
+    src_hash = source_hash()
     with cf.ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(lambda s: _compile(s, force), srcs))
+        results = list(ex.map(lambda s: _compile(s, force, src_hash), srcs))
     objs = [o for o, _ in results]
     rebuilt = any(r for _, r in results)
     if rebuilt or force or not os.path.exists(LIB):

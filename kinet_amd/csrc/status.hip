@@ -19,4 +19,10 @@ void set_error(const char* fmt, ...) {
 
 extern "C" const char* kinet_last_error(void) { return kinet::g_err; }
 
-extern "C" const char* kinet_version(void) { return "kinet_amd 0.1 gfx950 built " __DATE__ " " __TIME__; }
+#ifndef KINET_SRC_HASH
+#define KINET_SRC_HASH "unknown"
+#endif
+
+// "kinet_amd <ver> gfx950 src <hash>": <hash> = kinet_amd.build.source_hash() of the sources
+// this library was compiled from (tests/test_native_cpu.py / test_build_gpu compare it).
+extern "C" const char* kinet_version(void) { return "kinet_amd 0.2 gfx950 src " KINET_SRC_HASH; }

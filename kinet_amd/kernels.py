@@ -432,6 +432,11 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
     offlog (B, Lq, M*L*P*3) f32 (or f16 with 16-bit values) [offsets | logits];
     reference_points (B, Lq, L, 2|4) f32.
     out_dtype: value.dtype, or bfloat16 from float16 values (mixed-precision gather path).
+    query_tile_order: optional int32 (ceil(Lq/16),) processing order of the 16-query tiles
+    (encoder_tile_order); only the fast 16-bit D=32 kernel uses it, the generic kernel
+    ignores it (the output is identical either way).
+    Cached weights/geometry are built on the stream current at first use: a caller that
+    runs several streams from a cold start synchronises once after the first forward.
     Returns (B, Lq, d) [, loc, attw]."""
     if head_major:
         M_, B, S, D = value.shape
@@ -459,6 +464,13 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
         loc = torch.empty((B, Lq, n_heads, n_levels, n_points, 2), dtype=torch.float32, device=value.device)
         attw = torch.empty((B, Lq, n_heads, n_levels, n_points), dtype=torch.float32, device=value.device)
     qm = query_attn_mask.to(torch.uint8).contiguous() if query_attn_mask is not None else None
+    if query_tile_order is not None:
+        # the kernel reads torder[tile] for every 16-query tile of the grid
+        t = query_tile_order
+        if (t.dtype != torch.int32 or t.device != value.device or not t.is_contiguous()
+                or t.numel() != (Lq + 15) // 16):
+            raise RuntimeError(f'msda_fused: query_tile_order must be a contiguous int32 tensor on '
+                               f'{value.device} with ceil(Lq/16) = {(Lq + 15) // 16} entries')
     if offlog.dtype not in (torch.float32, torch.float16):
         raise RuntimeError('msda_fused: the offsets/logits projection must be f32 or f16')
     ev = value.element_size()

@@ -68,32 +68,5 @@ def build_model(args):
     return model, criterion, postprocessors
 
 
-def smoke_forward(device):
-    """One tiny detector forward on `device` checked against the reference fixture
-    (used by __graft_entry__.smoke())."""
-    import os
-    import sys
-    import numpy as np
-    here = os.path.dirname(os.path.abspath(__file__))
-    golden = os.path.join(here, '..', '..', 'tests', 'golden')
-    sys.path.insert(0, golden)
-    from weights import make_state_dict
-    from kinet_amd.models.config import load_args
-    d = np.load(os.path.join(golden, 'detr_config2_small.npz'))
-    args = load_args('train_deformable')
-    model, _, _ = build_model(args)
-    keys = [ln.split() for ln in open(os.path.join(golden, 'detr_config2_small.keys.txt'))]
-    model.load_state_dict(make_state_dict({k[0]: [int(s) for s in k[1:]] for k in keys}, seed=21))
-    model = model.to(device).eval()
-    imgs = [torch.from_numpy(d['img0']).to(device), torch.from_numpy(d['img1']).to(device)]
-    with torch.no_grad():
-        out = model(imgs)[0]
-    torch.cuda.synchronize()
-    err_l = (out['pred_logits'].cpu() - torch.from_numpy(d['pred_logits'])).abs().max().item()
-    err_b = (out['pred_boxes'].cpu() - torch.from_numpy(d['pred_boxes'])).abs().max().item()
-    assert err_l < 1e-3 and err_b < 1e-3, (err_l, err_b)
-    print(f'smoke detector: max|dlogits|={err_l:.2e} max|dboxes|={err_b:.2e}')
-
-
 __all__ = ['build_model', 'DeformableDETR', 'DeformableDETRTracking', 'DeformablePostProcess',
            'NestedTensor', 'nested_tensor_from_tensor_list']

@@ -209,7 +209,7 @@ class DeformableDETR(nn.Module):
     def forward(self, samples, targets: list = None, prev_features=None):
         if not isinstance(samples, NestedTensor):
             samples = nested_tensor_from_tensor_list(samples)
-        if not fast_path():
+        if not fast_path(self):
             return self._forward_reference(samples, targets, prev_features)
         dt = self.compute_dtype
         device = samples.tensors.device

@@ -47,9 +47,18 @@ def _get_activation_fn(activation):
 _FORCE_REFERENCE = [0]
 
 
-def fast_path():
-    """HIP inference path: no autograd, and not inside reference_path()."""
-    return not torch.is_grad_enabled() and not _FORCE_REFERENCE[0]
+def _active_dropout(module):
+    return module.training and any(isinstance(m, (nn.Dropout, nn.MultiheadAttention)) and
+                                   getattr(m, 'p', getattr(m, 'dropout', 0.0)) > 0 for m in module.modules())
+
+
+def fast_path(module=None):
+    """HIP inference path: no autograd, not inside reference_path(), and -- when `module`
+    is given -- no dropout that train mode would apply (a train-mode module under no_grad
+    must still drop activations as the reference does)."""
+    if torch.is_grad_enabled() or _FORCE_REFERENCE[0]:
+        return False
+    return module is None or not _active_dropout(module)
 
 
 class reference_path:
@@ -87,7 +96,7 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return self.norm2(src + self.dropout3(src2))
 
     def forward(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None):
-        if fast_path():
+        if fast_path(self):
             return self.forward_fast(src, pos, reference_points, spatial_shapes, padding_mask, query_order)
         src2 = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, spatial_shapes, padding_mask)
         src = self.norm1(src + self.dropout1(src2))
@@ -169,7 +178,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
 
     def forward(self, tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask=None,
                 query_attn_mask=None, value=None):
-        if fast_path():
+        if fast_path(self):
             return self.forward_fast(tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask,
                                      query_attn_mask, value)
         q = k = self.with_pos_embed(tgt, query_pos)
@@ -223,7 +232,7 @@ class DeformableTransformerDecoder(nn.Module):
 
     def forward(self, tgt, reference_points, src, src_spatial_shapes, src_valid_ratios,
                 query_pos=None, src_padding_mask=None, query_attn_mask=None):
-        if fast_path():
+        if fast_path(self):
             return self.forward_fast(tgt, reference_points, src, src_spatial_shapes, src_valid_ratios,
                                      query_pos, src_padding_mask, query_attn_mask)
         output = tgt
@@ -355,7 +364,7 @@ class DeformableTransformer(nn.Module):
 
     def forward(self, srcs, masks, pos_embeds, query_embed=None, targets=None):
         src_flatten, mask_flatten, lvl_pos, shapes, valid_ratios = self.prepare_inputs(srcs, masks, pos_embeds)
-        if fast_path():
+        if fast_path(self):
             dt = srcs[0].dtype
             src_flatten = src_flatten.to(dt).contiguous()
             lvl_pos = lvl_pos.to(dt).contiguous()
@@ -396,7 +405,7 @@ class DeformableTransformer(nn.Module):
             pm = pad[:, tok] if pad is not None else None
             src = src_flatten[:, tok]
             pos = lvl_pos_embed_flatten[:, tok]
-            if fast_path():
+            if fast_path(self):
                 src, pos = src.contiguous(), pos.contiguous()
                 pm = pm.contiguous() if pm is not None else None
             encs.append(self.encoder(src, e['spatial_shapes'], e['valid_ratios'], pos, pm, reference_points=e['ref'],
@@ -421,7 +430,7 @@ class DeformableTransformer(nn.Module):
             tgt = torch.cat([prev_hs_embed.to(tgt.dtype), tgt], dim=1)
             reference_points = torch.cat([prev_boxes[..., :2].to(reference_points.dtype), reference_points], dim=1)
         init_reference_out = reference_points
-        if fast_path():
+        if fast_path(self):
             dt = memory.dtype
             tgt = tgt.to(dt).contiguous()
             query_embed_ = query_embed_.to(dt).contiguous()

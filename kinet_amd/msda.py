@@ -8,8 +8,6 @@ attention_weights, im2col_step)` is the reference operator boundary
 (sampling_offsets / attention_weights / value_proj / output_proj, ms_deform_attn.py:27-30)
 so reference state_dicts load unchanged.
 """
-import warnings
-
 import torch
 from torch import nn
 from torch.autograd import Function
@@ -56,10 +54,6 @@ class MSDeformAttn(nn.Module):
         super().__init__()
         if d_model % n_heads != 0:
             raise ValueError('d_model must be divisible by n_heads, but got {} and {}'.format(d_model, n_heads))
-        _d_per_head = d_model // n_heads
-        if not ((_d_per_head & (_d_per_head - 1) == 0) and _d_per_head != 0):
-            warnings.warn("You'd better set d_model in MSDeformAttn to make the dimension of each attention "
-                          "head a power of 2 which is more efficient in our CUDA implementation.")
         self.im2col_step = im2col_step
         self.d_model = d_model
         self.n_levels = n_levels
@@ -93,7 +87,9 @@ class MSDeformAttn(nn.Module):
                 input_padding_mask=None, query_attn_mask=None):
         N, Len_q, _ = query.shape
         N, Len_in, _ = input_flatten.shape
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+        # autograd whenever grad mode is on (frozen parameters still need input gradients,
+        # as upstream's module is differentiable w.r.t. query / input_flatten / refs)
+        if torch.is_grad_enabled():
             return self._forward_autograd(query, reference_points, input_flatten, input_spatial_shapes,
                                           input_padding_mask, query_attn_mask)
         value = self.project_value(input_flatten, input_padding_mask)

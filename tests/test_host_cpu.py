@@ -32,6 +32,24 @@ def test_library_exports_every_declared_symbol():
     assert b'gfx950' in lib.kinet_version()
 
 
+def _check_library_matches_sources():
+    from kinet_amd import _native
+    from kinet_amd.build import source_hash
+    ver = _native.lib().kinet_version().decode()
+    assert ver.endswith('src ' + source_hash()), (ver, source_hash())
+
+
+def test_library_built_from_these_sources():
+    """kinet_version() embeds the hash of csrc/ + include/ it was compiled from."""
+    _check_library_matches_sources()
+
+
+@pytest.mark.gpu
+def test_library_built_from_these_sources_on_gpu_box():
+    """Same check in the GPU tier: the .so the box loads was built from the shipped sources."""
+    _check_library_matches_sources()
+
+
 def test_ctypes_signatures_cover_declarations():
     from kinet_amd import _native
     assert _declared_symbols() <= set(_native._SIGS)
