@@ -7,8 +7,14 @@ iterative box refinement, 91 focal logits) on synthetic 3x800x1333 frames, bf16 
 all kernels hand-written HIP (kinet_amd).  One step = one detection forward over a batch
 of `--batch` frames per GPU whose pixels are already resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload config2|config5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (driver)
+
+`--workload config5` (BASELINE.json configs[4], cfgs/train_full_res.yaml): ResNet-101,
+d=288 (head_dim 36), 500 object + 20 track queries, separate per-frame encoders and an
+8-level decoder over [current, prev] memory, fp16, 1080x1920 frames; one step = one
+tracking forward per frame with the previous frame's features (resident in HBM, as the
+online tracker holds them) -- the HBM-stress case for MSDeformAttn (S = 43,110 per frame).
 
 Multi-GPU: frames are independent -> one replica per GPU, no data-path collective
 ("scaling": "weak"); a barrier + max-over-ranks wall time brackets the timed region.
@@ -34,21 +40,38 @@ MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'f16': 2500.0, 'f32': 157.3}   # dense
 PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
 MSDA_KERNEL = 'msda_fused_fast_kernel'
 
+WORKLOADS = {
+    'config2': dict(cfgs=('train_deformable',), over={}, h=800, w=1333, batch=16, streams=3, dtype='bf16',
+                    K=0, desc='config2 cfgs/train_deformable.yaml: R-50 Deformable-DETR inference forward, '
+                              'd=256, 4 levels, 6/6 layers, 300 queries, box refine'),
+    'config5': dict(cfgs=('train_deformable', 'train_multi_frame', 'train_tracking', 'train_full_res'),
+                    over=dict(dataset='mot', backbone='resnet101'), h=1080, w=1920, batch=4, streams=2, dtype='f16',
+                    K=20, desc='config5 cfgs/train_full_res.yaml: R-101 multi-frame tracking forward, d=288, '
+                               '500 object + 20 track queries, separate per-frame encoders (L=4), 8-level decoder, '
+                               'prev-frame features resident'),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--batch', type=int, default=16, help='frames per GPU per step')
-    ap.add_argument('--streams', type=int, default=3,
+    ap.add_argument('--workload', default='config2', choices=sorted(WORKLOADS))
+    ap.add_argument('--batch', type=int, default=None, help='frames per GPU per step')
+    ap.add_argument('--streams', type=int, default=None,
                     help='batches in flight per GPU, each on its own HIP stream (serving-style pipelining)')
-    ap.add_argument('--height', type=int, default=800)
-    ap.add_argument('--width', type=int, default=1333)
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'f32'])
+    ap.add_argument('--height', type=int, default=None)
+    ap.add_argument('--width', type=int, default=None)
+    ap.add_argument('--dtype', default=None, choices=['bf16', 'f16', 'f32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=20.0, help='bound on the CPU baseline sample')
-    return ap.parse_args()
+    a = ap.parse_args()
+    wl = WORKLOADS[a.workload]
+    for k, wk in (('batch', 'batch'), ('streams', 'streams'), ('height', 'h'), ('width', 'w'), ('dtype', 'dtype')):
+        if getattr(a, k) is None:
+            setattr(a, k, wl[wk])
+    return a
 
 
 def setup_dist(a):
@@ -63,12 +86,14 @@ def setup_dist(a):
     return world, rank, torch.device('cuda', local if world > 1 else 0)
 
 
-def build(dev, dtype):
+def build(dev, dtype, wl):
     from kinet_amd.models import build_model
     from kinet_amd.models.config import load_args
     torch.manual_seed(0)
-    model, _, _ = build_model(load_args('train_deformable', device='cuda'))
+    model, _, _ = build_model(load_args(*wl['cfgs'], device='cuda', **wl['over']))
     model = model.to(dev).eval()
+    if wl['K']:
+        model.tracking()
     model.set_compute_dtype(dtype)
     return model
 
@@ -103,10 +128,22 @@ def pmc_traffic(kernel):
         return None, None
 
 
+def cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for ln in f:
+                if ln.startswith('model name'):
+                    return ln.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(seconds):
     """Reference CPU path (ms_deform_attn_core_pytorch, restated in oracle/msda_oracle.py)
     on one frame's MSDA work of the same workload: 6 encoder calls (Lq = S = 22,223) and
-    6 decoder calls (Lq = 300), fp32, all host threads."""
+    6 decoder calls (Lq = 300), fp32, all host threads; plus the config-5 encoder call
+    (S = 43,110 at 1080x1920, head_dim 36) that SURVEY 8(d) names."""
     from oracle.msda_oracle import core_pytorch
     # the box's CPU share (OMP_NUM_THREADS=16 there); os.cpu_count() reports the whole host
     threads = int(os.environ.get('OMP_NUM_THREADS') or torch.get_num_threads() or 1)
@@ -133,26 +170,57 @@ def cpu_baseline(seconds):
         dec.append(call(300))
     t_enc, t_dec = statistics.median(enc), statistics.median(dec)
     frame_s = 6 * t_enc + 6 * t_dec
+    # config 5 encoder call: 4 levels of a 1080x1920 frame, d=288 (M=8, D=36), Lq = S
+    shapes5 = torch.tensor([[135, 240], [68, 120], [34, 60], [17, 30]], dtype=torch.long)
+    S5 = int((shapes5[:, 0] * shapes5[:, 1]).sum())
+    value5 = torch.randn(1, S5, M, 36, generator=g)
+    loc5 = torch.rand(1, S5, M, L, P, 2, generator=g)
+    attw5 = torch.rand(1, S5, M, L, P, generator=g)
+    attw5 /= attw5.sum((-1, -2), keepdim=True)
+    t5 = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        core_pytorch(value5, shapes5, loc5, attw5)
+        t5.append(time.perf_counter() - t0)
     return {'value': 1.0 / frame_s, 'unit': 'frames/s (MSDA share only; upper bound of the CPU detector)',
-            'cores': threads, 'kind': 'port',
+            'cores': threads, 'cpu_model': cpu_model(), 'kind': 'port',
             'sample': f'{len(enc)} frames of MSDeformAttn work on the host CPU: 6 encoder calls '
                       f'(Lq=S={S}, median {t_enc * 1e3:.1f} ms) + 6 decoder calls (Lq=300, median '
-                      f'{t_dec * 1e3:.2f} ms), fp32 ms_deform_attn_core_pytorch restatement',
-            'msda_encoder_ms_per_call': t_enc * 1e3, 'msda_decoder_ms_per_call': t_dec * 1e3}
+                      f'{t_dec * 1e3:.2f} ms), fp32 ms_deform_attn_core_pytorch restatement; plus 2 config-5 '
+                      f'encoder calls (Lq=S={S5}, D=36, min {min(t5) * 1e3:.1f} ms)',
+            'msda_encoder_ms_per_call': t_enc * 1e3, 'msda_decoder_ms_per_call': t_dec * 1e3,
+            'config5_msda_encoder_ms_per_call': min(t5) * 1e3}
 
 
 def main():
     a = parse()
     world, rank, dev = setup_dist(a)
-    dtype = torch.bfloat16 if a.dtype == 'bf16' else torch.float32
+    dtype = {'bf16': torch.bfloat16, 'f16': torch.float16, 'f32': torch.float32}[a.dtype]
+    wl = WORKLOADS[a.workload]
     from kinet_amd import _native
     from kinet_amd.models import nested_tensor_from_tensor_list
-    model = build(dev, dtype)
+    model = build(dev, dtype, wl)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     # one independent batch per in-flight slot (distinct requests, all resident in HBM)
     nst = max(1, a.streams)
     batches = [nested_tensor_from_tensor_list([torch.randn(3, a.height, a.width, generator=g, device=dev)
                                                for _ in range(a.batch)]) for _ in range(nst)]
+    extra = [() for _ in range(nst)]
+    if wl['K']:
+        # tracking step inputs per slot: K track queries per frame (hs embeddings + boxes of
+        # the previous frame's detections) and the previous frame's backbone features
+        K_, d = wl['K'], model.hidden_dim
+        for i in range(nst):
+            prev = nested_tensor_from_tensor_list([torch.randn(3, a.height, a.width, generator=g, device=dev)
+                                                   for _ in range(a.batch)])
+            with torch.no_grad():
+                feats = model(prev)[2]
+            boxes = torch.cat([torch.rand(a.batch, K_, 2, generator=g, device=dev) * 0.8 + 0.1,
+                               torch.rand(a.batch, K_, 2, generator=g, device=dev) * 0.2 + 0.02], -1)
+            hs = torch.randn(a.batch, K_, d, generator=g, device=dev)
+            targets = [{'track_query_hs_embeds': hs[b], 'track_query_boxes': boxes[b]} for b in range(a.batch)]
+            extra[i] = (targets, feats)
+        torch.cuda.synchronize()
     streams = [torch.cuda.Stream(device=dev) for _ in range(nst)]
     for st in streams:   # the input batches were written on the default stream
         st.wait_stream(torch.cuda.current_stream(dev))
@@ -161,11 +229,11 @@ def main():
     def step(i=0):
         with torch.no_grad():
             if nst == 1:
-                return model(batches[0])
+                return model(batches[0], *extra[0])
             # step i runs batch i % nst on its own stream: the decoder / small-kernel phases of
             # one batch overlap the backbone of the next (no host syncs anywhere in a forward)
             with torch.cuda.stream(streams[i % nst]):
-                return model(batches[i % nst])
+                return model(batches[i % nst], *extra[i % nst])
 
     for i in range(max(1, a.warmup)):
         out = step(i)
@@ -195,7 +263,7 @@ def main():
     _native.trace_begin()
     for _ in range(3):
         with torch.no_grad():
-            model(samples)
+            model(samples, *extra[0])
     trace = _native.trace_end()
     torch.cuda.synchronize()
     fam, msda = summarize_trace(trace, 3)
@@ -207,7 +275,7 @@ def main():
     if rank == 0:
         frames_total = a.batch * a.steps * world
         value = frames_total / elapsed
-        dt_name = 'bf16' if dtype == torch.bfloat16 else 'f32'
+        dt_name = a.dtype
         enc = [m for m in msda if m[0] == m[1]]
         dec = [m for m in msda if m[0] != m[1]]
         msda_enc_ms = statistics.mean(m[2] for m in enc) if enc else None
@@ -223,8 +291,9 @@ def main():
             tot_ms = sum(m[2] for m in msda)
             tot_bytes = sum(m[3] for m in msda)
             ach = tot_bytes / (tot_ms * 1e-3) / 1e9
-            traffic, src = pmc_traffic(MSDA_KERNEL)
-            msda_roof = {'bound': 'hbm', 'kernel': MSDA_KERNEL + '<bf16_t, 4, 4> (encoder + decoder launches)',
+            traffic, src = pmc_traffic(MSDA_KERNEL) if a.workload == 'config2' else (None, None)
+            kname = MSDA_KERNEL + '<bf16_t, 4, 4>' if a.workload == 'config2' else 'msda_fused_kernel<f16_t, 4> (D=36)'
+            msda_roof = {'bound': 'hbm', 'kernel': kname + ' (encoder + decoder launches)',
                          'achieved': ach, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': ach / HBM_PEAK_GBS,
                          'traffic': traffic, 'traffic_source': src,
                          'algorithmic_bytes_per_launch': tot_bytes / len(msda),
@@ -244,8 +313,7 @@ def main():
             'ms_per_step': elapsed / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': dt_name,
             'data': 'synthetic N(0,1) 3x%dx%d frames, random-init weights (reference init)' % (a.height, a.width),
-            'config': {'workload': 'config2 cfgs/train_deformable.yaml: R-50 Deformable-DETR inference forward, '
-                                   'd=256, 4 levels, 6/6 layers, 300 queries, box refine',
+            'config': {'workload': wl['desc'],
                        'frames_per_gpu_per_step': a.batch, 'in_flight_batches': nst,
                        'frame': [3, a.height, a.width],
                        'parallelism': f'replicas x{world}'},
