@@ -26,6 +26,7 @@
 
 #include "../../include/kinet_msda.h"
 #include "common.h"
+#include "msda_util.h"
 
 namespace kinet {
 namespace {
@@ -36,11 +37,6 @@ constexpr int kMaxLevels = 16;
 // diagnostic flags (kinet_msda_set_flags): bit 0 = never use msda_fused_fast_kernel; bit 1 = its
 // 4-head x 4-sample-group variant, bit 2 = 4 heads x 2 (the default is 2 heads x 2; timing studies)
 int msda_flags = 0;
-
-template <typename T, int VEC>
-struct alignas(sizeof(T) * VEC) VecT {
-    T v[VEC];
-};
 
 struct LevelInfo {
     int start[kMaxLevels];
@@ -479,30 +475,6 @@ struct FastLevels {
     int start[kMaxLevels], H[kMaxLevels], W[kMaxLevels], ok[kMaxLevels];
     float Hf[kMaxLevels], Wf[kMaxLevels], rH[kMaxLevels], rW[kMaxLevels];
 };
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-
-// acc += f16(half of x) * f16(half of w) in f32 (both multiplicands 16-bit sources)
-__device__ __forceinline__ float fma_mix16_lo_lo(float acc, uint32_t x, uint32_t w) {
-    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(x), "v"(w));
-    return acc;
-}
-__device__ __forceinline__ float fma_mix16_lo_hi(float acc, uint32_t x, uint32_t w) {
-    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(x), "v"(w));
-    return acc;
-}
-__device__ __forceinline__ float fma_mix16_hi_lo(float acc, uint32_t x, uint32_t w) {
-    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(x), "v"(w));
-    return acc;
-}
-__device__ __forceinline__ float fma_mix16_hi_hi(float acc, uint32_t x, uint32_t w) {
-    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(x), "v"(w));
-    return acc;
-}
-__device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, (f16_t)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (f16_t)b) << 16);
-}
 
 // acc += f16(lo or hi half of x) * w in f32 -- one v_fma_mix_f32, no separate widening
 __device__ __forceinline__ float fma_mix_lo(float acc, uint32_t x, float w) {
