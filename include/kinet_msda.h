@@ -91,31 +91,6 @@ int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_
                              int value_dtype, int output_dtype, int offlog_dtype,
                              const int32_t* query_tile_order, kinet_stream_t stream);
 
-/* Encoder-call specialisation of kinet_msda_fused_forward (deformable_transformer.py:290-299:
- * the queries are the S pixels of the value levels, Lq == S, in level_start order).  A
- * workgroup owns one head and a 4 x 16 tile of query pixels; per level it stages the
- * bounding-box window of its samples' corners (up to 512 pixels) in LDS and gathers the
- * bilinear corners from there, falling back to global loads for samples outside the window.
- * Same arguments and results as kinet_msda_fused_forward with num_query = spatial_size,
- * except: head-major f16 values (value_ss = head_dim), head_dim 32, 4 levels, 4 points;
- * host_spatial_shapes is a HOST copy of spatial_shapes (it sizes the grid); tile_order is an
- * optional permutation of the kinet_msda_encoder_tiles() tiles (level-major, row-major
- * 4 x 16 tiles per level) giving their processing order. */
-int kinet_msda_encoder_forward(const void* value, int64_t value_sb, int64_t value_sm,
-                               const int64_t* host_spatial_shapes,
-                               const void* offsets_logits, int ld_off,
-                               const float* ref_points, int ref_dim,
-                               const uint8_t* query_attn_mask,
-                               void* output, float* loc_out, float* attw_out,
-                               int batch, int spatial_size, int num_heads, int channels,
-                               int num_levels, int num_point,
-                               int value_dtype, int output_dtype, int offlog_dtype,
-                               const int32_t* tile_order, kinet_stream_t stream);
-
-/* Number of query tiles of kinet_msda_encoder_forward for these (host) shapes; -1 if the
- * level count is not supported. */
-int kinet_msda_encoder_tiles(const int64_t* host_spatial_shapes, int num_levels);
-
 /* Diagnostic kernel-selection knob (no reference counterpart): bit 0 = never use the
  * specialised 16-bit / head_dim-32 fused kernel.  Returns the previous flags. */
 int kinet_msda_set_flags(int flags);

@@ -24,8 +24,6 @@ _SIGS = {
     'kinet_msda_backward_workspace_bytes': [I] * 5,
     'kinet_msda_set_flags': [I],
     'kinet_msda_fused_forward': [P, I64, I64, I64, P, P, I, P, I, P, P, P, P] + [I] * 10 + [P, P],
-    'kinet_msda_encoder_forward': [P, I64, I64, P, P, I, P, I, P, P, P, P] + [I] * 9 + [P, P],
-    'kinet_msda_encoder_tiles': [P, I],
     'kinet_gemm_set_flags': [I],
     'kinet_gemm_force_tile': [I, I],
     'kinet_gemm_headmajor': [P, P, P] + [I] * 7 + [P, P, I, I, P],

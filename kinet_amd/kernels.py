@@ -423,80 +423,6 @@ def encoder_tile_order(shapes, device, qt=16):
     return o
 
 
-_enc_plans = {}
-ENCODER_KERNEL = True   # diagnostic switch (tools/bench_msda.py --no-enc): route encoder calls to msda_fused
-
-
-def encoder_plan(shapes, device):
-    """Host shapes + processing order of kinet_msda_encoder_forward's 4x16 query tiles, cached
-    per (shapes, device).  Tiles run sorted by the normalised image row of their centre, so
-    the tiles of all levels that sample one image band run together and share its value rows
-    in L2 (the level-major order would sweep the image once per level)."""
-    key = (tuple(tuple(int(v) for v in s) for s in shapes), str(device))
-    plan = _enc_plans.get(key)
-    if plan is None:
-        import numpy as np
-        hs = torch.tensor(key[0], dtype=torch.int64).contiguous()
-        ys = []
-        for h, w in key[0]:
-            ty = np.arange((h + 3) // 4)
-            tx = (w + 15) // 16
-            ys.append(np.repeat((ty * 4 + 2.0) / max(h, 1), tx))
-        y = np.concatenate(ys) if ys else np.zeros(0)
-        n = N.lib().kinet_msda_encoder_tiles(N.ptr(hs), len(key[0]))
-        if n != len(y):
-            raise RuntimeError(f'encoder_plan: tile count mismatch ({n} vs {len(y)})')
-        order = torch.as_tensor(np.argsort(y, kind='stable').astype(np.int32), device=device)
-        plan = {'host_shapes': hs, 'order': order, 'tiles': n}
-        _enc_plans[key] = plan
-    return plan
-
-
-def encoder_supported(value, n_levels, n_points, head_major):
-    return (ENCODER_KERNEL and head_major and value.dtype == torch.float16 and value.shape[-1] == 32
-            and n_levels == 4 and n_points == 4)
-
-
-def msda_encoder(value, plan, offlog, reference_points, n_heads, query_attn_mask=None, want_loc_attw=False,
-                 out_dtype=None):
-    """Encoder call of MSDeformAttn.forward (queries = the pixels of the value levels,
-    deformable_transformer.py:290-299) through kinet_msda_encoder_forward: value head-major
-    (M, B, S, 32) f16 from value_proj_headmajor, offlog (B, S, M*L*P*3) f16/f32,
-    reference_points (B, S, 4, 2|4) f32.  Same results contract as msda_fused."""
-    M_, B, S, D = value.shape
-    if M_ != n_heads:
-        raise RuntimeError(f'head-major value has {M_} heads, module expects {n_heads}')
-    if value.stride(-1) != 1 or value.stride(2) != D or value.data_ptr() % 16:
-        value = value.contiguous()
-    if offlog.shape[1] != S:
-        raise RuntimeError('msda_encoder: the encoder queries are the S value pixels')
-    offlog = offlog.contiguous()
-    ref = reference_points.float().contiguous()
-    L = plan['host_shapes'].shape[0]
-    od = out_dtype or value.dtype
-    out = torch.empty((B, S, M_ * D), dtype=od, device=value.device)
-    loc = attw = None
-    if want_loc_attw:
-        loc = torch.empty((B, S, M_, L, 4, 2), dtype=torch.float32, device=value.device)
-        attw = torch.empty((B, S, M_, L, 4), dtype=torch.float32, device=value.device)
-    qm = query_attn_mask.to(torch.uint8).contiguous() if query_attn_mask is not None else None
-    order = plan['order']
-    if order.device != value.device:
-        raise RuntimeError('msda_encoder: plan built for another device')
-    nsamp = B * S * M_ * L * 4
-    N.call('kinet_msda_encoder_forward', N.ptr(value), value.stride(1), value.stride(0), N.ptr(plan['host_shapes']),
-           N.ptr(offlog), offlog.shape[-1], N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), N.ptr(loc),
-           N.ptr(attw), B, S, M_, D, L, 4, N.dtype_code(value.dtype), N.dtype_code(od), N.dtype_code(offlog.dtype),
-           N.ptr(order), N.stream(value.device),
-           work={'family': 'msda', 'flops': 10.0 * nsamp * D,
-                 'bytes': B * S * M_ * D * value.element_size() + nsamp * 3 * offlog.element_size() + ref.numel() * 4
-                 + B * S * M_ * D * out.element_size() + (nsamp * 3 * 4 if want_loc_attw else 0),
-                 'Lq': S, 'S': S, 'shape': (B, S, S)})
-    if want_loc_attw:
-        return out, loc, attw
-    return out
-
-
 def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_levels, n_points,
                query_attn_mask=None, want_loc_attw=False, head_major=False, out_dtype=None,
                query_tile_order=None):

@@ -95,22 +95,19 @@ class DeformableTransformerEncoderLayer(nn.Module):
         src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
         return self.norm2(src + self.dropout3(src2))
 
-    def forward(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None,
-                encoder_plan=None):
+    def forward(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None):
         if fast_path(self):
-            return self.forward_fast(src, pos, reference_points, spatial_shapes, padding_mask, query_order,
-                                     encoder_plan)
+            return self.forward_fast(src, pos, reference_points, spatial_shapes, padding_mask, query_order)
         src2 = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, spatial_shapes, padding_mask)
         src = self.norm1(src + self.dropout1(src2))
         return self.forward_ffn(src)
 
-    def forward_fast(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None,
-                     encoder_plan=None):
+    def forward_fast(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None):
         # deformable_transformer.py:290-299, one kernel per step
         a = self.self_attn
         value = a.project_value(src, padding_mask)                                     # head-major
         samp = a.sample(src, reference_points, value, spatial_shapes, query_add=pos,   # (src+pos) @ W
-                        query_order=query_order, encoder_plan=encoder_plan)
+                        query_order=query_order)
         n1, n2 = self.norm1, self.norm2
         src = K.linear(samp, a.output_proj.weight, a.output_proj.bias, residual=src, ln=(n1.weight, n1.bias, n1.eps))
         if K.ffn_supported(src, self.linear1, self.linear2):
@@ -141,7 +138,7 @@ class DeformableTransformerEncoder(nn.Module):
         return reference_points[:, :, None] * valid_ratios[:, None]
 
     def forward(self, src, spatial_shapes, valid_ratios, pos=None, padding_mask=None, reference_points=None,
-                query_order=None, encoder_plan=None):
+                query_order=None):
         output = src
         if reference_points is None:
             shapes = spatial_shapes.tolist() if torch.is_tensor(spatial_shapes) else spatial_shapes
@@ -149,8 +146,7 @@ class DeformableTransformerEncoder(nn.Module):
         if not torch.is_tensor(spatial_shapes):
             spatial_shapes = torch.as_tensor(spatial_shapes, dtype=torch.long, device=src.device)
         for layer in self.layers:
-            output = layer(output, pos, reference_points, spatial_shapes, padding_mask, query_order=query_order,
-                           encoder_plan=encoder_plan)
+            output = layer(output, pos, reference_points, spatial_shapes, padding_mask, query_order=query_order)
         return output
 
 
@@ -391,12 +387,10 @@ class DeformableTransformer(nn.Module):
                 vr = valid_ratios[:, sl_lv]
                 geo['enc'].append(dict(shapes=sh, spatial_shapes=geo['spatial_shapes'][sl_lv].contiguous(),
                                        valid_ratios=vr, tok=sl_tok, order=K.encoder_tile_order(sh, device),
-                                       plan=K.encoder_plan(sh, device) if len(sh) == 4 else None,
                                        ref=DeformableTransformerEncoder.get_reference_points(sh, vr, device)))
         else:
             geo['enc'] = [dict(shapes=geo['shapes'], spatial_shapes=geo['spatial_shapes'], valid_ratios=valid_ratios,
                                tok=slice(0, None), order=K.encoder_tile_order(geo['shapes'], device),
-                               plan=K.encoder_plan(geo['shapes'], device) if L == 4 else None,
                                ref=DeformableTransformerEncoder.get_reference_points(geo['shapes'], valid_ratios,
                                                                                      device))]
         return geo
@@ -415,7 +409,7 @@ class DeformableTransformer(nn.Module):
                 src, pos = src.contiguous(), pos.contiguous()
                 pm = pm.contiguous() if pm is not None else None
             encs.append(self.encoder(src, e['spatial_shapes'], e['valid_ratios'], pos, pm, reference_points=e['ref'],
-                                     query_order=e.get('order'), encoder_plan=e.get('plan')))
+                                     query_order=e.get('order')))
         if len(encs) == 2:
             prev_memory, memory = encs
             memory = torch.cat([memory, prev_memory], 1)   # [current, prev] -- reference order (:173)

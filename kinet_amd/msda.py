@@ -115,21 +115,16 @@ class MSDeformAttn(nn.Module):
         return w, b
 
     def sample(self, query, reference_points, value, input_spatial_shapes, query_attn_mask=None, query_add=None,
-               query_order=None, encoder_plan=None):
+               query_order=None):
         """value already projected: head-major (M, N, S, D) from project_value (or a
         row-major (N, S, d) tensor); the offsets/weights projection input is query
         (+ query_add, e.g. the position embedding, added at GEMM load time); returns the
-        pre-output_proj (N, Lq, d).  encoder_plan (kernels.encoder_plan): the queries are
-        the pixels of the value levels -- use the LDS-window encoder kernel when it applies."""
+        pre-output_proj (N, Lq, d)."""
         w, b = self.packed_offsets_weights()
         # bf16 compute: offsets/logits in f16 (half the bytes of f32 through HBM twice; f16
         # keeps 11 mantissa bits for the pixel offsets); parity mode stays f32
         od = torch.float16 if query.dtype == torch.bfloat16 else torch.float32
         offlog = K.linear(query, w, b, out_dtype=od, x_add=query_add)
-        if encoder_plan is not None and K.encoder_supported(value, self.n_levels, self.n_points, value.dim() == 4):
-            # encoder call: queries are the value pixels -> LDS-window kernel (csrc/msda_enc.hip)
-            return K.msda_encoder(value, encoder_plan, offlog, reference_points, self.n_heads, query_attn_mask,
-                                  out_dtype=query.dtype)
         return K.msda_fused(value, input_spatial_shapes, offlog, reference_points,
                             self.n_heads, self.n_levels, self.n_points, query_attn_mask,
                             head_major=(value.dim() == 4), out_dtype=query.dtype, query_tile_order=query_order)

@@ -253,97 +253,3 @@ def test_fast_fused_query_tile_order_invariant():
                               out_dtype=torch.bfloat16, query_tile_order=order)
     torch.cuda.synchronize()
     assert torch.equal(o0, o1) and torch.equal(l0, l1) and torch.equal(a0, a1)
-
-
-# ---- encoder-call kernel (LDS windows, csrc/msda_enc.hip) vs the fast gather kernel ----
-
-def _encoder_inputs(B, shapes, M, P, ref_dim, noise, seed, valid=None, pattern=True):
-    """Encoder-call inputs: queries = the pixels of the levels, reference points at the pixel
-    centres (deformable_transformer.py:309-321, optionally scaled by valid ratios), offsets =
-    the reference init's 8-direction grid (ms_deform_attn.py:35-41) plus `noise` units."""
-    import math
-    g = torch.Generator().manual_seed(seed)
-    L = len(shapes)
-    S = sum(h * w for h, w in shapes)
-    value = torch.randn(M, B, S, 32, generator=g).to(torch.float16)
-    refs = []
-    for h, w in shapes:
-        ys, xs = torch.meshgrid(torch.arange(h) + 0.5, torch.arange(w) + 0.5, indexing='ij')
-        refs.append(torch.stack([xs.reshape(-1) / w, ys.reshape(-1) / h], -1))
-    ref = torch.cat(refs, 0)[None, :, None, :].expand(B, S, L, 2).clone()
-    if valid is not None:
-        ref = ref * torch.tensor(valid).view(B, 1, 1, 2)
-    if ref_dim == 4:
-        ref = torch.cat([ref, torch.rand(B, S, L, 2, generator=g) * 0.3 + 0.02], -1)
-    off = torch.zeros(B, S, M, L, P, 2)
-    if pattern:
-        th = torch.arange(M, dtype=torch.float32) * (2.0 * math.pi / M)
-        grid = torch.stack([th.cos(), th.sin()], -1)
-        grid = grid / grid.abs().max(-1, keepdim=True)[0]
-        off += grid.view(1, 1, M, 1, 1, 2) * (torch.arange(P) + 1.0).view(1, 1, 1, 1, P, 1)
-    off += noise * torch.randn(off.shape, generator=g)
-    logits = torch.randn(B, S, M * L * P, generator=g)
-    offlog = torch.cat([off.reshape(B, S, -1), logits], -1).half()
-    qmask = torch.rand(B, S, generator=g) < 0.05
-    ss = torch.tensor(shapes, dtype=torch.int64)
-    return [t.cuda() for t in (value, ss, offlog, ref, qmask)]
-
-
-@pytest.mark.parametrize('shapes,ref_dim,noise,valid', [
-    (((40, 67), (20, 34), (10, 17), (5, 9)), 2, 0.0, None),           # reference-init pattern: all in-window
-    (((40, 67), (20, 34), (10, 17), (5, 9)), 2, 1.5, [[1, 1], [0.8, 0.7]]),   # jitter + valid ratios
-    (((37, 61), (19, 31), (10, 16), (5, 8)), 2, 12.0, None),          # large offsets: clipped windows, global path
-    (((13, 9), (7, 5), (4, 3), (2, 2)), 2, 3.0, None),                 # ragged levels smaller than a tile
-    (((40, 67), (20, 34), (10, 17), (5, 9)), 4, 2.0, None),           # 4-d reference boxes
-])
-@pytest.mark.parametrize('out_dtype', [torch.bfloat16, torch.float16])
-def test_encoder_kernel_bit_identical_to_gather_kernel(shapes, ref_dim, noise, valid, out_dtype):
-    """Same per-sample arithmetic and accumulation order as msda_fused_fast_kernel: locations and
-    attention weights equal to f32 rounding (the softmax sums 4 + 4 + 4 + 4 across a lane quad
-    instead of a 16-lane butterfly; fma contraction); outputs differ on < 0.2 % of the elements, by one
-    16-bit output ulp or by ~1e-4 absolute where the sum cancels (the compiler contracts the
-    bilinear-fraction arithmetic differently in the two kernels, moving a few f16 corner
-    weights by one f16 ulp; both kernels are equally far from the C oracle,
-    tools/enc_diff_probe.py), whichever samples take the LDS window and whichever fall back to
-    global loads.  An indexing error would show as O(0.1..1) differences."""
-    from kinet_amd import kernels as K
-    B, M, P = 2, 8, 4
-    value, ss, offlog, ref, qmask = _encoder_inputs(B, shapes, M, P, ref_dim, noise, 31 + int(noise), valid)
-    plan = K.encoder_plan(shapes, value.device)
-    o0, l0, a0 = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, want_loc_attw=True, head_major=True,
-                              out_dtype=out_dtype)
-    o1, l1, a1 = K.msda_encoder(value, plan, offlog, ref, M, qmask, want_loc_attw=True, out_dtype=out_dtype)
-    torch.cuda.synchronize()
-    torch.testing.assert_close(l1, l0, rtol=1e-6, atol=1e-7)
-    torch.testing.assert_close(a1, a0, rtol=2e-6, atol=1e-8)
-    ulp = 2.0 ** -10 if out_dtype == torch.float16 else 2.0 ** -7
-    d = (o0.float() - o1.float()).abs()
-    assert (d <= torch.maximum(o0.float().abs(), o1.float().abs()) * 2 * ulp + 1e-3).all(), d.max().item()
-    assert (d > 0).float().mean().item() < 2e-3
-
-
-def test_encoder_kernel_vs_oracle():
-    """The encoder kernel against the C oracle (through the loc / attw it reports), large
-    offsets so windows are clipped and part of the samples leave the image."""
-    from kinet_amd import kernels as K
-    from oracle import msda_oracle as O
-    shapes = ((24, 40), (12, 20), (6, 10), (3, 5))
-    B, M, P = 2, 8, 4
-    value, ss, offlog, ref, qmask = _encoder_inputs(B, shapes, M, P, 2, 6.0, 77)
-    out, loc, aw = K.msda_encoder(value, K.encoder_plan(shapes, value.device), offlog, ref, M, qmask,
-                                  want_loc_attw=True, out_dtype=torch.float16)
-    torch.cuda.synchronize()
-    v = value.float().permute(1, 2, 0, 3).contiguous().cpu().numpy()
-    ref_out = torch.from_numpy(O.fwd(v, ss.cpu().numpy(), loc.cpu().numpy(), aw.cpu().numpy())).reshape(out.shape)
-    d = (out.float().cpu() - ref_out).abs()
-    # f16 tap weights and f16 output rounding
-    assert (d <= 2e-3 * ref_out.abs() + 2e-3).all(), d.max().item()
-    assert (out.float()[qmask] == 0).all()
-
-
-def test_encoder_plan_order_is_a_permutation():
-    from kinet_amd import kernels as K
-    shapes = ((100, 167), (50, 84), (25, 42), (13, 21))
-    plan = K.encoder_plan(shapes, torch.device('cuda'))
-    n = sum(((h + 3) // 4) * ((w + 15) // 16) for h, w in shapes)
-    assert plan['tiles'] == n and sorted(plan['order'].tolist()) == list(range(n))

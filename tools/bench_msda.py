@@ -71,7 +71,6 @@ def main():
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--order', action='store_true', help='encoder tile order (kernels.encoder_tile_order)')
     ap.add_argument('--flags', type=int, default=0, help='kinet_msda_set_flags value (kernel variants)')
-    ap.add_argument('--enc', action='store_true', help='encoder-call LDS-window kernel (kernels.msda_encoder)')
     a = ap.parse_args()
     if a.flags:
         from kinet_amd import _native
@@ -82,9 +81,6 @@ def main():
     order = K.encoder_tile_order(ss.tolist(), value.device) if a.order and not a.decoder else None
     fn = lambda: K.msda_fused(value, ss, offlog, ref, M, L, P, head_major=True, out_dtype=torch.bfloat16,   # noqa: E731
                               query_tile_order=order)
-    if a.enc and not a.decoder:
-        plan = K.encoder_plan(ss.tolist(), value.device)
-        fn = lambda: K.msda_encoder(value, plan, offlog, ref, M, out_dtype=torch.bfloat16)   # noqa: E731
     ms = time_call(fn, a.iters)
     B, Lq = offlog.shape[:2]
     S = value.shape[2]
@@ -92,7 +88,7 @@ def main():
     gathered = nsamp * 4 * value.shape[-1] * value.element_size()
     compulsory = value.numel() * value.element_size() + offlog.numel() * 4 + ref.numel() * 4 + \
         B * Lq * M * value.shape[-1] * value.element_size()
-    print(f'[flags {a.flags}{" enc" if a.enc else ""}] msda {"decoder" if a.decoder else "encoder"} B={B} Lq={Lq} S={S} noise={a.noise}: {ms * 1e3:.1f} us/call  '
+    print(f'[flags {a.flags}] msda {"decoder" if a.decoder else "encoder"} B={B} Lq={Lq} S={S} noise={a.noise}: {ms * 1e3:.1f} us/call  '
           f'compulsory {compulsory / ms / 1e6:.0f} GB/s  gathered {gathered / ms / 1e6:.0f} GB/s')
 
 
