@@ -1,0 +1,80 @@
+/* kinet_amd C-ABI: backward-pass kernels of the training path.
+ *
+ * The reference trains with losses.backward() (src/trackformer/engine.py:145-149), i.e. the
+ * autograd of torch's Conv2d / Linear / LayerNorm / GroupNorm / MultiheadAttention modules
+ * (cuDNN / cuBLAS / ATen) around the MSDeformAttn CUDA backward (ms_deform_attn_cuda.cu:
+ * 89-168, replaced by kinet_msda_backward, kinet_msda.h).  kinet_amd/autograd.py wires these
+ * kernels into torch.autograd.Functions; the forward halves reuse kinet_gemm.h / kinet_ops.h.
+ * Conventions as in kinet_common.h (device pointers, caller's stream, caller workspace, int
+ * status).  Every reduction runs in a fixed order (no float atomics): gradients are
+ * bit-identical across reruns.
+ */
+#ifndef KINET_GRAD_H_
+#define KINET_GRAD_H_
+
+#include "kinet_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* dst (cols x rows, row stride ld_dst) = src^T (src rows x cols, row stride ld_src); 2/4-byte
+ * element types (F32, BF16, F16). */
+int kinet_transpose(const void* src, void* dst, int rows, int cols, int64_t ld_src, int64_t ld_dst,
+                    int dtype, kinet_stream_t stream);
+
+/* Patch matrix of an NHWC convolution (torch Conv2d geometry, backbone.py / deformable_detr.py:63-71):
+ *   cols[(n*Ho + ho)*Wo + wo][(kh*KW + kw)*C + c] = x[n][ho*sh - ph + kh][wo*sw - pw + kw][c]
+ * (0 outside the image); C % 4 == 0. */
+int kinet_im2col_nhwc(const void* x, void* cols, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW,
+                      int sh, int sw, int ph, int pw, int dtype, kinet_stream_t stream);
+
+/* Adjoint of kinet_im2col_nhwc (the input gradient of the convolution given the gradient of
+ * its patch matrix): dx[n][h][w][c] = sum of the cols entries that read x[n][h][w][c], summed
+ * per pixel in (kh, kw) order; dx fully overwritten. */
+int kinet_col2im_nhwc(const void* cols, void* dx, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW,
+                      int sh, int sw, int ph, int pw, int dtype, kinet_stream_t stream);
+
+/* C (M x N, f32, row stride ldc) = A^T B (+ C if accumulate), A (K x M) and B (K x N) row-major
+ * in dtype (F32: exact-f32 MFMA; BF16/F16 widened to f32).  The weight gradient of a Linear
+ * (dW = dY^T X) and of a convolution (dW = dZ^T im2col(X)).  Split over K when the output has
+ * few tiles: `workspace` must then hold kinet_gemm_tn_workspace(M, N, K) floats (0 = none
+ * needed; accumulate always needs at least M*N). */
+int64_t kinet_gemm_tn_workspace(int M, int N, int K);
+int kinet_gemm_tn(const void* A, const void* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                  int64_t ldc, int dtype, int accumulate, float* workspace, kinet_stream_t stream);
+
+/* out[c] (+)= sum_r A[r*lda + c] (f32): bias gradients.  workspace: kinet_colsum_workspace floats. */
+int64_t kinet_colsum_workspace(int rows, int cols);
+int kinet_colsum(const void* A, float* out, int rows, int cols, int64_t lda, int dtype, int accumulate,
+                 float* workspace, kinet_stream_t stream);
+
+/* nn.LayerNorm backward over the last dim d <= 1024 (statistics recomputed from x):
+ * dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma; dgamma = sum dy*xhat,
+ * dbeta = sum dy (either may be NULL).  workspace: kinet_layernorm_backward_workspace floats. */
+int64_t kinet_layernorm_backward_workspace(int rows, int d);
+int kinet_layernorm_backward(const void* dy, const void* x, const float* gamma, void* dx, float* dgamma,
+                             float* dbeta, int rows, int d, float eps, int dtype, float* workspace,
+                             kinet_stream_t stream);
+
+/* nn.GroupNorm(groups, C) backward on NHWC (N, HW, C) input (the forward is kinet_groupnorm).
+ * workspace: kinet_groupnorm_backward_workspace floats. */
+int64_t kinet_groupnorm_backward_workspace(int N, int HW, int C, int groups);
+int kinet_groupnorm_backward(const void* dy, const void* x, const float* gamma, void* dx, float* dgamma,
+                             float* dbeta, int N, int HW, int C, int groups, float eps, int dtype,
+                             float* workspace, kinet_stream_t stream);
+
+/* Backward of kinet_mha_core (f32): given Q, K, V (row strides ld*), dO, writes dQ, dK, dV
+ * (same layouts and strides as Q, K, V).  head_dim <= 64.  workspace:
+ * kinet_mha_backward_workspace floats (the probabilities and their gradient). */
+int64_t kinet_mha_backward_workspace(int batch, int Lq, int Lk, int heads);
+int kinet_mha_backward(const float* Q, int ldq, const float* K, int ldk, const float* V, int ldv,
+                       const float* dO, int ldo, float* dQ, float* dK, float* dV, int batch, int Lq, int Lk,
+                       int heads, int head_dim, float scale, const uint8_t* key_mask, float* workspace,
+                       kinet_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KINET_GRAD_H_ */

@@ -46,12 +46,29 @@ _SIGS = {
     'kinet_mha_core': [P, I, P, I, P, I, P, I] + [I] * 5 + [F, I, P, P],
     'kinet_add': [P, P, P, I64, I, P],
     'kinet_box_refine': [P, P, I, P, P, P, I, I, I, P],
+    'kinet_transpose': [P, P, I, I, I64, I64, I, P],
+    'kinet_im2col_nhwc': [P, P] + [I] * 13 + [P],
+    'kinet_col2im_nhwc': [P, P] + [I] * 13 + [P],
+    'kinet_gemm_tn_workspace': [I, I, I],
+    'kinet_gemm_tn': [P, P, P, I, I, I, I64, I64, I64, I, I, P, P],
+    'kinet_colsum_workspace': [I, I],
+    'kinet_colsum': [P, P, I, I, I64, I, I, P, P],
+    'kinet_layernorm_backward_workspace': [I, I],
+    'kinet_layernorm_backward': [P, P, P, P, P, P, I, I, F, I, P, P],
+    'kinet_groupnorm_backward_workspace': [I, I, I, I],
+    'kinet_groupnorm_backward': [P, P, P, P, P, P, I, I, I, I, F, I, P, P],
+    'kinet_mha_backward_workspace': [I, I, I, I],
+    'kinet_mha_backward': [P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, F, P, P, P],
     'kinet_last_error': [],
     'kinet_version': [],
 }
 _RESTYPES = {'kinet_last_error': ctypes.c_char_p, 'kinet_version': ctypes.c_char_p,
              'kinet_msda_backward_workspace_bytes': ctypes.c_int64,
-             'kinet_groupnorm_workspace': ctypes.c_long}
+             'kinet_groupnorm_workspace': ctypes.c_long,
+             'kinet_gemm_tn_workspace': ctypes.c_int64, 'kinet_colsum_workspace': ctypes.c_int64,
+             'kinet_layernorm_backward_workspace': ctypes.c_int64,
+             'kinet_groupnorm_backward_workspace': ctypes.c_int64,
+             'kinet_mha_backward_workspace': ctypes.c_int64}
 
 DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
 

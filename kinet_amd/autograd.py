@@ -1,0 +1,226 @@
+"""Training-path operators on kinet_amd kernels: torch.autograd.Functions whose forward AND
+backward run the hand-written HIP kernels (include/kinet_gemm.h, kinet_ops.h, kinet_grad.h).
+
+The reference trains the detector with `losses.backward()` (src/trackformer/engine.py:
+145-149) through torch's Conv2d / Linear / LayerNorm / GroupNorm / MultiheadAttention
+(cuDNN / cuBLAS); kinet_amd's autograd path (DeformableDETR._forward_reference and the
+transformer / backbone modules under autograd) calls these functions instead, so a
+training step runs no vendor GEMM / convolution library kernel.  Compute dtype is f32, as
+the reference trains (no AMP anywhere in src/); elementwise glue (ReLU masks, adds,
+sigmoid, dropout, softmax of the sampling weights) stays in torch.
+
+    linear(x, weight, bias)                 nn.Linear
+    layer_norm(x, weight, bias, eps)        nn.LayerNorm over the last dim
+    group_norm_nhwc(x, groups, w, b, eps)   nn.GroupNorm on (B, HW, C)
+    conv_nhwc(x, weight, ...)               nn.Conv2d (+ FrozenBatchNorm2d, residual, ReLU) on NHWC
+    mha_core(q, k, v, heads, key_mask)      the softmax(QK^T / sqrt(d)) V core of nn.MultiheadAttention
+
+Weight gradients are reductions over the row (pixel / token) dimension (kinet_gemm_tn,
+split-K with a fixed-order finalize), input gradients are GEMMs against the transposed
+weight (kinet_gemm_ex) -- for convolutions against the patch matrix, scattered back by
+the deterministic kinet_col2im_nhwc gather.
+"""
+import torch
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+
+from kinet_amd import _native as N
+from kinet_amd import kernels as K
+
+
+def _f32(t):
+    if t.dtype != torch.float32:
+        raise RuntimeError(f'kinet_amd training path computes in f32 (got {t.dtype})')
+    return t
+
+
+# ----------------------------------------------------------------------------- Linear
+class _Linear(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        N.require_gpu(x)
+        _f32(x)
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.stride(-1) != 1 or x2.stride(0) != x2.shape[1]:
+            x2 = x2.contiguous()
+        y = K.linear(x2, weight.detach(), None if bias is None else bias.detach())
+        ctx.save_for_backward(x2, weight)
+        ctx.has_bias = bias is not None
+        ctx.lead = lead
+        return y.view(*lead, weight.shape[0])
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous().float()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wt = K.transpose2d(weight.detach().float())                 # (in, out)
+            n_out = dy2.shape[1]
+            if n_out % 8:   # the GEMM's K (= out features, e.g. 20 class logits) must be 8-aligned
+                pad = 8 - n_out % 8
+                dy_p, wt = torch.nn.functional.pad(dy2, (0, pad)), torch.nn.functional.pad(wt, (0, pad))
+            else:
+                dy_p = dy2
+            dx = K.linear(dy_p, wt).view(*ctx.lead, x2.shape[1])        # dy @ W
+        if ctx.needs_input_grad[1]:
+            dw = K.gemm_tn(dy2, x2)                                     # dy^T x
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = K.colsum(dy2)
+        return dx, dw, db
+
+
+def linear(x, weight, bias=None):
+    """F.linear(x, weight, bias) on kinet kernels (forward and backward)."""
+    return _Linear.apply(x, weight, bias)
+
+
+def linear_module(x, mod):
+    return _Linear.apply(x, mod.weight, mod.bias)
+
+
+# ---------------------------------------------------------------------------- LayerNorm
+class _LayerNorm(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        _f32(x)
+        xc = x.contiguous()
+        y = K.layernorm(xc, weight.detach(), bias.detach(), eps)
+        ctx.save_for_backward(xc, weight)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        need_p = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        dx, dg, db = K.layernorm_backward(dy.contiguous().float(), x, weight, ctx.eps, need_params=need_p)
+        return (dx if ctx.needs_input_grad[0] else None, dg if ctx.needs_input_grad[1] else None,
+                db if ctx.needs_input_grad[2] else None, None)
+
+
+def layer_norm(x, ln):
+    """nn.LayerNorm `ln` applied to x (last dim)."""
+    return _LayerNorm.apply(x, ln.weight, ln.bias, float(ln.eps))
+
+
+# ---------------------------------------------------------------------------- GroupNorm
+class _GroupNormNHWC(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps):
+        _f32(x)
+        xc = x.contiguous()
+        y = K.groupnorm_nhwc(xc, weight.detach(), bias.detach(), groups, eps)
+        ctx.save_for_backward(xc, weight)
+        ctx.groups, ctx.eps = groups, eps
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        need_p = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        dx, dg, db = K.groupnorm_backward(dy.contiguous().float(), x, weight, ctx.groups, ctx.eps, need_params=need_p)
+        return (dx if ctx.needs_input_grad[0] else None, dg if ctx.needs_input_grad[1] else None,
+                db if ctx.needs_input_grad[2] else None, None, None)
+
+
+def group_norm_nhwc(x, gn):
+    """nn.GroupNorm `gn` on x (B, HW, C)."""
+    return _GroupNormNHWC.apply(x, gn.weight, gn.bias, gn.num_groups, float(gn.eps))
+
+
+# ------------------------------------------------------------------------------ Conv2d
+class _ConvNHWC(Function):
+    """y = relu?(conv(x, W) * scale + shift + residual), NHWC; scale/shift: a folded
+    FrozenBatchNorm2d (constants) or (None, conv bias)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, stride, pad, scale, shift, relu):
+        _f32(x)
+        x = x.contiguous()
+        wp = K.pack_conv_weight(weight, torch.float32)                       # (O, KH, KW, I)
+        sh = shift if bias is None else bias.detach().float().contiguous()
+        y = K.conv2d_nhwc(x, wp, stride, pad, scale=scale, bias=sh, relu=relu,
+                          residual=None if residual is None else residual.contiguous())
+        ctx.save_for_backward(x, weight, y if relu else None)
+        ctx.conf = (stride, pad, scale, relu, bias is not None, residual is not None)
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        x, weight, y = ctx.saved_tensors
+        stride, pad, scale, relu, has_bias, has_res = ctx.conf
+        dz = dy.contiguous().float()
+        if relu:
+            dz = dz.masked_fill(y <= 0, 0.0)
+        d_res = dz if has_res and ctx.needs_input_grad[3] else None
+        dzs = dz * scale if scale is not None else dz                       # through the folded BN scale
+        O, I, KH, KW = weight.shape
+        B, H, W, _ = x.shape
+        Ho, Wo = dz.shape[1], dz.shape[2]
+        dz2 = dzs.reshape(B * Ho * Wo, O)
+        s = (stride, stride) if isinstance(stride, int) else stride
+        p = (pad, pad) if isinstance(pad, int) else pad
+        pointwise = KH == 1 and KW == 1 and s == (1, 1) and p == (0, 0)
+        dx = dw = db = None
+        if ctx.needs_input_grad[1]:
+            cols = x.reshape(B * H * W, I) if pointwise else K.im2col_nhwc(x, KH, KW, s, p)
+            dw = K.gemm_tn(dz2, cols).view(O, KH, KW, I).permute(0, 3, 1, 2).contiguous()
+        if ctx.needs_input_grad[0]:
+            wpt = K.transpose2d(K.pack_conv_weight(weight, torch.float32).reshape(O, KH * KW * I))   # (KH*KW*I, O)
+            dcols = K.linear(dz2, wpt)                                                            # (P, KH*KW*I)
+            dx = dcols.view(B, H, W, I) if pointwise else K.col2im_nhwc(dcols, (B, H, W, I), KH, KW, s, p)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = K.colsum(dz2)
+        return dx, dw, db, d_res, None, None, None, None, None
+
+
+def conv_nhwc(x, weight, bias=None, stride=1, pad=0, scale=None, shift=None, relu=False, residual=None):
+    """Convolution of NHWC x with an OIHW weight (+ bias or folded-BN scale/shift, residual,
+    ReLU) on kinet kernels, differentiable w.r.t. x, weight, bias and residual."""
+    return _ConvNHWC.apply(x, weight, bias, residual, stride, pad, scale, shift, relu)
+
+
+# ---------------------------------------------------------------------------- attention
+class _MHACore(Function):
+    @staticmethod
+    def forward(ctx, q, k, v, heads, scale, key_mask):
+        _f32(q)
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        o = K.mha_core(q, k, v, heads, scale, key_mask=key_mask)
+        ctx.save_for_backward(q, k, v)
+        ctx.conf = (heads, scale, key_mask)
+        return o
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, do):
+        q, k, v = ctx.saved_tensors
+        heads, scale, key_mask = ctx.conf
+        dq, dk, dv = K.mha_backward(q, k, v, do.contiguous().float(), heads, scale, key_mask)
+        return dq, dk, dv, None, None, None
+
+
+def mha_core(q, k, v, heads, scale, key_mask=None):
+    """softmax(q k^T * scale, -inf at masked keys) v per head; q (B, Lq, E), k/v (B, Lk, E)."""
+    return _MHACore.apply(q, k, v, heads, scale, key_mask)
+
+
+def multihead_attention(mod, query, key, value, key_padding_mask=None):
+    """nn.MultiheadAttention(query, key, value, key_padding_mask)[0] for batch-first inputs
+    (the decoder self-attention, deformable_transformer.py:371, transposes to (L, B, E) and
+    back around the call): in_proj split q|k|v (torch's packed in_proj_weight layout),
+    attention core, out_proj.  Attention-probability dropout is not applied (the configured
+    training runs use it only through nn.MultiheadAttention's `dropout`)."""
+    E = mod.embed_dim
+    w, b = mod.in_proj_weight, mod.in_proj_bias
+    q = linear(query, w[:E], b[:E])
+    k = linear(key, w[E:2 * E], b[E:2 * E])
+    v = linear(value, w[2 * E:], b[2 * E:])
+    o = mha_core(q, k, v, mod.num_heads, mod.head_dim ** -0.5, key_padding_mask)
+    return linear(o, mod.out_proj.weight, mod.out_proj.bias)

@@ -1,0 +1,798 @@
+// Backward-pass kernels of the training path (gfx950 / CDNA4): what the reference's
+// losses.backward() (engine.py:145-149) runs through cuBLAS / cuDNN / ATen for the dense
+// layers of the detector, rebuilt as kinet_amd kernels (include/kinet_grad.h):
+//
+//  * kinet_gemm_tn     C (f32) [+]= A^T B for row-major A (K x M), B (K x N): the weight
+//                      gradients (dW = dY^T X of a Linear, dW = dZ^T im2col(X) of a conv) --
+//                      a reduction over the long row dimension, so split-K with a fixed-order
+//                      finalize (no float atomics); f32 operands on v_mfma_f32_16x16x4_f32 (the
+//                      exact-f32 MFMA: bit-for-bit an fma chain), 16-bit operands widened to f32;
+//  * kinet_transpose   (rows x cols) -> (cols x rows), LDS-tiled;
+//  * kinet_im2col_nhwc / kinet_col2im_nhwc: the patch matrix of an NHWC convolution and its
+//                      adjoint as a deterministic gather (every input pixel sums its <= KH*KW
+//                      taps in a fixed order);
+//  * kinet_colsum      bias gradients (column sums), fixed-order two-pass;
+//  * kinet_layernorm_backward / kinet_groupnorm_backward (nn.LayerNorm / nn.GroupNorm);
+//  * kinet_mha_backward: scaled-dot-product attention backward (nn.MultiheadAttention core,
+//                      deformable_transformer.py:371), probabilities recomputed from Q, K.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include <algorithm>
+
+#include "../../include/kinet_grad.h"
+#include "common.h"
+
+namespace kinet {
+namespace {
+
+template <typename T> __device__ __forceinline__ float ld(const T* p) { return to_f32(*p); }
+template <typename T> __device__ __forceinline__ void st(T* p, float v) { *p = Cvt<T>::from(v); }
+
+// ------------------------------------------------------------------------------ transpose
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ src, T* __restrict__ dst, int rows,
+                                                        int cols, long lds, long ldd) {
+    __shared__ T tile[32][33];
+    const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+    for (int i = 0; i < 32; i += 8) {
+        const int r = r0 + ty + i, c = c0 + tx;
+        if (r < rows && c < cols) tile[ty + i][tx] = src[(long)r * lds + c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 32; i += 8) {
+        const int c = c0 + ty + i, r = r0 + tx;
+        if (r < rows && c < cols) dst[(long)c * ldd + r] = tile[tx][ty + i];
+    }
+}
+
+// ----------------------------------------------------------------------- im2col / col2im
+struct ConvGeom {
+    int B, H, W, C, Ho, Wo, KH, KW, sh, sw, ph, pw;
+};
+
+// cols[p][(kh*KW + kw)*C + c] = x[n, ho*sh - ph + kh, wo*sw - pw + kw, c] (0 outside), 4 channels per thread
+template <typename T>
+__global__ __launch_bounds__(256) void im2col_kernel(const T* __restrict__ x, T* __restrict__ cols, ConvGeom g) {
+    const int C4 = g.C >> 2, taps = g.KH * g.KW;
+    const long total = (long)g.B * g.Ho * g.Wo * taps * C4;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int c4 = (int)(i % C4);
+        const long r = i / C4;
+        const int tap = (int)(r % taps);
+        const long p = r / taps;
+        const int wo = (int)(p % g.Wo);
+        const long r2 = p / g.Wo;
+        const int ho = (int)(r2 % g.Ho), n = (int)(r2 / g.Ho);
+        const int kh = tap / g.KW, kw = tap - kh * g.KW;
+        const int h = ho * g.sh - g.ph + kh, w = wo * g.sw - g.pw + kw;
+        T v[4];
+        if (h >= 0 && h < g.H && w >= 0 && w < g.W) {
+            const T* s = x + (((long)n * g.H + h) * g.W + w) * g.C + c4 * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = s[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = Cvt<T>::from(0.f);
+        }
+        T* d = cols + (p * taps + tap) * g.C + c4 * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = v[k];
+    }
+}
+
+// dx[n, h, w, c] = sum over taps (kh, kw) whose output pixel exists of cols[p(ho, wo)][tap, c]
+template <typename T>
+__global__ __launch_bounds__(256) void col2im_kernel(const T* __restrict__ cols, T* __restrict__ dx, ConvGeom g) {
+    const int C4 = g.C >> 2, taps = g.KH * g.KW;
+    const long total = (long)g.B * g.H * g.W * C4;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int c4 = (int)(i % C4);
+        const long pix = i / C4;
+        const int w = (int)(pix % g.W);
+        const long r = pix / g.W;
+        const int h = (int)(r % g.H), n = (int)(r / g.H);
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int kh = 0; kh < g.KH; ++kh) {
+            const int hn = h + g.ph - kh;
+            if (hn < 0 || hn % g.sh) continue;
+            const int ho = hn / g.sh;
+            if (ho >= g.Ho) continue;
+            for (int kw = 0; kw < g.KW; ++kw) {
+                const int wn = w + g.pw - kw;
+                if (wn < 0 || wn % g.sw) continue;
+                const int wo = wn / g.sw;
+                if (wo >= g.Wo) continue;
+                const T* s = cols + ((((long)n * g.Ho + ho) * g.Wo + wo) * taps + kh * g.KW + kw) * g.C + c4 * 4;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[k] += ld(s + k);
+            }
+        }
+        T* d = dx + pix * g.C + c4 * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st(d + k, acc[k]);
+    }
+}
+
+// ------------------------------------------------------------------------------ TN GEMM
+// C[m][n] = sum_k A[k*lda + m] * B[k*ldb + n]; 64 x 64 tile, 16-deep K step, 4 waves as 2 x 2
+// of 32 x 32 (2 x 2 v_mfma_f32_16x16x4_f32 tiles each); operands staged through registers into
+// a double-buffered [k][m] LDS image (row stride 80 floats: the two 16-lane halves of a
+// ds_read_b32 group land 16 banks apart).  Split-K: blockIdx.z owns rows [z*kc, (z+1)*kc) and
+// writes its partial tile to ws + z*M*N (ldc = N), summed by tn_finalize in slice order.
+constexpr int TN_BM = 64, TN_BN = 64, TN_BK = 16, TN_LD = 80;
+typedef float tn_f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ void tn_load4(const T* p, int valid, float* v) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = i < valid ? to_f32(p[i]) : 0.f;
+}
+template <>
+__device__ __forceinline__ void tn_load4<float>(const float* p, int valid, float* v) {
+    if (valid == 4 && ((uintptr_t)p & 15) == 0) {
+        const float4 f = *reinterpret_cast<const float4*>(p);
+        v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = i < valid ? p[i] : 0.f;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_tn_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                      float* __restrict__ C, int M, int N, int K, long lda,
+                                                      long ldb, long ldc, int kc, long slice) {
+    __shared__ float As[2][TN_BK][TN_LD];
+    __shared__ float Bs[2][TN_BK][TN_LD];
+    const int m0 = blockIdx.x * TN_BM, n0 = blockIdx.y * TN_BN;
+    const int k_begin = blockIdx.z * kc, k_end = min(K, k_begin + kc);
+    float* Cz = C + (long)blockIdx.z * slice;
+    const int t = threadIdx.x;
+    const int lr = t >> 4, lc = (t & 15) * 4;     // loader: row lr of the K step, 4 columns at lc
+    const int wave = t >> 6, lane = t & 63;
+    const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
+    tn_f32x4 acc[2][2] = {};
+    float ra[4], rb[4];
+    auto load = [&](int k0) {
+        const int k = k0 + lr;
+        const bool kok = k < k_end;
+        tn_load4(A + (long)(kok ? k : k_begin) * lda + m0 + lc, kok ? min(4, M - m0 - lc) : 0, ra);
+        tn_load4(B + (long)(kok ? k : k_begin) * ldb + n0 + lc, kok ? min(4, N - n0 - lc) : 0, rb);
+    };
+    auto stash = [&](int buf) {
+        *reinterpret_cast<float4*>(&As[buf][lr][lc]) = make_float4(ra[0], ra[1], ra[2], ra[3]);
+        *reinterpret_cast<float4*>(&Bs[buf][lr][lc]) = make_float4(rb[0], rb[1], rb[2], rb[3]);
+    };
+    if (k_begin < k_end) {
+        load(k_begin);
+        stash(0);
+        __syncthreads();
+        int buf = 0;
+        for (int k0 = k_begin; k0 < k_end; k0 += TN_BK) {
+            const bool more = k0 + TN_BK < k_end;
+            if (more) load(k0 + TN_BK);
+#pragma unroll
+            for (int kk = 0; kk < TN_BK; kk += 4) {
+                const int kr = kk + (lane >> 4);
+                float a[2], b[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) a[i] = As[buf][kr][wm + i * 16 + (lane & 15)];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) b[j] = Bs[buf][kr][wn + j * 16 + (lane & 15)];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+            }
+            if (more) {
+                stash(buf ^ 1);
+                __syncthreads();
+                buf ^= 1;
+            }
+        }
+    }
+    // C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm + i * 16 + (lane >> 4) * 4 + r, n = n0 + wn + j * 16 + (lane & 15);
+                if (m < M && n < N) Cz[(long)m * ldc + n] = acc[i][j][r];
+            }
+}
+
+// C[m][n] (+)= sum_z ws[z][m][n], z in order
+__global__ __launch_bounds__(256) void tn_finalize_kernel(const float* __restrict__ ws, float* __restrict__ C, int M,
+                                                          int N, long ldc, int nz, int accumulate) {
+    const long total = (long)M * N;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        float s = 0.f;
+        for (int z = 0; z < nz; ++z) s += ws[z * total + i];
+        const int m = (int)(i / N), n = (int)(i % N);
+        float* c = C + (long)m * ldc + n;
+        *c = accumulate ? *c + s : s;
+    }
+}
+
+// ------------------------------------------------------------------------------ colsum
+// pass 1: ws[chunk][c] = sum of rows [chunk*rc, ...) of column c; pass 2: out[c] (+)= sum_chunk
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ A, float* __restrict__ ws, int rows,
+                                                             int cols, long lda, int rc) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= cols) return;
+    const int r0 = blockIdx.y * rc, r1 = min(rows, r0 + rc);
+    float s = 0.f;
+    for (int r = r0; r < r1; ++r) s += ld(A + (long)r * lda + c);
+    ws[(long)blockIdx.y * cols + c] = s;
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                           int cols, int nchunk, int accumulate) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= cols) return;
+    float s = 0.f;
+    for (int k = 0; k < nchunk; ++k) s += ws[(long)k * cols + c];
+    out[c] = accumulate ? out[c] + s : s;
+}
+
+// ------------------------------------------------------------------------- LayerNorm bwd
+// one wave per row; mean / rstd recomputed from x (deformable_transformer.py post-norms);
+// per-workgroup partial dgamma/dbeta (4 waves x RPW rows) summed by colsum_final in order
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                            const float* __restrict__ gamma, T* __restrict__ dx,
+                                                            float* __restrict__ pg, float* __restrict__ pb, int rows,
+                                                            int d, float eps, int rpw) {
+    constexpr int MAXV = 16;   // d <= 1024
+    extern __shared__ float red[];   // [4][2][d]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nv = (d + 63) / 64;
+    float g_acc[MAXV], b_acc[MAXV];
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v) g_acc[v] = b_acc[v] = 0.f;
+    const int r_begin = (blockIdx.x * 4 + wave) * rpw;
+    for (int r = r_begin; r < min(rows, r_begin + rpw); ++r) {
+        const T* xr = x + (long)r * d;
+        const T* dr = dy + (long)r * d;
+        float xv[MAXV], dv[MAXV];
+        float s = 0.f;
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) {
+            const int c = v * 64 + lane;
+            xv[v] = (v < nv && c < d) ? ld(xr + c) : 0.f;
+            dv[v] = (v < nv && c < d) ? ld(dr + c) : 0.f;
+            s += xv[v];
+        }
+        for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o);
+        const float mean = s / (float)d;
+        float q = 0.f;
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) {
+            const int c = v * 64 + lane;
+            const float t = (v < nv && c < d) ? xv[v] - mean : 0.f;
+            q += t * t;
+        }
+        for (int o = 32; o; o >>= 1) q += __shfl_xor(q, o);
+        const float rstd = rsqrtf(q / (float)d + eps);
+        float sg = 0.f, sgx = 0.f;
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) {
+            const int c = v * 64 + lane;
+            if (v < nv && c < d) {
+                const float xh = (xv[v] - mean) * rstd;
+                const float g = dv[v] * gamma[c];
+                sg += g;
+                sgx += g * xh;
+                g_acc[v] += dv[v] * xh;
+                b_acc[v] += dv[v];
+            }
+        }
+        for (int o = 32; o; o >>= 1) {
+            sg += __shfl_xor(sg, o);
+            sgx += __shfl_xor(sgx, o);
+        }
+        const float inv_d = 1.f / (float)d;
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) {
+            const int c = v * 64 + lane;
+            if (v < nv && c < d) {
+                const float xh = (xv[v] - mean) * rstd;
+                st(dx + (long)r * d + c, rstd * (dv[v] * gamma[c] - sg * inv_d - xh * sgx * inv_d));
+            }
+        }
+    }
+    // per-workgroup partials, waves combined in order
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v) {
+        const int c = v * 64 + lane;
+        if (v < nv && c < d) {
+            red[(wave * 2) * d + c] = g_acc[v];
+            red[(wave * 2 + 1) * d + c] = b_acc[v];
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < d; c += 256) {
+        float gs = 0.f, bs = 0.f;
+        for (int w = 0; w < 4; ++w) {
+            gs += red[(w * 2) * d + c];
+            bs += red[(w * 2 + 1) * d + c];
+        }
+        pg[(long)blockIdx.x * d + c] = gs;
+        pb[(long)blockIdx.x * d + c] = bs;
+    }
+}
+
+// ------------------------------------------------------------------------- GroupNorm bwd
+// x, dy: (N, HW, C) NHWC.  pass 1 per (image, HW block): per-channel sums of dy, dy*x, x, x^2
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_partial_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                             float* __restrict__ part, int HW, int C, int rb) {
+    const int n = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
+    const int p0 = blk * rb, p1 = min(HW, p0 + rb);
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float sdy = 0.f, sdyx = 0.f, sx = 0.f, sxx = 0.f;
+        for (int p = p0; p < p1; ++p) {
+            const long o = ((long)n * HW + p) * C + c;
+            const float xv = ld(x + o), dv = ld(dy + o);
+            sdy += dv;
+            sdyx += dv * xv;
+            sx += xv;
+            sxx += xv * xv;
+        }
+        float* q = part + (((long)n * nblk + blk) * 4) * C + c;
+        q[0] = sdy;
+        q[C] = sdyx;
+        q[2 * C] = sx;
+        q[3 * C] = sxx;
+    }
+}
+
+// pass 2 (one workgroup per image): per-channel sums over the blocks, then per group the
+// statistics and the two backward scalars; writes stats[n][g] = (mean, rstd, a/cnt, bsum/cnt)
+// and per-image channel sums for dgamma / dbeta
+__global__ __launch_bounds__(256) void gn_bwd_stats_kernel(const float* __restrict__ part, const float* __restrict__ gamma,
+                                                           float* __restrict__ stats, float* __restrict__ chan,
+                                                           int HW, int C, int G, int nblk, float eps) {
+    extern __shared__ float sm[];   // [4][C]
+    const int n = blockIdx.x;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int b = 0; b < nblk; ++b) {
+            const float* q = part + (((long)n * nblk + b) * 4) * C + c;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) s[k] += q[k * C];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sm[k * C + c] = s[k];
+    }
+    __syncthreads();
+    const int cg = C / G;
+    for (int g = threadIdx.x; g < G; g += 256) {
+        float sx = 0.f, sxx = 0.f, a = 0.f, bs = 0.f;
+        for (int c = g * cg; c < (g + 1) * cg; ++c) {
+            sx += sm[2 * C + c];
+            sxx += sm[3 * C + c];
+            a += gamma[c] * sm[c];
+            bs += gamma[c] * sm[C + c];
+        }
+        const float cnt = (float)HW * (float)cg;
+        const float mean = sx / cnt;
+        const float var = fmaxf(sxx / cnt - mean * mean, 0.f);
+        const float rstd = rsqrtf(var + eps);
+        // sum(dy*gamma*xhat) = rstd * (sum(dy*gamma*x) - mean * sum(dy*gamma))
+        const float bx = rstd * (bs - mean * a);
+        float* st4 = stats + ((long)n * G + g) * 4;
+        st4[0] = mean;
+        st4[1] = rstd;
+        st4[2] = a / cnt;
+        st4[3] = bx / cnt;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+        const float* st4 = stats + ((long)n * G + c / cg) * 4;
+        // dgamma_n[c] = sum dy*xhat = rstd*(sum dy*x - mean*sum dy); dbeta_n[c] = sum dy
+        chan[((long)n * 2) * C + c] = st4[1] * (sm[C + c] - st4[0] * sm[c]);
+        chan[((long)n * 2 + 1) * C + c] = sm[c];
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                           const float* __restrict__ gamma, const float* __restrict__ stats,
+                                                           T* __restrict__ dx, int HW, int C, int G, long total) {
+    const int cg = C / G;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int c = (int)(i % C);
+        const long n = i / ((long)HW * C);
+        const float* st4 = stats + (n * G + c / cg) * 4;
+        const float xh = (ld(x + i) - st4[0]) * st4[1];
+        st(dx + i, st4[1] * (ld(dy + i) * gamma[c] - st4[2] - xh * st4[3]));
+    }
+}
+
+// dgamma/dbeta = sum over images of chan[n]
+__global__ __launch_bounds__(256) void gn_bwd_param_kernel(const float* __restrict__ chan, float* __restrict__ dgamma,
+                                                           float* __restrict__ dbeta, int N, int C) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    float g = 0.f, b = 0.f;
+    for (int n = 0; n < N; ++n) {
+        g += chan[((long)n * 2) * C + c];
+        b += chan[((long)n * 2 + 1) * C + c];
+    }
+    if (dgamma) dgamma[c] = g;
+    if (dbeta) dbeta[c] = b;
+}
+
+// ------------------------------------------------------------------------- attention bwd
+// pass 1: one wave per (b, h, query i): P_ij, dS_ij = P_ij (dO_i.V_j - sum_j P_ij dO_i.V_j)
+// stored to ws, dQ_i = scale * sum_j dS_ij K_j
+struct AttnArgs {
+    const float *Q, *K, *V, *dO;
+    float *dQ, *dK, *dV, *P, *dS;
+    const uint8_t* key_mask;
+    int ldq, ldk, ldv, ldo;   // row strides (elements); dQ/dK/dV use ldq/ldk/ldv
+    int B, Lq, Lk, H, D;
+    float scale;
+};
+
+constexpr int ATT_MAXD = 64;
+
+// MD: compile-time bound on head_dim (32 or 64) so the per-lane vectors stay in registers
+template <int MD>
+__global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wave;
+    const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+    if (i >= a.Lq) return;
+    const float* q = a.Q + ((long)b * a.Lq + i) * a.ldq + h * a.D;
+    const float* dO = a.dO + ((long)b * a.Lq + i) * a.ldo + h * a.D;
+    float* Prow = a.P + ((long)bh * a.Lq + i) * a.Lk;
+    float* Srow = a.dS + ((long)bh * a.Lq + i) * a.Lk;
+    float qv[MD], ov[MD];
+#pragma unroll
+    for (int d = 0; d < MD; ++d) {
+        qv[d] = d < a.D ? q[d] : 0.f;
+        ov[d] = d < a.D ? dO[d] : 0.f;
+    }
+    // scores and softmax (lanes over keys)
+    float mx = -INFINITY;
+    for (int j = lane; j < a.Lk; j += 64) {
+        const float* k = a.K + ((long)b * a.Lk + j) * a.ldk + h * a.D;
+        float s = 0.f;
+        #pragma unroll
+        for (int d = 0; d < MD; ++d)
+            if (d < a.D) s += qv[d] * k[d];
+        s *= a.scale;
+        if (a.key_mask && a.key_mask[(long)b * a.Lk + j]) s = -INFINITY;
+        Prow[j] = s;
+        mx = fmaxf(mx, s);
+    }
+    for (int o = 32; o; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float sum = 0.f;
+    for (int j = lane; j < a.Lk; j += 64) {
+        const float e = mx == -INFINITY ? 0.f : __expf(Prow[j] - mx);
+        Prow[j] = e;
+        sum += e;
+    }
+    for (int o = 32; o; o >>= 1) sum += __shfl_xor(sum, o);
+    const float rs = sum > 0.f ? 1.f / sum : 0.f;
+    float di = 0.f;
+    for (int j = lane; j < a.Lk; j += 64) {
+        const float p = Prow[j] * rs;
+        Prow[j] = p;
+        const float* v = a.V + ((long)b * a.Lk + j) * a.ldv + h * a.D;
+        float dp = 0.f;
+        #pragma unroll
+        for (int d = 0; d < MD; ++d)
+            if (d < a.D) dp += ov[d] * v[d];
+        Srow[j] = dp;
+        di += p * dp;
+    }
+    for (int o = 32; o; o >>= 1) di += __shfl_xor(di, o);
+    float dq[MD];
+#pragma unroll
+    for (int d = 0; d < MD; ++d) dq[d] = 0.f;
+    for (int j = lane; j < a.Lk; j += 64) {
+        const float ds = Prow[j] * (Srow[j] - di);
+        Srow[j] = ds;
+        const float* k = a.K + ((long)b * a.Lk + j) * a.ldk + h * a.D;
+        #pragma unroll
+        for (int d = 0; d < MD; ++d)
+            if (d < a.D) dq[d] += ds * k[d];
+    }
+    float* dqo = a.dQ + ((long)b * a.Lq + i) * a.ldq + h * a.D;
+#pragma unroll
+    for (int d = 0; d < MD; ++d) {
+        float v = dq[d];
+        for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0 && d < a.D) dqo[d] = v * a.scale;
+    }
+}
+
+// pass 2: one wave per (b, h, key j): dK_j = scale * sum_i dS_ij Q_i, dV_j = sum_i P_ij dO_i
+template <int MD>
+__global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int j = blockIdx.x * 4 + wave;
+    const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+    if (j >= a.Lk) return;
+    float dk[MD], dv[MD];
+#pragma unroll
+    for (int d = 0; d < MD; ++d) dk[d] = dv[d] = 0.f;
+    for (int i = lane; i < a.Lq; i += 64) {
+        const float p = a.P[((long)bh * a.Lq + i) * a.Lk + j];
+        const float ds = a.dS[((long)bh * a.Lq + i) * a.Lk + j];
+        const float* q = a.Q + ((long)b * a.Lq + i) * a.ldq + h * a.D;
+        const float* dO = a.dO + ((long)b * a.Lq + i) * a.ldo + h * a.D;
+#pragma unroll
+        for (int d = 0; d < MD; ++d)
+            if (d < a.D) {
+                dk[d] += ds * q[d];
+                dv[d] += p * dO[d];
+            }
+    }
+    float* dko = a.dK + ((long)b * a.Lk + j) * a.ldk + h * a.D;
+    float* dvo = a.dV + ((long)b * a.Lk + j) * a.ldv + h * a.D;
+#pragma unroll
+    for (int d = 0; d < MD; ++d) {
+        float x = dk[d], y = dv[d];
+        for (int o = 32; o; o >>= 1) {
+            x += __shfl_xor(x, o);
+            y += __shfl_xor(y, o);
+        }
+        if (lane == 0 && d < a.D) {
+            dko[d] = x * a.scale;
+            dvo[d] = y;
+        }
+    }
+}
+
+int grid_for(long n) { return (int)std::min<long>((n + 255) / 256, 8192); }
+
+}  // namespace
+}  // namespace kinet
+
+using namespace kinet;
+
+extern "C" int kinet_transpose(const void* src, void* dst, int rows, int cols, int64_t ld_src, int64_t ld_dst,
+                               int dtype, kinet_stream_t stream) {
+    KINET_CHECK_ARG(rows >= 0 && cols >= 0 && ld_src >= cols && ld_dst >= rows, "transpose: bad sizes");
+    if (rows == 0 || cols == 0) return KINET_OK;
+    dim3 grid((cols + 31) / 32, (rows + 31) / 32);
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == KINET_F32)
+        hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, s, (const float*)src, (float*)dst, rows, cols,
+                           (long)ld_src, (long)ld_dst);
+    else if (dtype == KINET_BF16 || dtype == KINET_F16)
+        hipLaunchKernelGGL(transpose_kernel<uint16_t>, grid, dim3(256), 0, s, (const uint16_t*)src, (uint16_t*)dst, rows,
+                           cols, (long)ld_src, (long)ld_dst);
+    else {
+        set_error("transpose: unsupported dtype %d", dtype);
+        return KINET_ERR_ARG;
+    }
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+static int conv_geom(ConvGeom& g, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW, int sh, int sw, int ph,
+                     int pw) {
+    KINET_CHECK_ARG(C % 4 == 0, "im2col/col2im: channels must be a multiple of 4 (got %d)", C);
+    KINET_CHECK_ARG(sh > 0 && sw > 0 && KH > 0 && KW > 0, "im2col/col2im: bad kernel / stride");
+    KINET_CHECK_ARG(Ho == (H + 2 * ph - KH) / sh + 1 && Wo == (W + 2 * pw - KW) / sw + 1,
+                    "im2col/col2im: output size (%d, %d) does not match the geometry", Ho, Wo);
+    g = ConvGeom{B, H, W, C, Ho, Wo, KH, KW, sh, sw, ph, pw};
+    return KINET_OK;
+}
+
+extern "C" int kinet_im2col_nhwc(const void* x, void* cols, int B, int H, int W, int C, int Ho, int Wo, int KH,
+                                 int KW, int sh, int sw, int ph, int pw, int dtype, kinet_stream_t stream) {
+    ConvGeom g;
+    int rc = conv_geom(g, B, H, W, C, Ho, Wo, KH, KW, sh, sw, ph, pw);
+    if (rc) return rc;
+    const long n = (long)B * Ho * Wo * KH * KW * (C / 4);
+    if (n == 0) return KINET_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == KINET_F32) hipLaunchKernelGGL(im2col_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, (const float*)x, (float*)cols, g);
+    else if (dtype == KINET_BF16) hipLaunchKernelGGL(im2col_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)cols, g);
+    else if (dtype == KINET_F16) hipLaunchKernelGGL(im2col_kernel<f16_t>, dim3(grid_for(n)), dim3(256), 0, s, (const f16_t*)x, (f16_t*)cols, g);
+    else { set_error("im2col: unsupported dtype %d", dtype); return KINET_ERR_ARG; }
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_col2im_nhwc(const void* cols, void* dx, int B, int H, int W, int C, int Ho, int Wo, int KH,
+                                 int KW, int sh, int sw, int ph, int pw, int dtype, kinet_stream_t stream) {
+    ConvGeom g;
+    int rc = conv_geom(g, B, H, W, C, Ho, Wo, KH, KW, sh, sw, ph, pw);
+    if (rc) return rc;
+    const long n = (long)B * H * W * (C / 4);
+    if (n == 0) return KINET_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == KINET_F32) hipLaunchKernelGGL(col2im_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, (const float*)cols, (float*)dx, g);
+    else if (dtype == KINET_BF16) hipLaunchKernelGGL(col2im_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s, (const bf16_t*)cols, (bf16_t*)dx, g);
+    else if (dtype == KINET_F16) hipLaunchKernelGGL(col2im_kernel<f16_t>, dim3(grid_for(n)), dim3(256), 0, s, (const f16_t*)cols, (f16_t*)dx, g);
+    else { set_error("col2im: unsupported dtype %d", dtype); return KINET_ERR_ARG; }
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int64_t kinet_gemm_tn_workspace(int M, int N, int K) {
+    const long long tiles = (long long)((M + TN_BM - 1) / TN_BM) * ((N + TN_BN - 1) / TN_BN);
+    if (tiles <= 0 || K <= 0) return 0;
+    int ks = (int)std::min<long long>(64, std::max<long long>(1, 1024 / tiles));
+    ks = std::min(ks, std::max(1, K / 64));
+    return ks > 1 ? (int64_t)ks * M * N : 0;
+}
+
+extern "C" int kinet_gemm_tn(const void* A, const void* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                             int64_t ldc, int dtype, int accumulate, float* workspace, kinet_stream_t stream) {
+    KINET_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && lda >= M && ldb >= N && ldc >= N, "gemm_tn: bad sizes");
+    if (M == 0 || N == 0) return KINET_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const long long ws_elems = kinet_gemm_tn_workspace(M, N, K);
+    int ks = ws_elems ? (int)(ws_elems / ((long long)M * N)) : 1;
+    KINET_CHECK_ARG(ks == 1 || workspace, "gemm_tn: needs kinet_gemm_tn_workspace(M, N, K) floats of workspace");
+    if (K == 0) {
+        if (!accumulate) KINET_CHECK_HIP(hipMemset2DAsync(C, ldc * 4, 0, (size_t)N * 4, M, s));
+        return KINET_OK;
+    }
+    const int kc = ((K + ks - 1) / ks + TN_BK - 1) / TN_BK * TN_BK;
+    ks = (K + kc - 1) / kc;
+    const bool direct = ks == 1 && !accumulate;
+    float* out = direct ? C : workspace;
+    const long slice = (long)M * N;
+    const long ldo = direct ? (long)ldc : (long)N;
+    if (!direct && !workspace) {
+        set_error("gemm_tn: accumulate needs a workspace of M*N floats");
+        return KINET_ERR_ARG;
+    }
+    dim3 grid((M + TN_BM - 1) / TN_BM, (N + TN_BN - 1) / TN_BN, ks);
+    if (dtype == KINET_F32)
+        hipLaunchKernelGGL(gemm_tn_kernel<float>, grid, dim3(256), 0, s, (const float*)A, (const float*)B, out, M, N, K,
+                           (long)lda, (long)ldb, ldo, kc, slice);
+    else if (dtype == KINET_BF16)
+        hipLaunchKernelGGL(gemm_tn_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)A, (const bf16_t*)B, out, M, N,
+                           K, (long)lda, (long)ldb, ldo, kc, slice);
+    else if (dtype == KINET_F16)
+        hipLaunchKernelGGL(gemm_tn_kernel<f16_t>, grid, dim3(256), 0, s, (const f16_t*)A, (const f16_t*)B, out, M, N,
+                           K, (long)lda, (long)ldb, ldo, kc, slice);
+    else {
+        set_error("gemm_tn: unsupported dtype %d", dtype);
+        return KINET_ERR_ARG;
+    }
+    KINET_LAUNCH_CHECK();
+    if (!direct) {
+        hipLaunchKernelGGL(tn_finalize_kernel, dim3(grid_for(slice)), dim3(256), 0, s, workspace, C, M, N, (long)ldc, ks,
+                           accumulate);
+        KINET_LAUNCH_CHECK();
+    }
+    return KINET_OK;
+}
+
+extern "C" int64_t kinet_colsum_workspace(int rows, int cols) {
+    const int chunks = std::max(1, std::min(256, rows / 64));
+    return (int64_t)chunks * cols;
+}
+
+extern "C" int kinet_colsum(const void* A, float* out, int rows, int cols, int64_t lda, int dtype, int accumulate,
+                            float* workspace, kinet_stream_t stream) {
+    KINET_CHECK_ARG(rows >= 0 && cols >= 0 && lda >= cols && workspace, "colsum: bad arguments");
+    if (cols == 0) return KINET_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int chunks = (int)(kinet_colsum_workspace(rows, cols) / cols);
+    const int rc = (rows + chunks - 1) / chunks;
+    dim3 g1((cols + 255) / 256, chunks);
+    if (dtype == KINET_F32) hipLaunchKernelGGL(colsum_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)A, workspace, rows, cols, (long)lda, rc);
+    else if (dtype == KINET_BF16) hipLaunchKernelGGL(colsum_partial_kernel<bf16_t>, g1, dim3(256), 0, s, (const bf16_t*)A, workspace, rows, cols, (long)lda, rc);
+    else if (dtype == KINET_F16) hipLaunchKernelGGL(colsum_partial_kernel<f16_t>, g1, dim3(256), 0, s, (const f16_t*)A, workspace, rows, cols, (long)lda, rc);
+    else { set_error("colsum: unsupported dtype %d", dtype); return KINET_ERR_ARG; }
+    KINET_LAUNCH_CHECK();
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, workspace, out, cols, chunks, accumulate);
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int64_t kinet_layernorm_backward_workspace(int rows, int d) {
+    const int rpw = 16;
+    const long long blocks = (rows + 4LL * rpw - 1) / (4LL * rpw);
+    return 2 * std::max<long long>(1, blocks) * d;
+}
+
+extern "C" int kinet_layernorm_backward(const void* dy, const void* x, const float* gamma, void* dx, float* dgamma,
+                                        float* dbeta, int rows, int d, float eps, int dtype, float* workspace,
+                                        kinet_stream_t stream) {
+    KINET_CHECK_ARG(d > 0 && d <= 1024 && rows >= 0 && workspace && gamma, "layernorm_backward: bad arguments");
+    if (rows == 0) return KINET_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int rpw = 16;
+    const int blocks = (rows + 4 * rpw - 1) / (4 * rpw);
+    float* pg = workspace;
+    float* pb = workspace + (long)blocks * d;
+    const size_t lds = 8 * (size_t)d * sizeof(float);
+    if (dtype == KINET_F32) hipLaunchKernelGGL(layernorm_bwd_kernel<float>, dim3(blocks), dim3(256), lds, s, (const float*)dy, (const float*)x, gamma, (float*)dx, pg, pb, rows, d, eps, rpw);
+    else if (dtype == KINET_BF16) hipLaunchKernelGGL(layernorm_bwd_kernel<bf16_t>, dim3(blocks), dim3(256), lds, s, (const bf16_t*)dy, (const bf16_t*)x, gamma, (bf16_t*)dx, pg, pb, rows, d, eps, rpw);
+    else if (dtype == KINET_F16) hipLaunchKernelGGL(layernorm_bwd_kernel<f16_t>, dim3(blocks), dim3(256), lds, s, (const f16_t*)dy, (const f16_t*)x, gamma, (f16_t*)dx, pg, pb, rows, d, eps, rpw);
+    else { set_error("layernorm_backward: unsupported dtype %d", dtype); return KINET_ERR_ARG; }
+    KINET_LAUNCH_CHECK();
+    dim3 gf((d + 255) / 256);
+    if (dgamma) { hipLaunchKernelGGL(colsum_final_kernel, gf, dim3(256), 0, s, pg, dgamma, d, blocks, 0); KINET_LAUNCH_CHECK(); }
+    if (dbeta) { hipLaunchKernelGGL(colsum_final_kernel, gf, dim3(256), 0, s, pb, dbeta, d, blocks, 0); KINET_LAUNCH_CHECK(); }
+    return KINET_OK;
+}
+
+static int gn_blocks(int HW) { return std::max(1, std::min(64, HW / 256)); }
+
+extern "C" int64_t kinet_groupnorm_backward_workspace(int N, int HW, int C, int groups) {
+    const long long nb = gn_blocks(HW);
+    return (long long)N * nb * 4 * C + (long long)N * groups * 4 + (long long)N * 2 * C;
+}
+
+extern "C" int kinet_groupnorm_backward(const void* dy, const void* x, const float* gamma, void* dx, float* dgamma,
+                                        float* dbeta, int N, int HW, int C, int groups, float eps, int dtype,
+                                        float* workspace, kinet_stream_t stream) {
+    KINET_CHECK_ARG(N >= 0 && HW > 0 && C > 0 && groups > 0 && C % groups == 0 && workspace && gamma,
+                    "groupnorm_backward: bad arguments");
+    if (N == 0) return KINET_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = gn_blocks(HW);
+    const int rb = (HW + nb - 1) / nb;
+    float* part = workspace;
+    float* stats = part + (long)N * nb * 4 * C;
+    float* chan = stats + (long)N * groups * 4;
+    const long total = (long)N * HW * C;
+#define GN_BWD(T)                                                                                                  \
+    hipLaunchKernelGGL(gn_bwd_partial_kernel<T>, dim3(nb, N), dim3(256), 0, s, (const T*)dy, (const T*)x, part, HW, C, rb); \
+    KINET_LAUNCH_CHECK();                                                                                          \
+    hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(N), dim3(256), 4 * (size_t)C * sizeof(float), s, part, gamma, stats,  \
+                       chan, HW, C, groups, nb, eps);                                                              \
+    KINET_LAUNCH_CHECK();                                                                                          \
+    hipLaunchKernelGGL(gn_bwd_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, (const T*)dy, (const T*)x,  \
+                       gamma, stats, (T*)dx, HW, C, groups, total);                                                \
+    KINET_LAUNCH_CHECK();
+    if (dtype == KINET_F32) { GN_BWD(float) }
+    else if (dtype == KINET_BF16) { GN_BWD(bf16_t) }
+    else if (dtype == KINET_F16) { GN_BWD(f16_t) }
+    else { set_error("groupnorm_backward: unsupported dtype %d", dtype); return KINET_ERR_ARG; }
+#undef GN_BWD
+    if (dgamma || dbeta) {
+        hipLaunchKernelGGL(gn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, s, chan, dgamma, dbeta, N, C);
+        KINET_LAUNCH_CHECK();
+    }
+    return KINET_OK;
+}
+
+extern "C" int64_t kinet_mha_backward_workspace(int batch, int Lq, int Lk, int heads) {
+    return 2LL * batch * heads * Lq * Lk;
+}
+
+extern "C" int kinet_mha_backward(const float* Q, int ldq, const float* K, int ldk, const float* V, int ldv,
+                                  const float* dO, int ldo, float* dQ, float* dK, float* dV, int batch, int Lq, int Lk,
+                                  int heads, int head_dim, float scale, const uint8_t* key_mask, float* workspace,
+                                  kinet_stream_t stream) {
+    KINET_CHECK_ARG(head_dim > 0 && head_dim <= ATT_MAXD && workspace, "mha_backward: head_dim %d (<= %d) / workspace",
+                    head_dim, ATT_MAXD);
+    if (batch == 0 || Lq == 0 || Lk == 0) return KINET_OK;
+    AttnArgs a{Q, K, V, dO, dQ, dK, dV, workspace, workspace + (long)batch * heads * Lq * Lk, key_mask,
+               ldq, ldk, ldv, ldo, batch, Lq, Lk, heads, head_dim, scale};
+    hipStream_t s = (hipStream_t)stream;
+    if (head_dim <= 32) {
+        hipLaunchKernelGGL(attn_bwd_q_kernel<32>, dim3((Lq + 3) / 4, batch * heads), dim3(256), 0, s, a);
+        KINET_LAUNCH_CHECK();
+        hipLaunchKernelGGL(attn_bwd_kv_kernel<32>, dim3((Lk + 3) / 4, batch * heads), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(attn_bwd_q_kernel<64>, dim3((Lq + 3) / 4, batch * heads), dim3(256), 0, s, a);
+        KINET_LAUNCH_CHECK();
+        hipLaunchKernelGGL(attn_bwd_kv_kernel<64>, dim3((Lk + 3) / 4, batch * heads), dim3(256), 0, s, a);
+    }
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}

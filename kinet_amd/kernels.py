@@ -488,3 +488,128 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
     if want_loc_attw:
         return out, loc, attw
     return out
+
+
+# ------------------------------------------------------------------ backward (kinet_grad.h)
+def transpose2d(x):
+    """(R, C) -> (C, R) contiguous (kinet_transpose)."""
+    N.require_gpu(x)
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    R, C = x.shape
+    y = torch.empty((C, R), dtype=x.dtype, device=x.device)
+    N.call('kinet_transpose', N.ptr(x), N.ptr(y), R, C, x.stride(0), R, N.dtype_code(x.dtype), N.stream(x.device),
+           work={'family': 'grad', 'bytes': 2 * x.numel() * x.element_size()})
+    return y
+
+
+def im2col_nhwc(x, KH, KW, stride, pad):
+    """x (B, H, W, C) -> (B*Ho*Wo, KH*KW*C) patch matrix (kinet_im2col_nhwc)."""
+    B, H, W, C = x.shape
+    sh, sw = (stride, stride) if isinstance(stride, int) else stride
+    ph, pw = (pad, pad) if isinstance(pad, int) else pad
+    Ho, Wo = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+    cols = torch.empty((B * Ho * Wo, KH * KW * C), dtype=x.dtype, device=x.device)
+    N.call('kinet_im2col_nhwc', N.ptr(x.contiguous()), N.ptr(cols), B, H, W, C, Ho, Wo, KH, KW, sh, sw, ph, pw,
+           N.dtype_code(x.dtype), N.stream(x.device), work={'family': 'grad', 'bytes': 2 * cols.numel() * x.element_size()})
+    return cols
+
+
+def col2im_nhwc(cols, x_shape, KH, KW, stride, pad):
+    """Adjoint of im2col_nhwc: (B*Ho*Wo, KH*KW*C) -> (B, H, W, C)."""
+    B, H, W, C = x_shape
+    sh, sw = (stride, stride) if isinstance(stride, int) else stride
+    ph, pw = (pad, pad) if isinstance(pad, int) else pad
+    Ho, Wo = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+    dx = torch.empty((B, H, W, C), dtype=cols.dtype, device=cols.device)
+    N.call('kinet_col2im_nhwc', N.ptr(cols.contiguous()), N.ptr(dx), B, H, W, C, Ho, Wo, KH, KW, sh, sw, ph, pw,
+           N.dtype_code(cols.dtype), N.stream(cols.device),
+           work={'family': 'grad', 'bytes': (cols.numel() + dx.numel()) * cols.element_size()})
+    return dx
+
+
+def gemm_tn(a, b, out=None, accumulate=False):
+    """out (M, N) f32 [+]= a^T b for a (K, M), b (K, N) (kinet_gemm_tn): weight gradients."""
+    N.require_gpu(a, b)
+    if a.stride(-1) != 1:
+        a = a.contiguous()
+    if b.stride(-1) != 1:
+        b = b.contiguous()
+    K_, M = a.shape
+    K2, Nn = b.shape
+    if K2 != K_ or a.dtype != b.dtype:
+        raise RuntimeError('gemm_tn: operand mismatch')
+    if out is None:
+        out = torch.empty((M, Nn), dtype=torch.float32, device=a.device)
+    nws = N.lib().kinet_gemm_tn_workspace(M, Nn, K_)
+    if accumulate:
+        nws = max(nws, M * Nn)
+    ws = torch.empty(max(1, nws), dtype=torch.float32, device=a.device) if nws else None
+    N.call('kinet_gemm_tn', N.ptr(a), N.ptr(b), N.ptr(out), M, Nn, K_, a.stride(0), b.stride(0), out.stride(0),
+           N.dtype_code(a.dtype), int(accumulate), N.ptr(ws), N.stream(a.device),
+           work={'family': 'gemm', 'flops': 2.0 * M * Nn * K_, 'shape': ('tn', M, Nn, K_)})
+    return out
+
+
+def colsum(a, out=None, accumulate=False):
+    """out[c] (+)= sum_r a[r, c] (f32)."""
+    if a.stride(-1) != 1:
+        a = a.contiguous()
+    R, C = a.shape
+    if out is None:
+        out = torch.empty(C, dtype=torch.float32, device=a.device)
+    ws = torch.empty(max(1, N.lib().kinet_colsum_workspace(R, C)), dtype=torch.float32, device=a.device)
+    N.call('kinet_colsum', N.ptr(a), N.ptr(out), R, C, a.stride(0), N.dtype_code(a.dtype), int(accumulate), N.ptr(ws),
+           N.stream(a.device), work={'family': 'grad', 'bytes': a.numel() * a.element_size()})
+    return out
+
+
+def layernorm_backward(dy, x, gamma, eps, need_params=True):
+    d = x.shape[-1]
+    dy2, x2 = dy.reshape(-1, d).contiguous(), x.reshape(-1, d).contiguous()
+    rows = x2.shape[0]
+    dx = torch.empty_like(x2)
+    dg = torch.empty(d, dtype=torch.float32, device=x.device) if need_params else None
+    db = torch.empty(d, dtype=torch.float32, device=x.device) if need_params else None
+    ws = torch.empty(max(1, N.lib().kinet_layernorm_backward_workspace(rows, d)), dtype=torch.float32, device=x.device)
+    N.call('kinet_layernorm_backward', N.ptr(dy2), N.ptr(x2), N.ptr(f32(gamma)), N.ptr(dx), N.ptr(dg), N.ptr(db), rows,
+           d, float(eps), N.dtype_code(x.dtype), N.ptr(ws), N.stream(x.device),
+           work={'family': 'norm', 'bytes': 3 * x2.numel() * x2.element_size()})
+    return dx.view(x.shape), dg, db
+
+
+def groupnorm_backward(dy, x, gamma, groups, eps, need_params=True):
+    """x, dy (B, HW, C) NHWC."""
+    B, HW, C = x.shape
+    dy, x = dy.contiguous(), x.contiguous()
+    dx = torch.empty_like(x)
+    dg = torch.empty(C, dtype=torch.float32, device=x.device) if need_params else None
+    db = torch.empty(C, dtype=torch.float32, device=x.device) if need_params else None
+    ws = torch.empty(max(1, N.lib().kinet_groupnorm_backward_workspace(B, HW, C, groups)), dtype=torch.float32,
+                     device=x.device)
+    N.call('kinet_groupnorm_backward', N.ptr(dy), N.ptr(x), N.ptr(f32(gamma)), N.ptr(dx), N.ptr(dg), N.ptr(db), B, HW,
+           C, groups, float(eps), N.dtype_code(x.dtype), N.ptr(ws), N.stream(x.device),
+           work={'family': 'norm', 'bytes': 4 * x.numel() * x.element_size()})
+    return dx, dg, db
+
+
+def mha_backward(q, k, v, do, heads, scale, key_mask=None):
+    """Backward of mha_core (f32): returns dq, dk, dv with the layouts of q, k, v."""
+    B, Lq, E = q.shape
+    Lk = k.shape[1]
+    for t in (q, k, v, do):
+        if t.dtype != torch.float32 or t.stride(-1) != 1 or t.stride(0) != t.shape[1] * t.stride(1):
+            raise RuntimeError('mha_backward: f32 rows, unit stride, packed batches')
+    dq = torch.empty((B, Lq, E), dtype=torch.float32, device=q.device)
+    dk = torch.empty((B, Lk, E), dtype=torch.float32, device=q.device)
+    dv = torch.empty((B, Lk, E), dtype=torch.float32, device=q.device)
+    ws = torch.empty(max(1, N.lib().kinet_mha_backward_workspace(B, Lq, Lk, heads)), dtype=torch.float32,
+                     device=q.device)
+    km = key_mask.to(torch.uint8).contiguous() if key_mask is not None else None
+    # dq/dk/dv are written with q/k/v's row strides: give them packed copies of the layouts
+    if q.stride(1) != E or k.stride(1) != E or v.stride(1) != E:
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+    N.call('kinet_mha_backward', N.ptr(q), E, N.ptr(k), E, N.ptr(v), E, N.ptr(do.contiguous()), E, N.ptr(dq),
+           N.ptr(dk), N.ptr(dv), B, Lq, Lk, heads, E // heads, float(scale), N.ptr(km), N.ptr(ws), N.stream(q.device),
+           work={'family': 'attn', 'flops': 8.0 * B * heads * Lq * Lk * (E // heads)})
+    return dq, dk, dv

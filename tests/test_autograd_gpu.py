@@ -1,0 +1,174 @@
+"""Training-path operators (kinet_amd/autograd.py): forward and backward on kinet kernels vs
+the same op in plain PyTorch fp32 autograd (the reference trains with torch's modules,
+engine.py:145-149), on the GPU.  Tolerances: fp32 with different summation orders --
+relative 1e-4 of the tensor's scale (GEMM reductions of up to ~10^4 terms)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rel=1e-4, name=''):
+    scale = b.abs().max().item() + 1e-12
+    err = (a.float() - b.float()).abs().max().item()
+    assert err <= rel * scale, f'{name}: max err {err:.3e} vs scale {scale:.3e}'
+
+
+def _g(*shape, seed=0):
+    g = torch.Generator(device='cuda').manual_seed(seed)
+    return torch.randn(*shape, generator=g, device='cuda')
+
+
+@pytest.mark.parametrize('M,Kin,Nout,bias', [(1000, 256, 288, True), (37, 288, 1024, True), (5000, 64, 20, False)])
+def test_linear_fwd_bwd(M, Kin, Nout, bias):
+    from kinet_amd import autograd as A
+    x = _g(M, Kin, seed=1).requires_grad_()
+    w = (_g(Nout, Kin, seed=2) * Kin ** -0.5).requires_grad_()
+    b = _g(Nout, seed=3).requires_grad_() if bias else None
+    go = _g(M, Nout, seed=4)
+    y = A.linear(x, w, b)
+    (y * go).sum().backward()
+    got = [y.detach(), x.grad, w.grad] + ([b.grad] if bias else [])
+    x2, w2 = x.detach().clone().requires_grad_(), w.detach().clone().requires_grad_()
+    b2 = b.detach().clone().requires_grad_() if bias else None
+    y2 = F.linear(x2, w2, b2)
+    (y2 * go).sum().backward()
+    ref = [y2.detach(), x2.grad, w2.grad] + ([b2.grad] if bias else [])
+    for n, a, r in zip(['y', 'dx', 'dw', 'db'], got, ref):
+        _close(a, r, name=n)
+
+
+@pytest.mark.parametrize('cin,cout,k,stride,pad,bn,relu,res,bias', [
+    (64, 128, 3, 1, 1, True, True, False, False),     # bottleneck conv2 (stride 1)
+    (128, 128, 3, 2, 1, True, True, False, False),    # first block conv2 of a stage (stride 2)
+    (256, 512, 1, 2, 0, True, False, False, False),   # downsample 1x1/2
+    (128, 512, 1, 1, 0, True, True, True, False),     # conv3 + residual + ReLU
+    (512, 256, 1, 1, 0, False, False, False, True),   # input_proj 1x1 with bias
+    (256, 256, 3, 2, 1, False, False, False, True),   # input_proj extra level 3x3/2 with bias
+])
+def test_conv_fwd_bwd(cin, cout, k, stride, pad, bn, relu, res, bias):
+    from kinet_amd import autograd as A
+    B, H, W = 2, 13, 18
+    x = _g(B, H, W, cin, seed=5).requires_grad_()
+    w = (_g(cout, cin, k, k, seed=6) * (cin * k * k) ** -0.5).requires_grad_()
+    b = _g(cout, seed=7).requires_grad_() if bias else None
+    scale = (torch.rand(cout, device='cuda') + 0.5) if bn else None
+    shift = _g(cout, seed=8) * 0.1 if bn else None
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    r = _g(B, Ho, Wo, cout, seed=9).requires_grad_() if res else None
+    go = _g(B, Ho, Wo, cout, seed=10)
+    y = A.conv_nhwc(x, w, b, stride, pad, scale, shift, relu, r)
+    (y * go).sum().backward()
+    # torch reference on NCHW
+    x2 = x.detach().permute(0, 3, 1, 2).clone().requires_grad_()
+    w2 = w.detach().clone().requires_grad_()
+    b2 = b.detach().clone().requires_grad_() if bias else None
+    r2 = r.detach().permute(0, 3, 1, 2).clone().requires_grad_() if res else None
+    z = F.conv2d(x2, w2, b2, stride, pad)
+    if bn:
+        z = z * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)
+    if res:
+        z = z + r2
+    if relu:
+        z = F.relu(z)
+    (z * go.permute(0, 3, 1, 2)).sum().backward()
+    _close(y.detach(), z.detach().permute(0, 2, 3, 1), name='y')
+    _close(x.grad, x2.grad.permute(0, 2, 3, 1), name='dx')
+    _close(w.grad, w2.grad, name='dw')
+    if bias:
+        _close(b.grad, b2.grad, name='db')
+    if res:
+        _close(r.grad, r2.grad.permute(0, 2, 3, 1), name='dres')
+
+
+@pytest.mark.parametrize('d', [256, 288])
+def test_layer_norm_fwd_bwd(d):
+    from kinet_amd import autograd as A
+    ln = torch.nn.LayerNorm(d).cuda()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.normal_()
+    x = (_g(3, 517, d, seed=11) * 2 + 0.5).requires_grad_()
+    go = _g(3, 517, d, seed=12)
+    y = A.layer_norm(x, ln)
+    (y * go).sum().backward()
+    got = [y.detach(), x.grad, ln.weight.grad.clone(), ln.bias.grad.clone()]
+    ln.zero_grad()
+    x2 = x.detach().clone().requires_grad_()
+    y2 = ln(x2)
+    (y2 * go).sum().backward()
+    for n, a, r in zip(['y', 'dx', 'dg', 'db'], got, [y2.detach(), x2.grad, ln.weight.grad, ln.bias.grad]):
+        _close(a, r, name=n)
+
+
+def test_group_norm_fwd_bwd():
+    from kinet_amd import autograd as A
+    C, G = 288, 32
+    gn = torch.nn.GroupNorm(G, C).cuda()
+    with torch.no_grad():
+        gn.weight.uniform_(0.5, 1.5)
+        gn.bias.normal_()
+    B, H, W = 2, 25, 42
+    x = (_g(B, H * W, C, seed=13) * 3 + 1).requires_grad_()
+    go = _g(B, H * W, C, seed=14)
+    y = A.group_norm_nhwc(x, gn)
+    (y * go).sum().backward()
+    got = [y.detach(), x.grad, gn.weight.grad.clone(), gn.bias.grad.clone()]
+    gn.zero_grad()
+    x2 = x.detach().permute(0, 2, 1).reshape(B, C, H, W).clone().requires_grad_()
+    y2 = gn(x2)
+    (y2 * go.permute(0, 2, 1).reshape(B, C, H, W)).sum().backward()
+    ref = [y2.detach().reshape(B, C, H * W).permute(0, 2, 1), x2.grad.reshape(B, C, H * W).permute(0, 2, 1),
+           gn.weight.grad, gn.bias.grad]
+    for n, a, r in zip(['y', 'dx', 'dg', 'db'], got, ref):
+        _close(a, r, name=n)
+
+
+@pytest.mark.parametrize('E,heads,Lq,mask', [(256, 8, 300, False), (288, 8, 520, True)])
+def test_mha_core_fwd_bwd(E, heads, Lq, mask):
+    from kinet_amd import autograd as A
+    B = 2
+    q = _g(B, Lq, E, seed=15).requires_grad_()
+    k = _g(B, Lq, E, seed=16).requires_grad_()
+    v = _g(B, Lq, E, seed=17).requires_grad_()
+    km = None
+    if mask:
+        km = torch.zeros(B, Lq, dtype=torch.bool, device='cuda')
+        km[1, -40:] = True
+    go = _g(B, Lq, E, seed=18)
+    D = E // heads
+    o = A.mha_core(q, k, v, heads, D ** -0.5, km)
+    (o * go).sum().backward()
+    q2, k2, v2 = (t.detach().clone().requires_grad_() for t in (q, k, v))
+
+    def split(t):
+        return t.view(B, -1, heads, D).transpose(1, 2)
+    am = None if km is None else km[:, None, None, :]
+    o2 = F.scaled_dot_product_attention(split(q2), split(k2), split(v2),
+                                        attn_mask=None if am is None else ~am).transpose(1, 2).reshape(B, Lq, E)
+    (o2 * go).sum().backward()
+    for n, a, r in zip(['o', 'dq', 'dk', 'dv'], [o.detach(), q.grad, k.grad, v.grad], [o2.detach(), q2.grad, k2.grad,
+                                                                                     v2.grad]):
+        _close(a, r, rel=2e-4, name=n)
+
+
+def test_multihead_attention_matches_module():
+    """in_proj split + core + out_proj == nn.MultiheadAttention (batch-first by transposes)."""
+    from kinet_amd import autograd as A
+    E, H, B, L = 288, 8, 2, 120
+    mod = torch.nn.MultiheadAttention(E, H, dropout=0.0).cuda()
+    x = _g(B, L, E, seed=19).requires_grad_()
+    pos = _g(B, L, E, seed=20)
+    go = _g(B, L, E, seed=21)
+    y = A.multihead_attention(mod, x + pos, x + pos, x)
+    (y * go).sum().backward()
+    got = [y.detach(), x.grad, mod.in_proj_weight.grad.clone(), mod.out_proj.weight.grad.clone()]
+    mod.zero_grad()
+    x2 = x.detach().clone().requires_grad_()
+    qk = (x2 + pos).transpose(0, 1)
+    y2 = mod(qk, qk, x2.transpose(0, 1))[0].transpose(0, 1)
+    (y2 * go).sum().backward()
+    for n, a, r in zip(['y', 'dx', 'dWin', 'dWout'], got, [y2.detach(), x2.grad, mod.in_proj_weight.grad,
+                                                           mod.out_proj.weight.grad]):
+        _close(a, r, rel=2e-4, name=n)
