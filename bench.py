@@ -65,6 +65,8 @@ def parse():
     ap.add_argument('--width', type=int, default=None)
     ap.add_argument('--dtype', default=None, choices=['bf16', 'f16', 'f32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-train', action='store_true', help='skip the config-4 training sub-benchmark')
+    ap.add_argument('--train-steps', type=int, default=4)
     ap.add_argument('--cpu-seconds', type=float, default=20.0, help='bound on the CPU baseline sample')
     a = ap.parse_args()
     wl = WORKLOADS[a.workload]
@@ -268,6 +270,13 @@ def main():
     torch.cuda.synchronize()
     fam, msda = summarize_trace(trace, 3)
 
+    # config-4 training step (BASELINE configs[3]): every rank runs the DDP step, gradients
+    # all-reduced over RCCL -- the path whose 1 -> 8 GPU scaling north_star targets
+    train = None
+    if not a.no_train and a.workload == 'config2':
+        from kinet_amd.train import benchmark_train
+        del out
+        train = benchmark_train(steps=a.train_steps, warmup=2, device=dev)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a.cpu_seconds)
@@ -322,6 +331,7 @@ def main():
             'msda_ms_per_call': {'encoder': msda_enc_ms, 'decoder': msda_dec_ms},
             'device_ms_per_step_by_family': {k: round(v['ms'], 4) for k, v in fam.items()},
             'cpu_baseline': cpu,
+            'train': train,
         }
         print(json.dumps(line))
     if world > 1:

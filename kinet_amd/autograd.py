@@ -44,11 +44,14 @@ class _Linear(Function):
         x2 = x.reshape(-1, x.shape[-1])
         if x2.stride(-1) != 1 or x2.stride(0) != x2.shape[1]:
             x2 = x2.contiguous()
-        y = K.linear(x2, weight.detach(), None if bias is None else bias.detach())
+        # the output is allocated in its final shape (not a view of a 2-D result), so callers
+        # may modify it in place as they would an nn.Linear output (deformable_transformer.py:420)
+        y = torch.empty(*lead, weight.shape[0], dtype=x.dtype, device=x.device)
+        K.linear(x2, weight.detach(), None if bias is None else bias.detach(), out=y.view(-1, weight.shape[0]))
         ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
         ctx.lead = lead
-        return y.view(*lead, weight.shape[0])
+        return y
 
     @staticmethod
     @once_differentiable

@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from kinet_amd import autograd as A
 from kinet_amd import kernels as K
 from kinet_amd.models.misc import NestedTensor
 from kinet_amd.models.position_encoding import build_position_encoding
@@ -82,14 +83,16 @@ class Bottleneck(nn.Module):
         identity = x if self.downsample is None else conv_bn(x, self.downsample[0], self.downsample[1], False)
         return conv_bn(out, self.conv3, self.bn3, True, residual=identity)
 
-    def forward(self, x):   # NCHW autograd path
+    def forward_autograd(self, x):
+        """Training path (NHWC, f32): the same conv + folded-BN (+ residual) + ReLU sequence on
+        kinet_amd.autograd Functions (kinet kernels forward and backward)."""
+        out = A.conv_nhwc(x, self.conv1.weight, None, 1, 0, *self.bn1.folded(), relu=True)
+        out = A.conv_nhwc(out, self.conv2.weight, None, self.conv2.stride[0], 1, *self.bn2.folded(), relu=True)
         identity = x
-        out = F.relu(self.bn1(self.conv1(x)))
-        out = F.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
         if self.downsample is not None:
-            identity = self.downsample(x)
-        return F.relu(out + identity)
+            ds, bn = self.downsample[0], self.downsample[1]
+            identity = A.conv_nhwc(x, ds.weight, None, ds.stride[0], 0, *bn.folded(), relu=False)
+        return A.conv_nhwc(out, self.conv3.weight, None, 1, 0, *self.bn3.folded(), relu=True, residual=identity)
 
 
 class ResNetBody(nn.Module):
@@ -124,6 +127,33 @@ class ResNetBody(nn.Module):
         # stem (torchvision conv1 7x7/2 + FrozenBN + ReLU): the 7 horizontal taps are folded
         # into 24 channels while packing the image, so the conv runs as 7x1 with strides
         # (2, 1): K = 7*24 = 168 instead of 7*7*8 = 392 (kinet_pack_image_kwfold)
+        x = self.forward_nhwc_stem_layer1(img_nchw, dtype)
+        outs = [x]
+        for layer in (self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                x = blk.forward_nhwc(x)
+            outs.append(x)
+        return outs
+
+    def forward_autograd(self, img_nchw):
+        """Training path -> OrderedDict like IntermediateLayerGetter, NCHW views of NHWC f32
+        tensors.  The stem and layer1 are frozen in every configuration (backbone.py:69-71
+        trains only layer2-4), so they run the inference kernels without a graph; layer2-4 run
+        on differentiable kinet Functions."""
+        frozen = [p for m in (self.conv1, self.layer1) for p in m.parameters()]
+        if any(p.requires_grad for p in frozen):
+            raise NotImplementedError('training the ResNet stem / layer1 is not supported '
+                                      '(the reference freezes them, backbone.py:69-71)')
+        with torch.no_grad():
+            x = self.forward_nhwc_stem_layer1(img_nchw, torch.float32)
+        outs = [x]
+        for layer in (self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                x = blk.forward_autograd(x)
+            outs.append(x)
+        return OrderedDict((str(i), nhwc_as_nchw(o)) for i, o in enumerate(outs))
+
+    def forward_nhwc_stem_layer1(self, img_nchw, dtype):
         c1 = self.conv1
         kh, kw = c1.kernel_size
         cg = (3 * kw + 7) // 8 * 8
@@ -132,20 +162,12 @@ class ResNetBody(nn.Module):
         x = K.conv2d_nhwc(x, K.pack_stem_weight(c1.weight, dtype, cg), (c1.stride[0], 1), (c1.padding[0], 0),
                           scale=scale, bias=bias, relu=True)
         x = K.maxpool_3x3s2(x)
-        outs = []
-        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
-            for blk in layer:
-                x = blk.forward_nhwc(x)
-            outs.append(x)
-        return outs
+        for blk in self.layer1:
+            x = blk.forward_nhwc(x)
+        return x
 
-    def forward(self, x):   # NCHW autograd path -> OrderedDict like IntermediateLayerGetter
-        x = self.maxpool(F.relu(self.bn1(self.conv1(x))))
-        out = OrderedDict()
-        for i, layer in enumerate((self.layer1, self.layer2, self.layer3, self.layer4)):
-            x = layer(x)
-            out[str(i)] = x
-        return out
+    def forward(self, x):
+        return self.forward_autograd(x)
 
 
 def nhwc_as_nchw(x):

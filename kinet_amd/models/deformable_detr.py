@@ -25,6 +25,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from kinet_amd import autograd as A
 from kinet_amd import kernels as K
 from kinet_amd.models.backbone import interp_mask, nchw_to_nhwc, nhwc_as_nchw
 from kinet_amd.models.deformable_transformer import fast_path, mlp_fast
@@ -45,9 +46,9 @@ class MLP(nn.Module):
         h = [hidden_dim] * (num_layers - 1)
         self.layers = nn.ModuleList(nn.Linear(n, k) for n, k in zip([input_dim] + h, h + [output_dim]))
 
-    def forward(self, x):
+    def forward(self, x):   # autograd path (kinet Linear Functions)
         for i, layer in enumerate(self.layers):
-            x = F.relu(layer(x)) if i < self.num_layers - 1 else layer(x)
+            x = F.relu(A.linear_module(x, layer)) if i < self.num_layers - 1 else A.linear_module(x, layer)
         return x
 
 
@@ -287,11 +288,29 @@ class DeformableDETR(nn.Module):
         return [{'pred_logits': a, 'pred_boxes': b} for a, b in zip(outputs_class[:-1], outputs_coord[:-1])]
 
     # ------------------------------------------------------------------ autograd path
+    def _input_proj_autograd(self, l, src_nchw):
+        """input_proj[l] (Conv2d + GroupNorm, deformable_detr.py:63-71) on kinet autograd
+        Functions; src (B, C, h, w) NCHW (a channels-last view of an NHWC buffer) -> NCHW view."""
+        conv, gn = self.input_proj[l][0], self.input_proj[l][1]
+        x = src_nchw.float().permute(0, 2, 3, 1)
+        if not x.is_contiguous():
+            x = x.contiguous()
+        B, h, w, C = x.shape
+        d = conv.out_channels
+        if conv.kernel_size == (1, 1) and conv.stride == (1, 1):
+            y = A.linear(x.reshape(B * h * w, C), conv.weight.view(d, C), conv.bias)
+        else:
+            y = A.conv_nhwc(x, conv.weight, conv.bias, conv.stride[0], conv.padding[0])
+            h, w = y.shape[1], y.shape[2]
+        y = A.group_norm_nhwc(y.reshape(B, h * w, d), gn)
+        return y.view(B, h, w, d).permute(0, 3, 1, 2)
+
     def _forward_reference(self, samples, targets=None, prev_features=None):
-        """deformable_detr.py:139-275 op for op (training / autograd): torch convs for the
-        backbone + input projections, MSDeformAttnFunction (HIP fwd/bwd) in attention."""
+        """deformable_detr.py:139-275 op for op (training / autograd) in f32 on kinet autograd
+        Functions: backbone convs, input projections, every Linear / LayerNorm / attention of
+        the transformer and heads (kinet_amd/autograd.py), MSDeformAttnFunction (HIP fwd/bwd)."""
         body = self.backbone[0]
-        xs = body.body(samples.tensors)
+        xs = body.body.forward_autograd(samples.tensors.float())
         features_all = []
         for i in body.return_idx:
             x = xs[str(i)]
@@ -306,14 +325,13 @@ class DeformableDETR(nn.Module):
             pos_list.extend([p[:, frame] for p in pos[-3:]] if three_d else pos[-3:])
             for l, feat in enumerate(frame_feat):
                 src, mask = feat.decompose()
-                src_list.append(self.input_proj[l](src.float()))
+                src_list.append(self._input_proj_autograd(l, src))
                 mask_list.append(mask)
             n_lv = self.num_feature_levels
             if n_lv > len(frame_feat):
                 _len = len(frame_feat)
                 for l in range(_len, n_lv):
-                    src = self.input_proj[l](frame_feat[-1].tensors.float()) if l == _len else \
-                        self.input_proj[l](src_list[-1])
+                    src = self._input_proj_autograd(l, frame_feat[-1].tensors if l == _len else src_list[-1])
                     m = interp_mask(frame_feat[0].mask, src.shape[-2:])
                     pos_l = self.backbone[1](NestedTensor(src, m)).to(src.dtype)
                     src_list.append(src)
@@ -325,7 +343,7 @@ class DeformableDETR(nn.Module):
         for lvl in range(hs.shape[0]):
             reference = init_reference if lvl == 0 else inter_references[lvl - 1]
             reference = inverse_sigmoid(reference)
-            outputs_class = self.class_embed[lvl](hs[lvl])
+            outputs_class = A.linear_module(hs[lvl], self.class_embed[lvl])
             tmp = self.bbox_embed[lvl](hs[lvl])
             if reference.shape[-1] == 4:
                 tmp = tmp + reference

@@ -25,6 +25,7 @@ import torch.nn.functional as F
 from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
+from kinet_amd import autograd as A
 from kinet_amd import kernels as K
 from kinet_amd.models.misc import inverse_sigmoid
 from kinet_amd.msda import MSDeformAttn, value_dtype_for
@@ -92,14 +93,14 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, src):
-        src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
-        return self.norm2(src + self.dropout3(src2))
+        src2 = A.linear_module(self.dropout2(self.activation(A.linear_module(src, self.linear1))), self.linear2)
+        return A.layer_norm(src + self.dropout3(src2), self.norm2)
 
     def forward(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None):
         if fast_path(self):
             return self.forward_fast(src, pos, reference_points, spatial_shapes, padding_mask, query_order)
         src2 = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, spatial_shapes, padding_mask)
-        src = self.norm1(src + self.dropout1(src2))
+        src = A.layer_norm(src + self.dropout1(src2), self.norm1)
         return self.forward_ffn(src)
 
     def forward_fast(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None):
@@ -173,8 +174,8 @@ class DeformableTransformerDecoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, tgt):
-        tgt2 = self.linear2(self.dropout3(self.activation(self.linear1(tgt))))
-        return self.norm3(tgt + self.dropout4(tgt2))
+        tgt2 = A.linear_module(self.dropout3(self.activation(A.linear_module(tgt, self.linear1))), self.linear2)
+        return A.layer_norm(tgt + self.dropout4(tgt2), self.norm3)
 
     def forward(self, tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask=None,
                 query_attn_mask=None, value=None):
@@ -182,12 +183,12 @@ class DeformableTransformerDecoderLayer(nn.Module):
             return self.forward_fast(tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask,
                                      query_attn_mask, value)
         q = k = self.with_pos_embed(tgt, query_pos)
-        tgt2 = self.self_attn(q.transpose(0, 1), k.transpose(0, 1), tgt.transpose(0, 1),
-                              key_padding_mask=query_attn_mask)[0].transpose(0, 1)
-        tgt = self.norm2(tgt + self.dropout2(tgt2))
+        # nn.MultiheadAttention on (L, B, E) transposes (:371) == the batch-first kinet path
+        tgt2 = A.multihead_attention(self.self_attn, q, k, tgt, key_padding_mask=query_attn_mask)
+        tgt = A.layer_norm(tgt + self.dropout2(tgt2), self.norm2)
         tgt2 = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_spatial_shapes,
                                src_padding_mask, query_attn_mask)
-        tgt = self.norm1(tgt + self.dropout1(tgt2))
+        tgt = A.layer_norm(tgt + self.dropout1(tgt2), self.norm1)
         return self.forward_ffn(tgt)
 
     def forward_fast(self, tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask=None,
@@ -421,7 +422,11 @@ class DeformableTransformer(nn.Module):
         query_embed_, tgt = torch.split(query_embed, c, dim=1)
         query_embed_ = query_embed_.unsqueeze(0).expand(bs, -1, -1)
         tgt = tgt.unsqueeze(0).expand(bs, -1, -1)
-        reference_points = self.reference_points(query_embed_).sigmoid()
+        rp = self.reference_points
+        if fast_path(self):
+            reference_points = K.linear(query_embed_.float(), rp.weight, rp.bias).sigmoid()
+        else:
+            reference_points = A.linear_module(query_embed_, rp).sigmoid()
         if targets is not None and 'track_query_hs_embeds' in targets[0]:
             prev_hs_embed = torch.stack([t['track_query_hs_embeds'] for t in targets])
             prev_boxes = torch.stack([t['track_query_boxes'] for t in targets])

@@ -15,6 +15,7 @@ from torch.autograd.function import once_differentiable
 from torch.nn.init import constant_, xavier_uniform_
 
 from kinet_amd import MultiScaleDeformableAttention as MSDA
+from kinet_amd import autograd as A
 from kinet_amd import kernels as K
 
 
@@ -135,12 +136,12 @@ class MSDeformAttn(nn.Module):
         import torch.nn.functional as F
         N, Len_q, _ = query.shape
         N, Len_in, _ = input_flatten.shape
-        value = self.value_proj(input_flatten)
+        value = A.linear_module(input_flatten, self.value_proj)
         if input_padding_mask is not None:
             value = value.masked_fill(input_padding_mask[..., None], float(0))
         value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
-        sampling_offsets = self.sampling_offsets(query).view(N, Len_q, self.n_heads, self.n_levels, self.n_points, 2)
-        attention_weights = self.attention_weights(query).view(N, Len_q, self.n_heads, self.n_levels * self.n_points)
+        sampling_offsets = A.linear_module(query, self.sampling_offsets).view(N, Len_q, self.n_heads, self.n_levels, self.n_points, 2)
+        attention_weights = A.linear_module(query, self.attention_weights).view(N, Len_q, self.n_heads, self.n_levels * self.n_points)
         attention_weights = F.softmax(attention_weights, -1).view(N, Len_q, self.n_heads, self.n_levels, self.n_points)
         if query_attn_mask is not None:
             attention_weights = attention_weights.masked_fill(query_attn_mask[..., None, None, None], float(0))
@@ -155,4 +156,4 @@ class MSDeformAttn(nn.Module):
                              .format(reference_points.shape[-1]))
         output = MSDeformAttnFunction.apply(value, input_spatial_shapes, sampling_locations,
                                             attention_weights, self.im2col_step)
-        return self.output_proj(output)
+        return A.linear_module(output, self.output_proj)

@@ -4,10 +4,12 @@ src/trackformer/engine.py:119-149 (forward -> criterion -> weighted sum -> backw
 clip -> step).
 
 Compute split:
-  * previous-frame forward without grad: the HIP inference path (bf16 or f32);
-  * current-frame forward with grad: op-for-op modules with the HIP MSDeformAttn
-    forward/backward kernels (MSDeformAttnFunction); dense layers via the library GEMMs
-    of PyTorch-ROCm;
+  * previous-frame forward without grad: the HIP inference path (bf16 or f32) when the
+    model has no active dropout, else the op-for-op path (train-mode dropout, as the
+    reference runs it) -- on kinet kernels either way;
+  * current-frame forward with grad: op-for-op modules in f32 on kinet_amd.autograd
+    Functions (backbone convs, Linear, LayerNorm, GroupNorm, attention: forward and backward
+    on kinet kernels) and MSDeformAttnFunction (HIP forward / backward);
   * Hungarian matching and track-query sampling on the host (north_star);
   * gradients averaged over ranks by DistributedDataParallel over RCCL ("nccl" backend),
     bucketed and overlapped with backward -- the one exchange step of the path; the
@@ -113,3 +115,63 @@ def setup_ddp(model, device):
     local = int(os.environ.get('LOCAL_RANK', '0'))
     return torch.nn.parallel.DistributedDataParallel(model, device_ids=[local] if device.type == 'cuda' else None,
                                                      find_unused_parameters=True)
+
+
+def benchmark_train(steps=5, warmup=2, batch=2, height=800, width=1333, prev_dtype=torch.bfloat16, device=None,
+                    dropout=None):
+    """Config-4 training throughput (BASELINE.json configs[3], cfgs/train_mot17.yaml: `mot17
+    deformable multi_frame tracking`, d=288, 500 queries, two-pass track-query training,
+    focal + L1 + GIoU with aux losses, AdamW, clip 0.1) on synthetic (current, prev) frame
+    pairs; DDP over the initialised process group when there is one.  Returns a dict with
+    frames/s (current frames of the whole job), images/s (= 2x) and s/step; the timed region
+    is bracketed by a barrier + device synchronisation and the elapsed time is the max over
+    ranks."""
+    import time
+    from kinet_amd.models import build_model
+    from kinet_amd.models.config import load_args
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    dev = device or torch.device('cuda', torch.cuda.current_device())
+    over = {} if dropout is None else {'dropout': dropout}
+    args = load_args('train_deformable', 'train_multi_frame', 'train_tracking', 'train_mot17', device='cuda', **over)
+    torch.manual_seed(0)
+    model, criterion, _ = build_model(args)
+    model = model.to(dev).train()
+    model.set_compute_dtype(prev_dtype)
+    ddp = setup_ddp(model, dev)
+    opt = build_optimizer(ddp, args)
+    g = torch.Generator().manual_seed(1000 + rank)
+    samples, targets = synthetic_mot_batch(batch, height, width, dev, g)
+
+    def step():
+        tg = [dict(t, prev_target=dict(t['prev_target'])) for t in targets]
+        return train_step(ddp, criterion, opt, samples, tg, args.clip_max_norm)[0]
+
+    for _ in range(max(1, warmup)):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    frames = batch * steps * world
+    return {'metric': 'train frames/sec (config 4: mot17 deformable multi_frame tracking, 3x%dx%d pairs)'
+                      % (height, width),
+            'value': frames / el, 'unit': 'frames/s', 'images_per_s': 2 * frames / el, 'n_gpus': world,
+            'steps': steps, 'warmup': warmup, 's_per_step': el / steps, 'loss': float(loss), 'scaling': 'weak',
+            'dtype': 'f32', 'data': 'synthetic frame pairs, 10-30 boxes, random-init weights',
+            'config': {'workload': 'config4 two-pass tracking training step (prev frame no-grad, current frame '
+                                   'fwd+bwd, AdamW)', 'batch_per_gpu': batch, 'hidden_dim': args.hidden_dim,
+                       'num_queries': args.num_queries, 'dropout': args.dropout,
+                       'prev_frame_dtype': str(prev_dtype).replace('torch.', ''),
+                       'grad_frame_dtype': 'f32', 'parallelism': f'ddp{world} (RCCL all-reduce)'}}
