@@ -69,6 +69,18 @@ int kinet_mha_set_mfma(int enable);
 int kinet_box_refine(const float* tmp, const float* ref, int ref_dim, const float* valid_ratios,
                      float* new_ref, float* ref_input, int N, int Q, int L, kinet_stream_t stream);
 
+/* Sine position embedding of a padding mask (PositionEmbeddingSine, position_encoding.py:85-121;
+ * PositionEmbeddingSine3D, :12-81, one frame `frame` of `frames` at a time), written as NHWC rows:
+ *   out[b*out_batch_stride + (h*W + w)*C + c] = pe(b, h, w, c) (+ level_embed[c] if non-NULL)
+ * C = 2*num_pos_feats ([y | x]) or 3*num_pos_feats ([z | y | x]); channel 2k = sin(e / dim_t[2k]),
+ * 2k+1 = cos(e / dim_t[2k+1]) with e the (normalised) cumulative count of unmasked pixels.
+ * dim_t (num_pos_feats f32, device): temperature ** (2 * (k // 2) / num_pos_feats) as the caller
+ * computes it (kinet_amd evaluates it with torch on the host, as the reference does). */
+int kinet_sine_position_embed(const uint8_t* mask, const float* dim_t, const float* level_embed, void* out,
+                              int B, int H, int W, int num_pos_feats, int three_d, int frame, int frames,
+                              int normalize, float scale, int64_t out_batch_stride, int out_dtype,
+                              kinet_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

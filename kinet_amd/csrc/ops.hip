@@ -4,6 +4,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 #include "../../include/kinet_ops.h"
 #include "common.h"
 
@@ -691,6 +693,87 @@ extern "C" int kinet_box_refine(const float* tmp, const float* ref, int ref_dim,
     if (N * Q == 0) return KINET_OK;
     hipLaunchKernelGGL(box_refine_kernel, dim3((N * Q + 255) / 256), dim3(256), 0, (hipStream_t)stream, tmp, ref,
                        ref_dim, valid_ratios, new_ref, ref_input, N, Q, L);
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+// ---------------------------------------------------------------------------------
+// sine position embedding (position_encoding.py:85-121 2-d, :12-81 3-d), NHWC rows
+// ---------------------------------------------------------------------------------
+namespace kinet {
+namespace {
+template <typename TO>
+__global__ __launch_bounds__(256) void sine_embed_kernel(const uint8_t* __restrict__ mask, const float* __restrict__ dim_t,
+                                                         const float* __restrict__ level_embed, TO* __restrict__ out,
+                                                         int B, int H, int W, int npf, int three_d, int frame,
+                                                         int frames, int normalize, float scale, long out_bs) {
+    const long total = (long)B * H * W;
+    const int C = (three_d ? 3 : 2) * npf;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int w = (int)(i % W);
+        const long r = i / W;
+        const int h = (int)(r % H), b = (int)(r / H);
+        const uint8_t* mb = mask + (long)b * H * W;
+        // cumulative counts of unmasked pixels along the column (y) and the row (x)
+        float ycum = 0.f, ytot = 0.f, xcum = 0.f, xtot = 0.f;
+        for (int k = 0; k < H; ++k) {
+            const float v = mb[(long)k * W + w] ? 0.f : 1.f;
+            ytot += v;
+            if (k <= h) ycum += v;
+        }
+        for (int k = 0; k < W; ++k) {
+            const float v = mb[(long)h * W + k] ? 0.f : 1.f;
+            xtot += v;
+            if (k <= w) xcum += v;
+        }
+        const bool valid = !mb[(long)h * W + w];
+        float ye = ycum, xe = xcum, ze = valid ? (float)(frame + 1) : 0.f;
+        if (normalize) {
+            const float eps = 1e-6f;
+            if (three_d) {   // :49-51, no -0.5 offset
+                ze = ze / ((valid ? (float)frames : 0.f) + eps) * scale;
+                ye = ye / (ytot + eps) * scale;
+                xe = xe / (xtot + eps) * scale;
+            } else {         // :106-108
+                ye = (ye - 0.5f) / (ytot + eps) * scale;
+                xe = (xe - 0.5f) / (xtot + eps) * scale;
+            }
+        }
+        TO* o = out + (long)b * out_bs + ((long)h * W + w) * C;
+        // channel order: [z (3-d only) | y | x], each interleaving sin (even) / cos (odd)
+        for (int c = 0; c < C; ++c) {
+            const int part = c / npf, k = c - part * npf;
+            const float e = three_d ? (part == 0 ? ze : part == 1 ? ye : xe) : (part == 0 ? ye : xe);
+            const float a = e / dim_t[k];
+            float v = (k & 1) ? cosf(a) : sinf(a);
+            if (level_embed) v += level_embed[c];
+            o[c] = Cvt<TO>::from(v);
+        }
+    }
+}
+}  // namespace
+}  // namespace kinet
+
+extern "C" int kinet_sine_position_embed(const uint8_t* mask, const float* dim_t, const float* level_embed, void* out,
+                                         int B, int H, int W, int num_pos_feats, int three_d, int frame, int frames,
+                                         int normalize, float scale, int64_t out_batch_stride, int out_dtype,
+                                         kinet_stream_t stream) {
+    using namespace kinet;
+    KINET_CHECK_ARG(mask && dim_t && out && num_pos_feats > 0 && B >= 0 && H >= 0 && W >= 0,
+                    "sine_position_embed: bad arguments");
+    KINET_CHECK_ARG(!three_d || (frames > 0 && frame >= 0 && frame < frames), "sine_position_embed: frame %d of %d",
+                    frame, frames);
+    const long n = (long)B * H * W;
+    if (n == 0) return KINET_OK;
+    const int grid = (int)std::min<long>((n + 255) / 256, 4096);
+    hipStream_t s = (hipStream_t)stream;
+#define SE(TO) hipLaunchKernelGGL(sine_embed_kernel<TO>, dim3(grid), dim3(256), 0, s, mask, dim_t, level_embed, (TO*)out, \
+                                  B, H, W, num_pos_feats, three_d, frame, frames, normalize, scale, (long)out_batch_stride)
+    if (out_dtype == KINET_F32) SE(float);
+    else if (out_dtype == KINET_BF16) SE(bf16_t);
+    else if (out_dtype == KINET_F16) SE(f16_t);
+    else { set_error("sine_position_embed: unsupported dtype %d", out_dtype); return KINET_ERR_ARG; }
+#undef SE
     KINET_LAUNCH_CHECK();
     return KINET_OK;
 }

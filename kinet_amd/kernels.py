@@ -361,6 +361,26 @@ def add(a, b, out=None):
     return y
 
 
+# ---------------------------------------------------------------- position embedding
+def sine_position_embed(mask, dim_t, num_pos_feats, three_d=False, frame=0, frames=1, normalize=True, scale=1.0,
+                        level_embed=None, out=None, out_batch_stride=None, out_dtype=torch.float32):
+    """Sine embedding of a padding mask (B, H, W) as NHWC rows (kinet_sine_position_embed):
+    returns (B, H*W, C) (or writes rows into `out` at out + b*out_batch_stride)."""
+    N.require_gpu(mask)
+    B, H, W = mask.shape
+    C = (3 if three_d else 2) * num_pos_feats
+    if out is None:
+        out = torch.empty((B, H * W, C), dtype=out_dtype, device=mask.device)
+        out_batch_stride = H * W * C
+    m = mask.to(torch.uint8).contiguous()
+    N.call('kinet_sine_position_embed', N.ptr(m), N.ptr(dim_t), N.ptr(f32(level_embed) if level_embed is not None
+                                                                          else None),
+           N.ptr(out), B, H, W, num_pos_feats, int(three_d), frame, frames, int(normalize), float(scale),
+           int(out_batch_stride), N.dtype_code(out.dtype), N.stream(mask.device),
+           work={'family': 'pos_embed', 'bytes': B * H * W * C * out.element_size()})
+    return out
+
+
 # --------------------------------------------------------------------------- attention
 def mha_core(q, k, v, heads, scale, key_mask=None, out=None):
     """q (B, Lq, E) (row stride may exceed E), k/v (B, Lk, E) -> (B, Lq, E)."""

@@ -130,10 +130,6 @@ class DeformableDETR(nn.Module):
         return self
 
     # ------------------------------------------------------------------ geometry cache
-    def _pos_embed(self, mask):
-        pe = self.backbone[1]
-        return pe.embed_mask(mask)
-
     def _geometry(self, cur_masks, prev_masks, shapes_by_frame, key, device):
         """Masks / valid ratios / refs / position+level embeddings for one frame geometry.
         cur_masks: the 3 backbone-level masks of the current frame; prev_masks the same for
@@ -146,25 +142,30 @@ class DeformableDETR(nn.Module):
             return ent[1]
         frames = [prev_masks, cur_masks] if self.multi_frame_attention else [cur_masks]
         three_d = self.multi_frame_attention and self.multi_frame_encoding
-        # pos for the backbone levels is computed from the CURRENT frame's masks (:141, :167)
-        cur_pos = [self._pos_embed(m) for m in cur_masks]
-        masks, pos = [], []
+        pe = self.backbone[1]
+        # (mask the embedding is computed from, frame index of the 3-d embedding) per level, in
+        # level order; the backbone levels use the CURRENT frame's masks (:141, :167)
+        masks, pos_src = [], []
         for frame, fmasks in enumerate(frames):
             for l, m in enumerate(fmasks):
                 masks.append(m)
-                p = cur_pos[l]
-                pos.append(p[:, frame] if three_d else p)
+                pos_src.append((cur_masks[l], frame if three_d else 0))
             hw_extra = shapes_by_frame[frame][len(fmasks):]
             for (h, w) in hw_extra:
                 m = interp_mask(fmasks[0], (h, w))     # :212-213 (from the first level's mask)
                 masks.append(m)
-                p = self._pos_embed(m)
-                pos.append(p[:, frame] if three_d else p)
+                pos_src.append((m, frame if three_d else 0))
         shapes = [s for fs in shapes_by_frame for s in fs]
-        lvl_pos = []
-        for lvl, (p, (h, w)) in enumerate(zip(pos, shapes)):
-            lvl_pos.append(p.flatten(2).transpose(1, 2) + lvl_embed[lvl].detach().view(1, 1, -1))
-        lvl_pos = torch.cat(lvl_pos, 1).to(self.compute_dtype).contiguous()
+        B = masks[0].shape[0]
+        S = sum(h * w for h, w in shapes)
+        d = self.hidden_dim
+        # sine embedding + level embedding written straight into the flattened (B, S, d) rows
+        # (deformable_transformer.py:141-157) in the compute dtype, one kernel per level
+        lvl_pos = torch.empty((B, S, d), dtype=self.compute_dtype, device=device)
+        off = 0
+        for lvl, ((m, f), (h, w)) in enumerate(zip(pos_src, shapes)):
+            pe.rows(m, f, level_embed=lvl_embed[lvl].detach(), out=lvl_pos[:, off:off + h * w], out_batch_stride=S * d)
+            off += h * w
         mask_flatten = torch.cat([m.flatten(1) for m in masks], 1)
         valid_ratios = torch.stack([self.transformer.get_valid_ratio(m) for m in masks], 1)
         geo = self.transformer.geometry(shapes, valid_ratios, mask_flatten, device)
