@@ -234,13 +234,21 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
     ws[(long)blockIdx.y * cols + c] = s;
 }
 
+// one workgroup per column: thread t sums chunks t, t+256, ... in order, then a fixed-order
+// LDS tree (deterministic; a serial per-column loop over ~10^3 partials was 50 us a call)
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ ws, float* __restrict__ out,
                                                            int cols, int nchunk, int accumulate) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= cols) return;
+    __shared__ float red[256];
+    const int c = blockIdx.x;
     float s = 0.f;
-    for (int k = 0; k < nchunk; ++k) s += ws[(long)k * cols + c];
-    out[c] = accumulate ? out[c] + s : s;
+    for (int k = threadIdx.x; k < nchunk; k += 256) s += ws[(long)k * cols + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[c] = accumulate ? out[c] + red[0] : red[0];
 }
 
 // ------------------------------------------------------------------------- LayerNorm bwd
@@ -696,7 +704,7 @@ extern "C" int kinet_colsum(const void* A, float* out, int rows, int cols, int64
     else if (dtype == KINET_F16) hipLaunchKernelGGL(colsum_partial_kernel<f16_t>, g1, dim3(256), 0, s, (const f16_t*)A, workspace, rows, cols, (long)lda, rc);
     else { set_error("colsum: unsupported dtype %d", dtype); return KINET_ERR_ARG; }
     KINET_LAUNCH_CHECK();
-    hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, workspace, out, cols, chunks, accumulate);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(cols), dim3(256), 0, s, workspace, out, cols, chunks, accumulate);
     KINET_LAUNCH_CHECK();
     return KINET_OK;
 }
@@ -723,7 +731,7 @@ extern "C" int kinet_layernorm_backward(const void* dy, const void* x, const flo
     else if (dtype == KINET_F16) hipLaunchKernelGGL(layernorm_bwd_kernel<f16_t>, dim3(blocks), dim3(256), lds, s, (const f16_t*)dy, (const f16_t*)x, gamma, (f16_t*)dx, pg, pb, rows, d, eps, rpw);
     else { set_error("layernorm_backward: unsupported dtype %d", dtype); return KINET_ERR_ARG; }
     KINET_LAUNCH_CHECK();
-    dim3 gf((d + 255) / 256);
+    dim3 gf(d);
     if (dgamma) { hipLaunchKernelGGL(colsum_final_kernel, gf, dim3(256), 0, s, pg, dgamma, d, blocks, 0); KINET_LAUNCH_CHECK(); }
     if (dbeta) { hipLaunchKernelGGL(colsum_final_kernel, gf, dim3(256), 0, s, pb, dbeta, d, blocks, 0); KINET_LAUNCH_CHECK(); }
     return KINET_OK;

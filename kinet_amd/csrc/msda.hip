@@ -753,11 +753,20 @@ __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
         const int m = g - qi * M;
         const int c0 = lane * VEC;
         const T* vb = value + (long)b * S * MD + c0;
-        GA* gvb = gvalue + (long)b * S * MD + c0;
         const VecT<T, VEC> gv = *reinterpret_cast<const VecT<T, VEC>*>(gout + ((long)b * Lq + q) * MD + (long)m * D + c0);
         Acc gc[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) gc[j] = to_acc(gv.v[j], (Acc*)nullptr);
+        // the grad_value scatter uses a lane-STRIDED channel map (channel j*LPQ + lane): each
+        // atomic wave-instruction then adds LPQ contiguous dwords per (query, head) group
+        // instead of dwords VEC apart (1-2 64-byte atomic requests per group, not 3-4)
+        GA* gvs = gvalue + (long)b * S * MD + lane;
+        Acc gs[VEC];
+        {
+            const T* go = gout + ((long)b * Lq + q) * MD + (long)m * D + lane;
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) gs[j] = to_acc(go[j * LPQ], (Acc*)nullptr);
+        }
         const int sbase = (qi * M + m) * LP;
         for (int s = 0; s < LP; ++s) {
             const BwdTap<Acc> t = taps[sbase + s];
@@ -786,13 +795,13 @@ __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
                     px += gc[j] * dw;
                     py += gc[j] * dh;
                 }
-                // grad_value scatter (cuh:285-304): 4 taps x VEC contiguous channels
+                // grad_value scatter (cuh:285-304): 4 taps x VEC channels (lane-strided, see gs)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     if (t.off[k] >= 0) {
                         const Acc wk = wt[k] * t.a;
 #pragma unroll
-                        for (int j = 0; j < VEC; ++j) atomicAdd(gvb + t.off[k] + j, (GA)(gc[j] * wk));
+                        for (int j = 0; j < VEC; ++j) atomicAdd(gvs + t.off[k] + j * LPQ, (GA)(gs[j] * wk));
                     }
                 }
             }
