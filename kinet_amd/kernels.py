@@ -188,7 +188,7 @@ def ffn_pack(w1, w2, dtype):
     return cached_multi([w1, w2], ('ffn_pack', dtype), make)
 
 
-def ffn_fused(x, linear1, linear2, norm=None):
+def ffn_fused(x, linear1, linear2, norm=None, out=None):
     """y = norm(x + linear2(relu(linear1(x)))) in one launch (deformable_transformer.py:284-288,
     :361-365); the (M, F) hidden tensor stays on chip.  x (..., D) bf16/f16."""
     N.require_gpu(x)
@@ -199,7 +199,10 @@ def ffn_fused(x, linear1, linear2, norm=None):
         x2 = x2.contiguous()
     M = x2.shape[0]
     wp = ffn_pack(linear1.weight, linear2.weight, x.dtype)
-    out = torch.empty((M, D), dtype=x.dtype, device=x.device)
+    if out is None:
+        out = torch.empty((M, D), dtype=x.dtype, device=x.device)
+    elif out.dtype != x.dtype or out.stride(-1) != 1 or out.numel() != M * D:
+        raise RuntimeError('ffn_fused: out must be a unit-stride (M, D) tensor of the input dtype')
     g, b, eps = (f32(norm.weight), f32(norm.bias), float(norm.eps)) if norm is not None else (None, None, 0.0)
     e = x.element_size()
     work = {'family': 'gemm', 'flops': 4.0 * M * D * F_, 'shape': ('ffn', M, D, F_),
@@ -398,12 +401,13 @@ def mha_core(q, k, v, heads, scale, key_mask=None, out=None):
     return o
 
 
-def box_refine(tmp, ref, valid_ratios=None, want_input=True):
-    """tmp (B, Q, 4) f32, ref (B, Q, 2|4) f32 -> new_ref (B, Q, 4) [, ref_input (B, Q, L, 4)]."""
+def box_refine(tmp, ref, valid_ratios=None, want_input=True, out=None):
+    """tmp (B, Q, 4) f32, ref (B, Q, 2|4) f32 -> new_ref (B, Q, 4) [, ref_input (B, Q, L, 4)];
+    out: optional contiguous (B, Q, 4) f32 destination of new_ref."""
     B, Q, _ = tmp.shape
     tmp = tmp.float().contiguous()
     ref = ref.float().contiguous()
-    nref = torch.empty((B, Q, 4), dtype=torch.float32, device=tmp.device)
+    nref = out if out is not None else torch.empty((B, Q, 4), dtype=torch.float32, device=tmp.device)
     rin = None
     L = 0
     if want_input:

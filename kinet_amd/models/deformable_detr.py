@@ -202,7 +202,7 @@ class DeformableDETR(nn.Module):
             out = src[:, off:off + h * w]
             normed = K.groupnorm_nhwc(y.view(B, h * w, d), gn.weight, gn.bias, gn.num_groups, gn.eps,
                                       out=out, out_batch_stride=S * d)
-            if l >= nb:
+            if l >= nb and l + 1 < self.num_feature_levels:
                 # the next extra level convolves this level's normalised output (:209)
                 last = out.reshape(B, h, w, d) if B == 1 else out.contiguous().view(B, h, w, d)
             del normed
@@ -217,7 +217,9 @@ class DeformableDETR(nn.Module):
         device = samples.tensors.device
         feats = self.backbone[0].forward_nhwc(samples.tensors, dt)   # layer1..4 NHWC
         sizes = samples.sizes
-        all_masks = [interp_mask(samples.mask, f.shape[1:3]) for f in feats]
+        # the padding masks per level depend only on the input mask: cached per mask tensor
+        all_masks = [K.cached(samples.mask, ('interp', tuple(f.shape[1:3])),
+                              lambda m, hw=tuple(f.shape[1:3]): interp_mask(m, hw)) for f in feats]
         features_all = [NestedTensor(nhwc_as_nchw(f), m, sizes) for f, m in zip(feats, all_masks)]
         features = features_all[-3:]
         cur_nhwc = feats[-3:]
@@ -263,17 +265,18 @@ class DeformableDETR(nn.Module):
         hs, memory, init_reference, inter_references, _, _ = self.transformer.forward_flat(
             src, geo['lvl_pos'], geo, self.query_embed.weight, targets)
 
-        outputs_classes, outputs_coords = [], []
-        for lvl in range(hs.shape[0]):
-            outputs_classes.append(K.linear(hs[lvl], self.class_embed[lvl].weight, self.class_embed[lvl].bias,
-                                            out_dtype=torch.float32))
-            if self.with_box_refine:
-                outputs_coords.append(inter_references[lvl])
-            else:
+        nl = hs.shape[0]
+        n_cls = self.class_embed[0].weight.shape[0]
+        outputs_class = torch.empty((nl,) + tuple(hs.shape[1:3]) + (n_cls,), dtype=torch.float32, device=device)
+        outputs_coords = []
+        for lvl in range(nl):
+            K.linear(hs[lvl], self.class_embed[lvl].weight, self.class_embed[lvl].bias, out_dtype=torch.float32,
+                     out=outputs_class[lvl].view(-1, n_cls))
+            if not self.with_box_refine:
                 tmp = mlp_fast(self.bbox_embed[lvl], hs[lvl])
                 outputs_coords.append(K.box_refine(tmp, init_reference, want_input=False)[0])
-        outputs_class = torch.stack(outputs_classes)
-        outputs_coord = torch.stack(outputs_coords)
+        # with box refinement the per-layer boxes ARE the decoder's refined references (module doc)
+        outputs_coord = inter_references if self.with_box_refine else torch.stack(outputs_coords)
         out = {'pred_logits': outputs_class[-1], 'pred_boxes': outputs_coord[-1], 'hs_embed': hs[-1].float()}
         if self.aux_loss:
             out['aux_outputs'] = self._set_aux_loss(outputs_class, outputs_coord)

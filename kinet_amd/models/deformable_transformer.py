@@ -178,10 +178,10 @@ class DeformableTransformerDecoderLayer(nn.Module):
         return A.layer_norm(tgt + self.dropout4(tgt2), self.norm3)
 
     def forward(self, tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask=None,
-                query_attn_mask=None, value=None):
+                query_attn_mask=None, value=None, out=None):
         if fast_path(self):
             return self.forward_fast(tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask,
-                                     query_attn_mask, value)
+                                     query_attn_mask, value, out)
         q = k = self.with_pos_embed(tgt, query_pos)
         # nn.MultiheadAttention on (L, B, E) transposes (:371) == the batch-first kinet path
         tgt2 = A.multihead_attention(self.self_attn, q, k, tgt, key_padding_mask=query_attn_mask)
@@ -192,7 +192,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
         return self.forward_ffn(tgt)
 
     def forward_fast(self, tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask=None,
-                     query_attn_mask=None, value=None):
+                     query_attn_mask=None, value=None, out=None):
         # deformable_transformer.py:367-386
         d = tgt.shape[-1]
         sa = self.self_attn
@@ -207,10 +207,14 @@ class DeformableTransformerDecoderLayer(nn.Module):
             value = ca.project_value(src, src_padding_mask)
         samp = ca.sample(tgt, reference_points, value, src_spatial_shapes, query_attn_mask, query_add=query_pos)
         tgt = K.linear(samp, ca.output_proj.weight, ca.output_proj.bias, residual=tgt, ln=(n1.weight, n1.bias, n1.eps))
+        out2 = None if out is None else out.view(-1, out.shape[-1])
         if K.ffn_supported(tgt, self.linear1, self.linear2):
-            return K.ffn_fused(tgt, self.linear1, self.linear2, n3)
-        h = K.linear(tgt, self.linear1.weight, self.linear1.bias, relu=True)
-        return K.linear(h, self.linear2.weight, self.linear2.bias, residual=tgt, ln=(n3.weight, n3.bias, n3.eps))
+            y = K.ffn_fused(tgt, self.linear1, self.linear2, n3, out=out2)
+        else:
+            h = K.linear(tgt, self.linear1.weight, self.linear1.bias, relu=True)
+            y = K.linear(h, self.linear2.weight, self.linear2.bias, residual=tgt, ln=(n3.weight, n3.bias, n3.eps),
+                         out=out2)
+        return y if out is None else out
 
 
 def mlp_fast(mlp, x, out_dtype=torch.float32):
@@ -284,21 +288,29 @@ class DeformableTransformerDecoder(nn.Module):
         nh = ca0.n_heads
         values = K.value_proj_headmajor(src, vw, vb, d // nh, row_mask=src_padding_mask,
                                         out_dtype=value_dtype_for(src.dtype))                # (nl*M, B, S, D)
-        intermediate, intermediate_reference_points = [], []
+        # every layer writes its output / refined boxes straight into the stacked result
+        # (the reference stacks the intermediates afterwards, :427-432)
+        B, Q = tgt.shape[:2]
+        hs_buf = torch.empty((nl, B, Q, d), dtype=tgt.dtype, device=tgt.device) if self.return_intermediate else None
+        ref_buf = None
+        if self.return_intermediate and self.bbox_embed is not None:
+            ref_buf = torch.empty((nl, B, Q, 4), dtype=torch.float32, device=tgt.device)
+        intermediate_reference_points = []
         for lid, layer in enumerate(self.layers):
             output = layer(output, query_pos, ref_in, src, src_spatial_shapes, src_padding_mask, query_attn_mask,
-                           value=values[lid * nh:(lid + 1) * nh])
+                           value=values[lid * nh:(lid + 1) * nh], out=None if hs_buf is None else hs_buf[lid])
             last = lid == nl - 1
             if self.bbox_embed is not None:
                 tmp = mlp_fast(self.bbox_embed[lid], output)
-                reference_points, nxt = K.box_refine(tmp, reference_points, vr, want_input=not last)
+                reference_points, nxt = K.box_refine(tmp, reference_points, vr, want_input=not last,
+                                                     out=None if ref_buf is None else ref_buf[lid])
                 if not last:
                     ref_in = nxt
             if self.return_intermediate:
-                intermediate.append(output)
                 intermediate_reference_points.append(reference_points)
         if self.return_intermediate:
-            return torch.stack(intermediate), torch.stack(intermediate_reference_points)
+            refs = ref_buf if ref_buf is not None else torch.stack(intermediate_reference_points)
+            return hs_buf, refs
         return output, reference_points
 
 
@@ -396,6 +408,20 @@ class DeformableTransformer(nn.Module):
                                                                                      device))]
         return geo
 
+    def _query_inputs(self, query_embed, bs, dt):
+        """(query_pos, tgt, reference_points) for `bs` frames without track queries, cached per
+        parameter version (deformable_transformer.py:198-202)."""
+        rp = self.reference_points
+        c = self.d_model
+
+        def make(qe, w, b):
+            q, t = torch.split(qe.detach(), c, dim=1)
+            ref = K.linear(q.float().contiguous(), w, b).sigmoid()
+            return (q.to(dt).unsqueeze(0).expand(bs, -1, -1).contiguous(),
+                    t.to(dt).unsqueeze(0).expand(bs, -1, -1).contiguous(),
+                    ref.unsqueeze(0).expand(bs, -1, -1).contiguous())
+        return K.cached_multi([query_embed, rp.weight, rp.bias], ('query_inputs', bs, dt), make)
+
     def forward_flat(self, src_flatten, lvl_pos_embed_flatten, geo, query_embed=None, targets=None):
         """deformable_transformer.py:159-257 on flattened inputs."""
         assert query_embed is not None
@@ -419,15 +445,23 @@ class DeformableTransformer(nn.Module):
 
         bs, _, c = memory.shape
         query_attn_mask = None
-        query_embed_, tgt = torch.split(query_embed, c, dim=1)
-        query_embed_ = query_embed_.unsqueeze(0).expand(bs, -1, -1)
-        tgt = tgt.unsqueeze(0).expand(bs, -1, -1)
-        rp = self.reference_points
-        if fast_path(self):
-            reference_points = K.linear(query_embed_.float(), rp.weight, rp.bias).sigmoid()
+        tracking = targets is not None and 'track_query_hs_embeds' in targets[0]
+        if fast_path(self) and not tracking:
+            # inference without track queries: the object queries, their positional half and
+            # the initial reference points depend only on parameters -> cached per parameter
+            # version, dtype and batch size (no per-forward casts / copies / GEMM)
+            query_embed_, tgt, reference_points = self._query_inputs(query_embed, bs, memory.dtype)
         else:
-            reference_points = A.linear_module(query_embed_, rp).sigmoid()
-        if targets is not None and 'track_query_hs_embeds' in targets[0]:
+            query_embed_, tgt = torch.split(query_embed, c, dim=1)
+            query_embed_ = query_embed_.unsqueeze(0).expand(bs, -1, -1)
+            tgt = tgt.unsqueeze(0).expand(bs, -1, -1)
+            rp = self.reference_points
+            if fast_path(self):
+                reference_points = K.linear(query_embed_[0].float(), rp.weight, rp.bias).sigmoid()
+                reference_points = reference_points.unsqueeze(0).expand(bs, -1, -1)
+            else:
+                reference_points = A.linear_module(query_embed_, rp).sigmoid()
+        if tracking:
             prev_hs_embed = torch.stack([t['track_query_hs_embeds'] for t in targets])
             prev_boxes = torch.stack([t['track_query_boxes'] for t in targets])
             prev_query_embed = torch.zeros_like(prev_hs_embed)
@@ -435,7 +469,7 @@ class DeformableTransformer(nn.Module):
             tgt = torch.cat([prev_hs_embed.to(tgt.dtype), tgt], dim=1)
             reference_points = torch.cat([prev_boxes[..., :2].to(reference_points.dtype), reference_points], dim=1)
         init_reference_out = reference_points
-        if fast_path(self):
+        if fast_path(self) and tracking:
             dt = memory.dtype
             tgt = tgt.to(dt).contiguous()
             query_embed_ = query_embed_.to(dt).contiguous()
