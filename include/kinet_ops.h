@@ -81,6 +81,13 @@ int kinet_sine_position_embed(const uint8_t* mask, const float* dim_t, const flo
                               int normalize, float scale, int64_t out_batch_stride, int out_dtype,
                               kinet_stream_t stream);
 
+/* Greedy non-maximum suppression with torchvision.ops.nms semantics (the tracker's track /
+ * detection NMS, tracker.py:437, :511): boxes (n, 4) xyxy f32, scores (n) f32 -> keep[i] = 1 for
+ * the kept boxes (in order of descending score, ties by index; a box is dropped when its IoU
+ * with a kept higher-ranked box exceeds iou_threshold).  n <= 4096, one workgroup. */
+int kinet_nms(const float* boxes, const float* scores, uint8_t* keep, int n, float iou_threshold,
+              kinet_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,6 +46,7 @@ _SIGS = {
     'kinet_mha_core': [P, I, P, I, P, I, P, I] + [I] * 5 + [F, I, P, P],
     'kinet_add': [P, P, P, I64, I, P],
     'kinet_box_refine': [P, P, I, P, P, P, I, I, I, P],
+    'kinet_nms': [P, P, P, I, F, P],
     'kinet_sine_position_embed': [P, P, P, P] + [I] * 8 + [F, I64, I, P],
     'kinet_transpose': [P, P, I, I, I64, I64, I, P],
     'kinet_im2col_nhwc': [P, P] + [I] * 13 + [P],

@@ -777,3 +777,63 @@ extern "C" int kinet_sine_position_embed(const uint8_t* mask, const float* dim_t
     KINET_LAUNCH_CHECK();
     return KINET_OK;
 }
+
+// ---------------------------------------------------------------------------------
+// greedy non-maximum suppression (torchvision.ops.nms semantics, tracker.py:437, :511)
+// ---------------------------------------------------------------------------------
+namespace kinet {
+namespace {
+constexpr int NMS_MAX = 4096;
+
+// one workgroup: rank every box by score (descending, ties by index -- a stable order), then
+// walk the ranks; each kept box suppresses, in parallel, every later box with IoU > thresh
+__global__ __launch_bounds__(1024) void nms_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
+                                                   uint8_t* __restrict__ keep, int n, float thresh) {
+    __shared__ int order[NMS_MAX];
+    __shared__ uint8_t supp[NMS_MAX];
+    __shared__ int cur;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const float si = scores[i];
+        int r = 0;
+        for (int j = 0; j < n; ++j) {
+            const float sj = scores[j];
+            r += (sj > si || (sj == si && j < i)) ? 1 : 0;
+        }
+        order[r] = i;
+        supp[i] = 0;
+        keep[i] = 0;
+    }
+    __syncthreads();
+    for (int r = 0; r < n; ++r) {
+        if (threadIdx.x == 0) cur = supp[order[r]] ? -1 : order[r];
+        __syncthreads();
+        const int i = cur;
+        if (i >= 0) {
+            if (threadIdx.x == 0) keep[i] = 1;
+            const float x1 = boxes[4 * i], y1 = boxes[4 * i + 1], x2 = boxes[4 * i + 2], y2 = boxes[4 * i + 3];
+            const float ai = (x2 - x1) * (y2 - y1);
+            for (int k = r + 1 + threadIdx.x; k < n; k += blockDim.x) {
+                const int j = order[k];
+                const float* b = boxes + 4 * j;
+                const float w = fmaxf(fminf(x2, b[2]) - fmaxf(x1, b[0]), 0.f);
+                const float h = fmaxf(fminf(y2, b[3]) - fmaxf(y1, b[1]), 0.f);
+                const float inter = w * h;
+                const float iou = inter / (ai + (b[2] - b[0]) * (b[3] - b[1]) - inter);
+                if (iou > thresh) supp[j] = 1;
+            }
+        }
+        __syncthreads();
+    }
+}
+}  // namespace
+}  // namespace kinet
+
+extern "C" int kinet_nms(const float* boxes, const float* scores, uint8_t* keep, int n, float iou_threshold,
+                         kinet_stream_t stream) {
+    using namespace kinet;
+    KINET_CHECK_ARG(n >= 0 && n <= NMS_MAX, "nms: %d boxes (at most %d)", n, NMS_MAX);
+    if (n == 0) return KINET_OK;
+    hipLaunchKernelGGL(nms_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, boxes, scores, keep, n, iou_threshold);
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}

@@ -384,6 +384,21 @@ def sine_position_embed(mask, dim_t, num_pos_feats, three_d=False, frame=0, fram
     return out
 
 
+def nms(boxes, scores, iou_threshold):
+    """torchvision.ops.nms semantics on the GPU: indices of the kept boxes, by descending score
+    (ties by index).  boxes (n, 4) xyxy, scores (n)."""
+    N.require_gpu(boxes, scores)
+    n = boxes.shape[0]
+    keep = torch.zeros(n, dtype=torch.uint8, device=boxes.device)
+    if n:
+        b = boxes.float().contiguous()
+        s = scores.float().contiguous()
+        N.call('kinet_nms', N.ptr(b), N.ptr(s), N.ptr(keep), n, float(iou_threshold), N.stream(boxes.device))
+        idx = keep.nonzero().flatten()
+        return idx[torch.argsort(-s[idx], stable=True)]
+    return keep.nonzero().flatten()
+
+
 # --------------------------------------------------------------------------- attention
 def mha_core(q, k, v, heads, scale, key_mask=None, out=None):
     """q (B, Lq, E) (row stride may exceed E), k/v (B, Lk, E) -> (B, Lq, E)."""

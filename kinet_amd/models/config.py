@@ -38,6 +38,12 @@ NAMED = {
     'train_full_res': dict(img_transform={'max_size': 1920, 'val_width': 1080}),
 }
 
+# cfgs/track.yaml:28-49, the tracker thresholds as shipped
+TRACKER_CFG = dict(public_detections=False, detection_obj_score_thresh=0.4, track_obj_score_thresh=0.4,
+                   detection_nms_thresh=0.9, track_nms_thresh=0.9, steps_termination=1, prev_frame_dist=1,
+                   inactive_patience=-1, reid_sim_threshold=0.0, reid_sim_only=False, reid_score_thresh=0.4,
+                   reid_greedy_matching=False)
+
 
 def load_args(*names, **overrides):
     d = dict(DEFAULTS)
