@@ -26,7 +26,10 @@
 //    (Cin % 8 == 0) so the im2col gather is a 16-byte load or a zero fill.
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "../../include/kinet_gemm.h"
 #include "common.h"
@@ -38,7 +41,9 @@ namespace {
 // diagnostic kernel-selection flags (kinet_gemm_set_flags): bit 1 = allow gemm_big_kernel
 // (measured slower than gemm_kernel on every detector shape, DESIGN.md, so off by default);
 // bit 2 = never use the resident-weight kernel (gemm_rw.hip); bit 4 = LDS-DMA gemm_dma_kernel;
-// bit 32 = never use the dedicated stem convolution (stem.hip)
+// bit 32 = never use the dedicated stem convolution (stem.hip); bit 64 = 8-wave LDS-DMA tiles
+// (256x128 / 128x256) where their tile rounds are well filled; bit 128 = stream-K 8-wave tiles;
+// bit 256 = 8-wave 256x256 / 256x128 data-parallel tiles wherever eligible
 int kinet_gemm_flags = 0;
 // diagnostic tile override for gemm_kernel (kinet_gemm_force_tile; 0 = heuristic)
 int force_bm = 0, force_bn = 0;
@@ -295,6 +300,18 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
     // when Cin is a multiple of the K-step, one K-step lies inside one filter tap: the tap
     // (kh, kw) is wave-uniform and computed on the scalar unit, not per lane
     const bool tap_uniform = CONV && (p.Cin % BK) == 0;
+    const int nk = (K - kbeg + BK - 1) / BK;
+    // K-step order of a multi-tap conv: channel-chunk-major, tap-minor -- the KH*KW shifted
+    // reads of one input-channel chunk run in consecutive K-steps (the rows they touch are
+    // still in L2) instead of KH*KW passes over all channels; the weight columns follow
+    const int ntaps = CONV ? p.K / p.Cin : 1;
+    const bool korder = tap_uniform && p.kchunk == 0 && ntaps > 1;
+    const int nchunk = p.Cin / BK;
+    auto kmap = [&](int kt) -> int {
+        if (!korder || kt >= nk) return kt * BK;
+        const int c = kt / ntaps, t = kt - c * ntaps;
+        return (t * nchunk + c) * BK;
+    };
     // Offsets past the edges / padding taps get bit 31 set: past num_records, so the range
     // check returns zeros.  Computed arithmetically (no select): hipcc otherwise branches
     // around the offset math of each load (s_and_saveexec) to skip it for masked lanes.
@@ -351,7 +368,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
 #pragma unroll
         for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = (K - kbeg + BK - 1) / BK;
     auto compute = [&](int buf) {
         const char* xl = lds + buf * STAGE;
         const char* wl = xl + BM * ROWB;
@@ -377,13 +393,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
     // a conditional load makes hipcc's vmcnt count assume the short path and drain the
     // younger prefetch before every LDS write
     auto step = [&](int kt, u32x4 (&xi)[XR], u32x4 (&wi)[WR], const u32x4 (&xn)[XR], const u32x4 (&wn)[WR]) {
-        load_tile((kt + 2) * BK, xi, wi);
+        load_tile(kmap(kt + 2), xi, wi);
         compute(kt & 1);
         store_tile((kt + 1) & 1, xn, wn);
         __syncthreads();
     };
-    load_tile(0, xs0, ws0);
-    load_tile(BK, xs1, ws1);
+    load_tile(kmap(0), xs0, ws0);
+    load_tile(kmap(1), xs1, ws1);
     store_tile(0, xs0, ws0);
     __syncthreads();
     // two K-steps per iteration, both unconditional (an odd last step multiplies zeros)
@@ -409,6 +425,95 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
 }
 
 #include "gemm_dma.h"   // gemm_dma_kernel: the same tiles staged by LDS-DMA through a 3-slot ring
+#include "gemm_sk.h"    // gemm_sk_kernel: stream-K scheduling of the 8-wave LDS-DMA tiles
+
+// Stream-K workspace, one per (device, stream): the partial-tile slots and the flag words of
+// gemm_sk_kernel.  Kernels on one stream run in order, so a stream's launches share it; the
+// epoch (launch counter) makes the flags self-resetting.  Grown (never shrunk) on demand,
+// outside graph capture only.
+struct SkWorkspace {
+    float* part = nullptr;
+    unsigned* flags = nullptr;
+    size_t part_bytes = 0;
+    int nflags = 0;
+    unsigned epoch = 0;
+};
+std::mutex sk_mutex;
+std::map<std::pair<int, hipStream_t>, SkWorkspace> sk_pool;
+
+int sk_num_cus() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+    return n;
+}
+
+bool sk_workspace(hipStream_t s, size_t part_bytes, int nflags, float** part, unsigned** flags, unsigned* epoch) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    std::lock_guard<std::mutex> guard(sk_mutex);
+    SkWorkspace& w = sk_pool[std::make_pair(dev, s)];
+    if (w.part_bytes < part_bytes || w.nflags < nflags || w.epoch == 0xffffffffu) {
+        if (w.part) {
+            // the stream's earlier launches may still read the old buffers
+            if (hipStreamSynchronize(s) != hipSuccess) return false;
+            (void)hipFree(w.part);
+            (void)hipFree(w.flags);
+        }
+        w = SkWorkspace{};
+        const size_t fbytes = ((size_t)nflags * 4 + 15) / 16 * 16;
+        if (hipMalloc(&w.part, part_bytes) != hipSuccess) {
+            w = SkWorkspace{};
+            return false;
+        }
+        if (hipMalloc(&w.flags, fbytes) != hipSuccess || hipMemsetAsync(w.flags, 0, fbytes, s) != hipSuccess) {
+            (void)hipFree(w.part);
+            w = SkWorkspace{};
+            return false;
+        }
+        w.part_bytes = part_bytes;
+        w.nflags = nflags;
+    }
+    *part = w.part;
+    *flags = w.flags;
+    *epoch = ++w.epoch;
+    return true;
+}
+
+// Stream-K launch of a 16-bit GEMM / implicit conv on 256x256 (N >= 256) or 256x128 tiles;
+// false = not eligible (the caller falls back to the data-parallel kernels).
+template <typename T, typename TO, bool CONV>
+bool launch_sk(const GemmArgs& a, hipStream_t stream) {
+    if constexpr (sizeof(T) != 2) {
+        return false;
+    } else {
+        if (a.ln_g != nullptr || a.A2 != nullptr || a.kchunk != 0 || a.M < 4096 || a.N < 128) return false;
+        const bool wide = a.N >= 256;
+        const int bm = 256, bn = wide ? 256 : 128;
+        const int nMt = (a.M + bm - 1) / bm, nNt = (a.N + bn - 1) / bn;
+        const long tiles = (long)nMt * nNt;
+        const int nk = (a.K + 63) / 64;
+        const long total = tiles * nk;
+        const int cus = sk_num_cus();
+        const long per = (total + cus - 1) / cus;
+        if (tiles >= (1L << 30) || per < 2) return false;
+        const int grid = (int)((total + per - 1) / per);
+        float* part = nullptr;
+        unsigned* flags = nullptr;
+        unsigned epoch = 0;
+        if (!sk_workspace(stream, (size_t)grid * bm * bn * 4, grid, &part, &flags, &epoch)) return false;
+        if (wide)
+            hipLaunchKernelGGL((gemm_sk_kernel<T, TO, 256, 256, 2, 4, CONV, 2>), dim3(grid), dim3(512), 0, stream, a,
+                               nNt, (int)tiles, (int)per, part, flags, epoch);
+        else
+            hipLaunchKernelGGL((gemm_sk_kernel<T, TO, 256, 128, 4, 2, CONV, 3>), dim3(grid), dim3(512), 0, stream, a,
+                               nNt, (int)tiles, (int)per, part, flags, epoch);
+        return true;
+    }
+}
 
 // Large-M GEMM / implicit conv: 512 threads (8 waves, WGM x WGN, each wave a (BM/WGM) x 64
 // output tile), BM x BN tile with BN in {128, 256}, BK = 64 (one 128-byte LDS row).
@@ -616,6 +721,10 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;
     }
+    if ((kinet_gemm_flags & 128) && force_bm == 0 && launch_sk<T, TO, CONV>(a, stream)) {
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
     int bm, bn;
     if (ln) {
         KINET_CHECK_ARG(a.N <= 320, "gemm: fused LayerNorm needs N <= 320 (got %d)", a.N);
@@ -639,6 +748,31 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         // slots: 3-6 % faster than 64x128 at batch 16 (tools/sweep_conv.py 16), neutral at 8
         if (CONV && a.K >= 1152 && a.N >= 128 && t128 >= 1000) bm = bn = 128;
     }
+    // 8-wave LDS-DMA tiles (one workgroup per CU, 256 slots): when their last round of tiles
+    // is well filled (tail quantisation is what costs them on the mid-size conv shapes)
+    if (sizeof(T) == 2 && (kinet_gemm_flags & 64) && !ln && a.A2 == nullptr && a.kchunk == 0 && a.N >= 128 &&
+        a.M >= 4096) {
+        double best = 0.0;
+        for (int c = 0; c < 2; ++c) {
+            const int tm = c ? 128 : 256, tn = c ? 256 : 128;
+            if (tn == 256 && a.N < 256) continue;
+            const long t = (long)((a.M + tm - 1) / tm) * ((a.N + tn - 1) / tn);
+            const long rounds = (t + 255) / 256;
+            const double eff = (double)a.M * a.N / ((double)rounds * 256.0 * tm * tn);
+            if (eff > best) {
+                best = eff;
+                if (eff >= 0.75) {
+                    bm = tm;
+                    bn = tn;
+                }
+            }
+        }
+    }
+    if (sizeof(T) == 2 && (kinet_gemm_flags & 256) && !ln && a.A2 == nullptr && a.kchunk == 0 && a.N >= 128 &&
+        a.M >= 4096) {
+        bm = 256;
+        bn = a.N >= 256 ? 256 : 128;
+    }
     if (force_bm && !ln) {
         bm = force_bm;
         bn = force_bn;
@@ -652,6 +786,19 @@ int launch(const GemmArgs& a, hipStream_t stream) {
     // kernel on the detector's conv / GEMM shapes at batch 8 (tools/sweep_conv.py), so the
     // register path stays the default; A2 (load-time add) needs the register path anyway
     const bool dma = a.A2 == nullptr && (kinet_gemm_flags & 16);
+    // 8-wave LDS-DMA tiles (16-bit operands, no load-time A2 add, no fused LayerNorm)
+    if constexpr (sizeof(T) == 2) {
+        if (!ln && a.A2 == nullptr && (bm == 256 || bn == 256)) {
+            if (bm == 256 && bn == 256)
+                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 256, 2, 4, CONV, false, 2>), grid, dim3(512), 0, stream, a, nNt);
+            else if (bm == 256)
+                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 128, 4, 2, CONV, false>), grid, dim3(512), 0, stream, a, nNt);
+            else
+                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 128, 256, 2, 4, CONV, false>), grid, dim3(512), 0, stream, a, nNt);
+            KINET_LAUNCH_CHECK();
+            return KINET_OK;
+        }
+    }
 #define L_(BM_, BN_, WM_, WN_, LN_)                                                                             \
     do {                                                                                                        \
         if (dma) hipLaunchKernelGGL((gemm_dma_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0,   \
@@ -884,7 +1031,8 @@ extern "C" int kinet_gemm_splitk(const void* A, const void* B, void* C, int M, i
 }
 
 extern "C" int kinet_gemm_force_tile(int bm, int bn) {
-    KINET_CHECK_ARG((bm == 0 && bn == 0) || ((bm == 32 && bn == 64) || ((bm == 64 || bm == 128) && (bn == 64 || bn == 128))),
+    KINET_CHECK_ARG((bm == 0 && bn == 0) || ((bm == 32 && bn == 64) || ((bm == 64 || bm == 128) && (bn == 64 || bn == 128))) ||
+                        (bm == 256 && bn == 128) || (bm == 128 && bn == 256) || (bm == 256 && bn == 256),
                     "gemm_force_tile: unsupported tile %dx%d", bm, bn);
     force_bm = bm;
     force_bn = bn;

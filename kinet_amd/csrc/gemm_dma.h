@@ -11,15 +11,23 @@
 //    step kt-1 used; a counted `s_waitcnt vmcnt` (one step's DMA count) retires step kt while
 //    kt+1 stays in flight across the raw s_barrier; the loop holds no VGPR-destination load,
 //    so hipcc adds no vmcnt(0) of its own;
-//  * steps past K are issued too (range check -> zeros): no conditional DMA, exact counts.
+//  * steps past K are issued too (range check -> zeros): no conditional DMA, exact counts;
+//  * 4 waves (64x128-class tiles, 2 workgroups per CU) or 8 waves (256x128 / 128x256 tiles,
+//    64x64 per wave, one workgroup per CU: 3 x 48 KiB ring, the 256x132 f32 epilogue tile
+//    reuses it; 256x256, 128x64 per wave: 2 x 64 KiB ring, epilogue in two row halves) --
+//    the 8-wave tiles halve the LDS fragment reads per MFMA of the 4-wave 64x128 tile and
+//    the L2 -> LDS bytes per flop.
 #pragma once
 
-template <int BM, int BN>
+template <int BM, int BN, int NS_>
 struct DmaSmem {
     static constexpr int STAGE = (BM + BN) * ROWB;
-    static constexpr int NS = 3;
+    static constexpr int NS = NS_;
     static constexpr int EPI_LD = BN + 4;
-    static constexpr int EPI = BM * EPI_LD * 4;
+    // the f32 epilogue tile is parked whole, or in two row halves when the whole tile would
+    // not fit beside the ring (256x256)
+    static constexpr int EPI_ROWS = (BM * EPI_LD * 4 <= NS * STAGE || BM * EPI_LD * 4 <= 160 * 1024) ? BM : BM / 2;
+    static constexpr int EPI = EPI_ROWS * EPI_LD * 4;
     static constexpr int BYTES = (NS * STAGE > EPI) ? NS * STAGE : EPI;
 };
 
@@ -34,20 +42,26 @@ __device__ __forceinline__ void gemm_lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
-template <typename T, typename TO, int BM, int BN, int WGM, int WGN, bool CONV, bool LN>
-__global__ __launch_bounds__(256, 2) void gemm_dma_kernel(const GemmArgs p, const int nNt) {
-    static_assert(WGM * WGN == 4, "4 waves");
+template <typename T, typename TO, int BM, int BN, int WGM, int WGN, bool CONV, bool LN, int NS_ = 3>
+__global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN == 4 ? 2 : 1) void gemm_dma_kernel(const GemmArgs p,
+                                                                                        const int nNt) {
+    constexpr int NW = WGM * WGN;
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
     constexpr int EPC = Mma<T>::EPC;
     constexpr int BK = ROWB / (int)sizeof(T);
     constexpr int WTM = BM / WGM, WTN = BN / WGN;   // wave tile
     constexpr int TM = WTM / 16, TN = WTN / 16;
-    constexpr int STAGE = DmaSmem<BM, BN>::STAGE;
-    constexpr int NS = DmaSmem<BM, BN>::NS;
-    constexpr int EPI_LD = DmaSmem<BM, BN>::EPI_LD;
-    constexpr int XS = BM / 32, WS = BN / 32;      // DMA wave-instructions per wave per K-step
+    using SM = DmaSmem<BM, BN, NS_>;
+    constexpr int STAGE = SM::STAGE;
+    constexpr int NS = SM::NS;
+    constexpr int EPI_LD = SM::EPI_LD;
+    constexpr int EROWS = SM::EPI_ROWS;
+    static_assert(NS == 2 || NS == 3, "ring of 2 or 3 slots");
+    static_assert(EROWS % WTM == 0, "a wave's rows must lie in one epilogue part");
+    constexpr int XS = BM / (8 * NW), WS = BN / (8 * NW);   // DMA wave-instructions per wave per K-step
     constexpr int SLOTS = XS + WS;
-    static_assert(BM % 32 == 0 && BN % 32 == 0, "whole 8-row groups per wave");
-    __shared__ __attribute__((aligned(16))) char lds[DmaSmem<BM, BN>::BYTES];
+    static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "whole 8-row groups per wave");
+    __shared__ __attribute__((aligned(16))) char lds[SM::BYTES];
 
     int bid = blockIdx.x;
     {
@@ -68,7 +82,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dma_kernel(const GemmArgs p, cons
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
 
-    // this lane's staging rows: A row-group wave + 4i (i < XS), B row-group wave + 4i (i < WS),
+    // this lane's staging rows: A row-group wave + NW*i (i < XS), B row-group wave + NW*i (i < WS),
     // row (lane >> 3) of the group, logical 16-byte chunk sch of the row
     const int rsub = lane >> 3;
     const int sch = (lane & 7) ^ rsub;            // (row & 7) == rsub: groups are 8-row aligned
@@ -77,7 +91,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dma_kernel(const GemmArgs p, cons
     bool xok[XS];
 #pragma unroll
     for (int i = 0; i < XS; ++i) {
-        const int m = m0 + (wave + 4 * i) * 8 + rsub;
+        const int m = m0 + (wave + NW * i) * 8 + rsub;
         xok[i] = m < M;
         if (CONV) {
             const int hw = p.Hout * p.Wout;
@@ -98,16 +112,26 @@ __global__ __launch_bounds__(256, 2) void gemm_dma_kernel(const GemmArgs p, cons
     bool wok[WS];
 #pragma unroll
     for (int i = 0; i < WS; ++i) {
-        const int n = n0 + (wave + 4 * i) * 8 + rsub;
+        const int n = n0 + (wave + NW * i) * 8 + rsub;
         wok[i] = n < N;
         wbase[i] = (unsigned)n * (unsigned)p.ldb;
     }
     const bool tap_uniform = CONV && (p.Cin % BK) == 0;
+    const int nk = (K - kbeg + BK - 1) / BK;
+    // channel-chunk-major, tap-minor K-step order (gemm_kernel's kmap)
+    const int ntaps = CONV ? p.K / p.Cin : 1;
+    const bool korder = tap_uniform && p.kchunk == 0 && ntaps > 1;
+    const int nchunk = p.Cin / BK;
+    auto kmap = [&](int kt) -> int {
+        if (!korder || kt >= nk) return kt * BK;
+        const int c = kt / ntaps, t = kt - c * ntaps;
+        return (t * nchunk + c) * BK;
+    };
 
     // DMA of K-step kt into ring slot kt % NS (offsets with bit 31 set read zeros)
     auto stage = [&](int kt) {
         char* st = lds + (kt % NS) * STAGE;
-        const int k0 = kbeg + kt * BK;
+        const int k0 = kbeg + kmap(kt);
         const int k = k0 + sch * EPC;
         const unsigned kbad = k < K ? 0u : OOB;
         int kh = 0, kw = 0, dk = 0;
@@ -135,11 +159,11 @@ __global__ __launch_bounds__(256, 2) void gemm_dma_kernel(const GemmArgs p, cons
             } else {
                 off = xbase[i] + (unsigned)k;
             }
-            dma16(ra, st + (wave + 4 * i) * 8 * ROWB, (off * (unsigned)sizeof(T)) | bad);
+            dma16(ra, st + (wave + NW * i) * 8 * ROWB, (off * (unsigned)sizeof(T)) | bad);
         }
 #pragma unroll
         for (int i = 0; i < WS; ++i)
-            dma16(rb, st + (BM + (wave + 4 * i) * 8) * ROWB,
+            dma16(rb, st + (BM + (wave + NW * i) * 8) * ROWB,
                   ((wbase[i] + (unsigned)k) * (unsigned)sizeof(T)) | kbad | (wok[i] ? 0u : OOB));
     };
 
@@ -169,30 +193,36 @@ __global__ __launch_bounds__(256, 2) void gemm_dma_kernel(const GemmArgs p, cons
         }
     };
 
-    const int nk = (K - kbeg + BK - 1) / BK;
     stage(0);
-    stage(1);
+    if (NS == 3) stage(1);
     for (int kt = 0; kt < nk; ++kt) {
-        gemm_wait_vmcnt<SLOTS>();      // this wave's step-kt DMA landed (kt+1 may fly)
-        gemm_lds_barrier();            // everyone's landed; everyone done with step kt-1's slot
-        stage(kt + 2);
+        gemm_wait_vmcnt<(NS - 2) * SLOTS>();   // this wave's step-kt DMA landed (kt+1 may fly)
+        gemm_lds_barrier();                    // everyone's landed; everyone done with step kt-1's slot
+        stage(kt + NS - 1);
         compute(kt % NS);
     }
-    gemm_wait_vmcnt<0>();              // the two zero-filled steps past the end
+    gemm_wait_vmcnt<0>();              // the zero-filled steps past the end
     gemm_lds_barrier();
 
-    // ---- epilogue: residual rows in flight, park the f32 tile in LDS, stream whole rows ----
-    ResRows<TO, BN, 4, BM> rp;
-    rp.issue(p, m0, n0, 0, wave, lane);
+    // ---- epilogue: residual rows in flight, park the f32 tile (or one row half of it) in
+    // LDS, stream whole rows ----
     float* ep = reinterpret_cast<float*>(lds);
 #pragma unroll
-    for (int a = 0; a < TN; ++a)
+    for (int h = 0; h < BM / EROWS; ++h) {
+        ResRows<TO, BN, NW, EROWS> rp;
+        rp.issue(p, m0, n0, h * EROWS, wave, lane);
+        if (h) __syncthreads();
+        if ((wm * WTM) / EROWS == h) {
 #pragma unroll
-        for (int b = 0; b < TM; ++b) {
-            const int ml = wm * WTM + b * 16 + (lane & 15);
-            const int nl = wn * WTN + a * 16 + (lane >> 4) * 4;
-            *reinterpret_cast<f32x4*>(ep + ml * EPI_LD + nl) = acc[a][b];
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int b = 0; b < TM; ++b) {
+                    const int ml = wm * WTM - h * EROWS + b * 16 + (lane & 15);
+                    const int nl = wn * WTN + a * 16 + (lane >> 4) * 4;
+                    *reinterpret_cast<f32x4*>(ep + ml * EPI_LD + nl) = acc[a][b];
+                }
         }
-    __syncthreads();
-    epilogue_rows<TO, BN, EPI_LD, 4, LN, BM>(p, ep, m0, n0, 0, wave, lane, rp);
+        __syncthreads();
+        epilogue_rows<TO, BN, EPI_LD, NW, LN, EROWS>(p, ep, m0, n0, h * EROWS, wave, lane, rp);
+    }
 }

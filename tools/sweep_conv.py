@@ -18,7 +18,7 @@ def main():
               (100, 167, 256, 256, 3, 2), (50, 84, 256, 256, 3, 1), (50, 84, 512, 512, 3, 2), (25, 42, 512, 512, 3, 1),
               (25, 42, 2048, 256, 3, 2), (50, 84, 1024, 256, 1, 1), (100, 167, 512, 128, 1, 1), (25, 42, 512, 2048, 1, 1),
               (25, 42, 2048, 512, 1, 1), (100, 167, 512, 256, 1, 1), (50, 84, 1024, 512, 1, 1)]
-    tiles = [(0, 0), (128, 128), (64, 128), (128, 64), (64, 64)]
+    tiles = [(0, 0), (256, 128), (128, 256), (128, 128), (64, 128), (128, 64), (64, 64)]
     for H, W, Cin, Cout, k, s in shapes:
         x = torch.randn(B, H, W, Cin, device='cuda', dtype=dt)
         wp = K.pack_conv_weight(torch.randn(Cout, Cin, k, k, device='cuda') * 0.02, dt)
@@ -28,10 +28,16 @@ def main():
         res = []
         for bm, bn in tiles:
             L.kinet_gemm_force_tile(bm, bn)
-            for ks in ([None] if bm == 0 else [1, 2, 3, 4]):
+            for ks in ([None] if bm == 0 else [1] if bm == 256 or bn == 256 else [1, 2, 3, 4]):
                 if ks and ks > 1 and k * k * Cin < 512:
                     continue
                 try:
+                    if ks == 1:   # every tile must agree with the heuristic's output
+                        L.kinet_gemm_force_tile(0, 0)
+                        y0 = K.conv2d_nhwc(x, wp, s, p).float()
+                        L.kinet_gemm_force_tile(bm, bn)
+                        err = (K.conv2d_nhwc(x, wp, s, p).float() - y0).abs().max().item()
+                        assert err <= 0.02 * y0.abs().max().item(), (bm, bn, err)
                     t = timeit(lambda: K.conv2d_nhwc(x, wp, s, p, ksplit=ks), iters=10)
                 except RuntimeError as e:   # noqa: BLE001
                     continue
