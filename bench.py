@@ -68,7 +68,6 @@ def parse():
     ap.add_argument('--no-train', action='store_true', help='skip the config-4 training sub-benchmark')
     ap.add_argument('--train-steps', type=int, default=4)
     ap.add_argument('--cpu-seconds', type=float, default=20.0, help='bound on the CPU baseline sample')
-    ap.add_argument('--gemm-flags', type=int, default=0, help=argparse.SUPPRESS)   # kernel-selection A/B runs
     a = ap.parse_args()
     wl = WORKLOADS[a.workload]
     for k, wk in (('batch', 'batch'), ('streams', 'streams'), ('height', 'h'), ('width', 'w'), ('dtype', 'dtype')):
@@ -202,8 +201,6 @@ def main():
     wl = WORKLOADS[a.workload]
     from kinet_amd import _native
     from kinet_amd.models import nested_tensor_from_tensor_list
-    if a.gemm_flags:
-        _native.lib().kinet_gemm_set_flags(a.gemm_flags)
     model = build(dev, dtype, wl)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     # one independent batch per in-flight slot (distinct requests, all resident in HBM)

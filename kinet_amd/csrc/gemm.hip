@@ -26,10 +26,7 @@
 //    (Cin % 8 == 0) so the im2col gather is a 16-byte load or a zero fill.
 #include <hip/hip_runtime.h>
 
-#include <map>
-#include <mutex>
 #include <type_traits>
-#include <utility>
 
 #include "../../include/kinet_gemm.h"
 #include "common.h"
@@ -38,12 +35,10 @@
 namespace kinet {
 namespace {
 
-// diagnostic kernel-selection flags (kinet_gemm_set_flags): bit 1 = allow gemm_big_kernel
-// (measured slower than gemm_kernel on every detector shape, DESIGN.md, so off by default);
-// bit 2 = never use the resident-weight kernel (gemm_rw.hip); bit 4 = LDS-DMA gemm_dma_kernel;
-// bit 32 = never use the dedicated stem convolution (stem.hip); bit 64 = 8-wave LDS-DMA tiles
-// (256x128 / 128x256) where their tile rounds are well filled; bit 128 = stream-K 8-wave tiles;
-// bit 256 = 8-wave 256x256 / 256x128 data-parallel tiles wherever eligible
+// diagnostic kernel-selection flags (kinet_gemm_set_flags), by value: 2 = the 8-wave LDS-DMA
+// tiles (gemm_dma.h) wherever eligible; 4 = never the resident-weight kernel (gemm_rw.hip);
+// 8 = resident-weight kernel from M >= 256; 16 = LDS-DMA staging for the 4-wave tiles;
+// 32 = never the dedicated stem convolution (stem.hip)
 int kinet_gemm_flags = 0;
 // diagnostic tile override for gemm_kernel (kinet_gemm_force_tile; 0 = heuristic)
 int force_bm = 0, force_bn = 0;
@@ -425,306 +420,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
 }
 
 #include "gemm_dma.h"   // gemm_dma_kernel: the same tiles staged by LDS-DMA through a 3-slot ring
-#include "gemm_sk.h"    // gemm_sk_kernel: stream-K scheduling of the 8-wave LDS-DMA tiles
-
-// Stream-K workspace, one per (device, stream): the partial-tile slots and the flag words of
-// gemm_sk_kernel.  Kernels on one stream run in order, so a stream's launches share it; the
-// epoch (launch counter) makes the flags self-resetting.  Grown (never shrunk) on demand,
-// outside graph capture only.
-struct SkWorkspace {
-    float* part = nullptr;
-    unsigned* flags = nullptr;
-    size_t part_bytes = 0;
-    int nflags = 0;
-    unsigned epoch = 0;
-};
-std::mutex sk_mutex;
-std::map<std::pair<int, hipStream_t>, SkWorkspace> sk_pool;
-
-int sk_num_cus() {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-        n = 256;
-    return n;
-}
-
-bool sk_workspace(hipStream_t s, size_t part_bytes, int nflags, float** part, unsigned** flags, unsigned* epoch) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
-    std::lock_guard<std::mutex> guard(sk_mutex);
-    SkWorkspace& w = sk_pool[std::make_pair(dev, s)];
-    if (w.part_bytes < part_bytes || w.nflags < nflags || w.epoch == 0xffffffffu) {
-        if (w.part) {
-            // the stream's earlier launches may still read the old buffers
-            if (hipStreamSynchronize(s) != hipSuccess) return false;
-            (void)hipFree(w.part);
-            (void)hipFree(w.flags);
-        }
-        w = SkWorkspace{};
-        const size_t fbytes = ((size_t)nflags * 4 + 15) / 16 * 16;
-        if (hipMalloc(&w.part, part_bytes) != hipSuccess) {
-            w = SkWorkspace{};
-            return false;
-        }
-        if (hipMalloc(&w.flags, fbytes) != hipSuccess || hipMemsetAsync(w.flags, 0, fbytes, s) != hipSuccess) {
-            (void)hipFree(w.part);
-            w = SkWorkspace{};
-            return false;
-        }
-        w.part_bytes = part_bytes;
-        w.nflags = nflags;
-    }
-    *part = w.part;
-    *flags = w.flags;
-    *epoch = ++w.epoch;
-    return true;
-}
-
-// Stream-K launch of a 16-bit GEMM / implicit conv on 256x256 (N >= 256) or 256x128 tiles;
-// false = not eligible (the caller falls back to the data-parallel kernels).
-template <typename T, typename TO, bool CONV>
-bool launch_sk(const GemmArgs& a, hipStream_t stream) {
-    if constexpr (sizeof(T) != 2) {
-        return false;
-    } else {
-        if (a.ln_g != nullptr || a.A2 != nullptr || a.kchunk != 0 || a.M < 4096 || a.N < 128) return false;
-        const bool wide = a.N >= 256;
-        const int bm = 256, bn = wide ? 256 : 128;
-        const int nMt = (a.M + bm - 1) / bm, nNt = (a.N + bn - 1) / bn;
-        const long tiles = (long)nMt * nNt;
-        const int nk = (a.K + 63) / 64;
-        const long total = tiles * nk;
-        const int cus = sk_num_cus();
-        const long per = (total + cus - 1) / cus;
-        if (tiles >= (1L << 30) || per < 2) return false;
-        const int grid = (int)((total + per - 1) / per);
-        float* part = nullptr;
-        unsigned* flags = nullptr;
-        unsigned epoch = 0;
-        if (!sk_workspace(stream, (size_t)grid * bm * bn * 4, grid, &part, &flags, &epoch)) return false;
-        if (wide)
-            hipLaunchKernelGGL((gemm_sk_kernel<T, TO, 256, 256, 2, 4, CONV, 2>), dim3(grid), dim3(512), 0, stream, a,
-                               nNt, (int)tiles, (int)per, part, flags, epoch);
-        else
-            hipLaunchKernelGGL((gemm_sk_kernel<T, TO, 256, 128, 4, 2, CONV, 3>), dim3(grid), dim3(512), 0, stream, a,
-                               nNt, (int)tiles, (int)per, part, flags, epoch);
-        return true;
-    }
-}
-
-// Large-M GEMM / implicit conv: 512 threads (8 waves, WGM x WGN, each wave a (BM/WGM) x 64
-// output tile), BM x BN tile with BN in {128, 256}, BK = 64 (one 128-byte LDS row).
-// Operands are staged by LDS-DMA (buffer_load_dwordx4 ... lds): one wave-instruction fills
-// 8 consecutive 128-byte LDS rows (1 KiB, lane-linear), so the XOR swizzle is applied on
-// the SOURCE side -- lane l of a row-group loads logical chunk (l & 7) ^ (row & 7), and the
-// fragment reads use the same swz().  Out-of-range lanes (M/N edge, K tail, conv padding)
-// get an offset past num_records: the hardware writes zeros into LDS, so staging is
-// branch-free and needs no VGPRs.  Two LDS buffers; the loads of K-step k+1 are issued
-// before the MFMAs of step k.  The epilogue parks half the tile at a time in LDS and runs
-// the shared row epilogue with all 8 waves.
-template <int BM, int BN>
-struct BigSmem {
-    static constexpr int STAGE = (BM + BN) * ROWB;
-    static constexpr int EPI_LD = BN + 4;
-    static constexpr int EPI = (BM / 2) * EPI_LD * 4;
-    static constexpr int BYTES = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
-};
-
-
-template <typename T, typename TO, int BM, int BN, bool CONV, bool LN>
-__global__ __launch_bounds__(512, 1) void gemm_big_kernel(const GemmArgs p, const int nNt) {
-    static_assert(sizeof(T) == 2, "16-bit operands only");
-    constexpr int WGN = BN / 64, WGM = 8 / WGN;
-    constexpr int WTM = BM / WGM, TM = WTM / 16, TN = 4;
-    constexpr int BK = ROWB / (int)sizeof(T);
-    constexpr int XR = BM / 64, WR = BN / 64;     // LDS row-groups of 64 rows per operand
-    constexpr int STAGE = BigSmem<BM, BN>::STAGE;
-    constexpr int EPI_LD = BigSmem<BM, BN>::EPI_LD;
-    constexpr int HALF = BM / 2;
-    static_assert(HALF % WTM == 0, "a wave's rows must lie in one epilogue half");
-    __shared__ __attribute__((aligned(16))) char lds[BigSmem<BM, BN>::BYTES];
-
-    int bid = blockIdx.x;
-    {
-        const int nblk = gridDim.x, q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    }
-    const int mt = bid / nNt, nt = bid - (bid / nNt) * nNt;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave % WGM, wn = wave / WGM;
-    const int M = p.M, N = p.N, K = p.K;
-
-    constexpr unsigned OOB = 0x80000000u;
-    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
-
-    // this lane stages, in row-group i, tile row i*64 + wave*8 + (lane>>3), logical chunk sch
-    const int srow = wave * 8 + (lane >> 3);
-    const int sch = (lane & 7) ^ ((lane >> 3) & 7);
-    unsigned xbase[XR];
-    int xih[XR], xiw[XR];
-    bool xok[XR];
-#pragma unroll
-    for (int i = 0; i < XR; ++i) {
-        const int m = m0 + srow + 64 * i;
-        xok[i] = m < M;
-        if (CONV) {
-            const int hw = p.Hout * p.Wout;
-            const int img = m / hw;
-            const int rem = m - img * hw;
-            const int oh = rem / p.Wout, ow = rem - (rem / p.Wout) * p.Wout;
-            xih[i] = oh * p.stride - p.pad;
-            xiw[i] = ow * p.stride_w - p.pad_w;
-            xbase[i] = (unsigned)img * (unsigned)(p.Hin * p.Win * p.Cin);
-        } else {
-            xih[i] = xiw[i] = 0;
-            xbase[i] = (unsigned)m * (unsigned)p.lda;
-        }
-    }
-    unsigned wbase[WR];
-    bool wok[WR];
-#pragma unroll
-    for (int i = 0; i < WR; ++i) {
-        const int n = n0 + srow + 64 * i;
-        wok[i] = n < N;
-        wbase[i] = (unsigned)n * (unsigned)p.ldb;
-    }
-
-    auto stage = [&](int k0, int buf) {
-        char* xl = lds + buf * STAGE + wave * 8 * ROWB;
-        char* wl = lds + buf * STAGE + BM * ROWB + wave * 8 * ROWB;
-        const int k = k0 + sch * 8;
-        const bool kok = k < K;
-        int kh = 0, kw = 0, cc = k;
-        if (CONV) {
-            const int tap = k / p.Cin;
-            cc = k - tap * p.Cin;
-            kh = tap / p.KW;
-            kw = tap - kh * p.KW;
-        }
-#pragma unroll
-        for (int i = 0; i < XR; ++i) {
-            bool ok = xok[i] && kok;
-            unsigned off;
-            if (CONV) {
-                const int ih = xih[i] + kh, iw = xiw[i] + kw;
-                ok = ok && ih >= 0 && ih < p.Hin && iw >= 0 && iw < p.Win;
-                off = xbase[i] + (unsigned)((ih * p.Win + iw) * p.Cin + cc);
-            } else {
-                off = xbase[i] + (unsigned)k;
-            }
-            dma16(ra, xl + i * 64 * ROWB, ok ? off * (unsigned)sizeof(T) : OOB);
-        }
-#pragma unroll
-        for (int i = 0; i < WR; ++i)
-            dma16(rb, wl + i * 64 * ROWB, (wok[i] && kok) ? (wbase[i] + (unsigned)k) * (unsigned)sizeof(T) : OOB);
-    };
-
-    f32x4 acc[TN][TM];
-#pragma unroll
-    for (int a = 0; a < TN; ++a)
-#pragma unroll
-        for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    auto compute = [&](int buf) {
-        const char* xl = lds + buf * STAGE;
-        const char* wl = xl + BM * ROWB;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int ch = kk * 4 + (lane >> 4);
-            u32x4 bfr[TM], afr[TN];
-#pragma unroll
-            for (int t = 0; t < TN; ++t)
-                afr[t] = *reinterpret_cast<const u32x4*>(wl + swz(wn * 64 + t * 16 + (lane & 15), ch));
-#pragma unroll
-            for (int t = 0; t < TM; ++t)
-                bfr[t] = *reinterpret_cast<const u32x4*>(xl + swz(wm * WTM + t * 16 + (lane & 15), ch));
-#pragma unroll
-            for (int b = 0; b < TM; ++b)
-#pragma unroll
-                for (int a = 0; a < TN; ++a) Mma<T>::run(acc[a][b], afr[a], bfr[b]);
-        }
-    };
-
-    const int nk = (K + BK - 1) / BK;
-    stage(0, 0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) stage((kt + 1) * BK, (kt + 1) & 1);
-        compute(kt & 1);
-        __syncthreads();   // waits this thread's DMA (vmcnt) and everyone's reads of kt
-    }
-
-    float* ep = reinterpret_cast<float*>(lds);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        ResRows<TO, BN, 8, HALF> rp;
-        rp.issue(p, m0, n0, h * HALF, wave, lane);
-        if (h) __syncthreads();
-        if ((wm * WTM) / HALF == h) {
-#pragma unroll
-            for (int a = 0; a < TN; ++a)
-#pragma unroll
-                for (int b = 0; b < TM; ++b) {
-                    const int ml = wm * WTM - h * HALF + b * 16 + (lane & 15);
-                    const int nl = wn * 64 + a * 16 + (lane >> 4) * 4;
-                    *reinterpret_cast<f32x4*>(ep + ml * EPI_LD + nl) = acc[a][b];
-                }
-        }
-        __syncthreads();
-        epilogue_rows<TO, BN, EPI_LD, 8, LN, HALF>(p, ep, m0, n0, h * HALF, wave, lane, rp);
-    }
-}
-
-// Launch the 512-thread LDS-DMA kernel when the problem suits it (16-bit operands, large
-// M, N >= 128, no load-time A2 add); false = use the 256-thread kernel.
-template <typename T, typename TO, bool CONV>
-bool launch_big(const GemmArgs& a, hipStream_t stream) {
-    const bool ln = a.ln_g != nullptr;
-    if (a.A2 == nullptr && a.M >= 16384 && a.N >= 128 && (!ln || a.N <= 256) && (kinet_gemm_flags & 2)) {
-        const int bn = (a.N > 128 || ln) ? 256 : 128;   // LN needs the whole row in one tile
-        const long t256 = (long)((a.M + 255) / 256) * ((a.N + bn - 1) / bn);
-        const int bm = (bn == 256 && t256 < 512) ? 128 : 256;
-        const int nMt = (a.M + bm - 1) / bm, nNt = (a.N + bn - 1) / bn;
-        const long nblk = (long)nMt * nNt;
-        if (nblk >= (1L << 31)) return false;
-        dim3 grid((unsigned)nblk), block(512);
-#define B_(BM_, BN_, LN_) \
-    hipLaunchKernelGGL((gemm_big_kernel<T, TO, BM_, BN_, CONV, LN_>), grid, block, 0, stream, a, nNt)
-        if (ln) {
-            if (bm == 128) B_(128, 256, true);
-            else B_(256, 256, true);
-        } else if (bn == 128) B_(256, 128, false);
-        else if (bm == 128) B_(128, 256, false);
-        else B_(256, 256, false);
-#undef B_
-        return true;
-    }
-    return false;
-}
-template <>
-bool launch_big<float, float, false>(const GemmArgs&, hipStream_t) { return false; }
-template <>
-bool launch_big<float, float, true>(const GemmArgs&, hipStream_t) { return false; }
-
 template <typename T, typename TO, bool CONV>
 int launch(const GemmArgs& a, hipStream_t stream) {
     if (a.M == 0 || a.N == 0) return KINET_OK;
     const bool ln = a.ln_g != nullptr;
-    if (a.kchunk == 0 && launch_big<T, TO, CONV>(a, stream)) {
-        KINET_LAUNCH_CHECK();
-        return KINET_OK;
-    }
-    if ((kinet_gemm_flags & 128) && force_bm == 0 && launch_sk<T, TO, CONV>(a, stream)) {
-        KINET_LAUNCH_CHECK();
-        return KINET_OK;
-    }
     int bm, bn;
     if (ln) {
         KINET_CHECK_ARG(a.N <= 320, "gemm: fused LayerNorm needs N <= 320 (got %d)", a.N);
@@ -748,30 +447,25 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         // slots: 3-6 % faster than 64x128 at batch 16 (tools/sweep_conv.py 16), neutral at 8
         if (CONV && a.K >= 1152 && a.N >= 128 && t128 >= 1000) bm = bn = 128;
     }
-    // 8-wave LDS-DMA tiles (one workgroup per CU, 256 slots): when their last round of tiles
-    // is well filled (tail quantisation is what costs them on the mid-size conv shapes)
-    if (sizeof(T) == 2 && (kinet_gemm_flags & 64) && !ln && a.A2 == nullptr && a.kchunk == 0 && a.N >= 128 &&
-        a.M >= 4096) {
-        double best = 0.0;
-        for (int c = 0; c < 2; ++c) {
-            const int tm = c ? 128 : 256, tn = c ? 256 : 128;
-            if (tn == 256 && a.N < 256) continue;
-            const long t = (long)((a.M + tm - 1) / tm) * ((a.N + tn - 1) / tn);
-            const long rounds = (t + 255) / 256;
-            const double eff = (double)a.M * a.N / ((double)rounds * 256.0 * tm * tn);
-            if (eff > best) {
-                best = eff;
-                if (eff >= 0.75) {
-                    bm = tm;
-                    bn = tn;
-                }
-            }
+    // 8-wave LDS-DMA tiles (one workgroup per CU: 256 slots per round): chosen for long-K
+    // problems whose rounds of tiles are well filled (a square 4096^3 bf16 GEMM: 1115 TF/s
+    // on 256x256 vs 456 on the 4-wave 128x128 tile, tools/gemm_probe.py); on the detector's
+    // conv / GEMM shapes their last, partly filled round costs more than the faster main loop
+    // gains (DESIGN.md "GEMM / conv kernel"), so those keep the 4-wave tiles.  Flag 2 forces
+    // them wherever eligible.
+    int bm8 = 0, bn8 = 0;
+    if (sizeof(T) == 2 && a.A2 == nullptr && a.kchunk == 0 && a.M >= 4096 && a.N >= 128 && (!ln || a.N <= 256)) {
+        const int tn = (a.N > 128 || ln) ? 256 : 128;
+        const long t = (long)((a.M + 255) / 256) * ((a.N + tn - 1) / tn);
+        const double eff = (double)a.M * a.N / ((double)((t + 255) / 256) * 256.0 * 256.0 * tn);
+        if ((kinet_gemm_flags & 2) || (!ln && a.K >= 1024 && eff >= 0.9)) {
+            bm8 = 256;
+            bn8 = tn;
         }
     }
-    if (sizeof(T) == 2 && (kinet_gemm_flags & 256) && !ln && a.A2 == nullptr && a.kchunk == 0 && a.N >= 128 &&
-        a.M >= 4096) {
-        bm = 256;
-        bn = a.N >= 256 ? 256 : 128;
+    if (bm8) {
+        bm = bm8;
+        bn = bn8;
     }
     if (force_bm && !ln) {
         bm = force_bm;
@@ -786,15 +480,18 @@ int launch(const GemmArgs& a, hipStream_t stream) {
     // kernel on the detector's conv / GEMM shapes at batch 8 (tools/sweep_conv.py), so the
     // register path stays the default; A2 (load-time add) needs the register path anyway
     const bool dma = a.A2 == nullptr && (kinet_gemm_flags & 16);
-    // 8-wave LDS-DMA tiles (16-bit operands, no load-time A2 add, no fused LayerNorm)
+    // 8-wave LDS-DMA tiles (16-bit operands, no load-time A2 add; LayerNorm on 256-wide rows)
     if constexpr (sizeof(T) == 2) {
-        if (!ln && a.A2 == nullptr && (bm == 256 || bn == 256)) {
-            if (bm == 256 && bn == 256)
-                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 256, 2, 4, CONV, false, 2>), grid, dim3(512), 0, stream, a, nNt);
+        if (a.A2 == nullptr && (bm == 256 || bn == 256)) {
+            const dim3 blk(512);
+            if (ln)
+                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 256, 2, 4, CONV, true, 2>), grid, blk, 0, stream, a, nNt);
+            else if (bm == 256 && bn == 256)
+                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 256, 2, 4, CONV, false, 2>), grid, blk, 0, stream, a, nNt);
             else if (bm == 256)
-                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 128, 4, 2, CONV, false>), grid, dim3(512), 0, stream, a, nNt);
+                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 128, 4, 2, CONV, false>), grid, blk, 0, stream, a, nNt);
             else
-                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 128, 256, 2, 4, CONV, false>), grid, dim3(512), 0, stream, a, nNt);
+                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 128, 256, 2, 4, CONV, false>), grid, blk, 0, stream, a, nNt);
             KINET_LAUNCH_CHECK();
             return KINET_OK;
         }

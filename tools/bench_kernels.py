@@ -114,18 +114,10 @@ if __name__ == '__main__':
         from kinet_amd import _native
         _native.lib().kinet_gemm_set_flags(4)
         print('[bench_kernels] GEMM flags = 4 (no resident-weight kernel)')
-    if 'big' in which:     # allow the 512-thread 256x256-tile LDS-DMA kernel
+    if 'big' in which:     # the 8-wave LDS-DMA tiles wherever eligible
         from kinet_amd import _native
         _native.lib().kinet_gemm_set_flags(2)
-        print('[bench_kernels] GEMM flags = 2 (big-tile kernel allowed)')
-    if 'dma8' in which:    # 8-wave LDS-DMA tiles where their rounds are well filled
-        from kinet_amd import _native
-        _native.lib().kinet_gemm_set_flags(64)
-        print('[bench_kernels] GEMM flags = 64 (8-wave LDS-DMA tiles)')
-    if 'dp256' in which:   # 8-wave 256x256 / 256x128 data-parallel tiles wherever eligible
-        from kinet_amd import _native
-        _native.lib().kinet_gemm_set_flags(256)
-        print('[bench_kernels] GEMM flags = 256 (8-wave data-parallel tiles)')
+        print('[bench_kernels] GEMM flags = 2 (8-wave LDS-DMA tiles)')
     if 'gemm' in which:
         gemm()
     if 'ffn' in which:

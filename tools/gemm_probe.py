@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """GEMM / implicit-conv main-loop comparison across kernel variants (diagnostic for
-csrc/gemm.hip): the 4-wave register-staged kernel (heuristic tile), the 8-wave 256x256
-LDS-DMA kernel (flag 2), the 8-wave 256x128 / 128x256 LDS-DMA tiles (forced), on a
+csrc/gemm.hip): the default selection, the 4-wave register-staged 128x128 tile, the 8-wave
+LDS-DMA tiles wherever eligible (flag 2) and each 8-wave tile forced, on a
 square GEMM and the ResNet conv shapes at batch B (bf16).  Every variant's output is
 checked against the heuristic's.   python tools/gemm_probe.py [B]"""
 import os
@@ -20,9 +20,8 @@ def main():
     L = _native.lib()
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
     dt = torch.bfloat16
-    variants = [('reg', NO_RW, (0, 0)), ('big256', NO_RW | 2, (0, 0)), ('dma256x128', NO_RW, (256, 128)),
-                ('dma128x256', NO_RW, (128, 256)), ('dma256x256', NO_RW, (256, 256)),
-                ('streamK', NO_RW | 128, (0, 0))]
+    variants = [('default', NO_RW, (0, 0)), ('reg128', NO_RW, (128, 128)), ('8wave', NO_RW | 2, (0, 0)),
+                ('dma256x128', NO_RW, (256, 128)), ('dma128x256', NO_RW, (128, 256)), ('dma256x256', NO_RW, (256, 256))]
     cases = []
     for M, N, Kd in [(4096, 4096, 4096), (B * 22223, 256, 1024), (B * 22223, 1024, 256)]:
         x = torch.randn(M, Kd, device='cuda', dtype=dt)
