@@ -1,12 +1,14 @@
 """Hungarian matcher of the training path (src/trackformer/models/matcher.py:86-202,
 build_matcher :685-712).
 
-The cost matrix (focal or softmax class cost, L1 box cost, -GIoU) is built on the device
-where the predictions live; the linear sum assignment stays on the host
-(scipy.optimize.linear_sum_assignment, as in the reference, matcher.py:198) -- the
-north_star keeps the matcher host-side.  Track queries are forced onto the targets whose
-track ids they carry and false-positive track queries are made unmatchable exactly as
-matcher.py:177-196 does.
+The cost matrix (focal or softmax class cost, L1 box cost, -GIoU) is built batched on the
+device where the predictions live and crosses to the host in ONE copy; the linear sum
+assignment stays on the host (scipy.optimize.linear_sum_assignment, as in the reference,
+matcher.py:198) -- the north_star keeps the matcher host-side.  Track queries are forced
+onto the targets whose track ids they carry and false-positive track queries are made
+unmatchable with the same result as matcher.py:177-196, but as whole-row / whole-column
+tensor writes instead of the reference's Python loop over every query (which, with the
+masks on the GPU, synchronises once per query).
 """
 import numpy as np
 import torch
@@ -57,24 +59,24 @@ class HungarianMatcher(nn.Module):
         cost_matrix = self.cost_matrix(outputs, targets).cpu()
         sizes = [len(v["boxes"]) for v in targets]
         offsets = np.cumsum([0] + sizes[:-1])
-        for i, target in enumerate(targets):
-            if 'track_query_match_ids' not in target:
-                continue
-            # matcher.py:179-196: false-positive track queries match nothing; a true track
-            # query is forced onto its target (cost -1 there, inf elsewhere in row/column)
-            fal_pos = target['track_queries_fal_pos_mask'].cpu()
-            tq_mask = target['track_queries_mask'].cpu()
-            match_ids = target['track_query_match_ids'].cpu()
-            prop_i = 0
-            for j in range(cost_matrix.shape[1]):
-                if fal_pos[j]:
-                    cost_matrix[i, j] = np.inf
-                elif tq_mask[j]:
-                    col = int(match_ids[prop_i]) + int(offsets[i])
-                    prop_i += 1
-                    cost_matrix[i, j] = np.inf
-                    cost_matrix[i, :, col] = np.inf
-                    cost_matrix[i, j, col] = -1
+        tq = [i for i, t in enumerate(targets) if 'track_query_match_ids' in t]
+        if tq:
+            # matcher.py:177-196 without its per-query Python loop: every sample's masks and
+            # match ids come over in one copy each; a false-positive track query matches
+            # nothing (row = inf); the k-th true track query is forced onto target
+            # match_ids[k] (its row and that column inf, -1 at the pair)
+            masks = torch.stack([torch.stack([targets[i]['track_queries_fal_pos_mask'],
+                                              targets[i]['track_queries_mask']]) for i in tq]).cpu()
+            ids = [targets[i]['track_query_match_ids'] for i in tq]
+            counts = [len(m) for m in ids]
+            ids = torch.cat(ids).cpu().split(counts) if sum(counts) else [torch.zeros(0, dtype=torch.long)] * len(tq)
+            for n, i in enumerate(tq):
+                fal_pos, tq_mask = masks[n, 0], masks[n, 1]
+                rows = (tq_mask & ~fal_pos).nonzero().flatten()
+                cols = ids[n][:len(rows)].long() + int(offsets[i])
+                cost_matrix[i, fal_pos | tq_mask] = np.inf
+                cost_matrix[i, :, cols] = np.inf
+                cost_matrix[i, rows, cols] = -1
         indices = [linear_sum_assignment(c[i]) for i, c in enumerate(cost_matrix.split(sizes, -1))]
         return [(torch.as_tensor(i, dtype=torch.int64), torch.as_tensor(j, dtype=torch.int64)) for i, j in indices]
 

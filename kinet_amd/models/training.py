@@ -61,38 +61,37 @@ def add_track_queries_to_targets(model, targets, prev_indices, prev_out, add_fal
         target['track_query_match_ids'] = match.nonzero()[:, 1]
 
         if add_false_pos:
-            # random false positives next to matched detections (:97-158)
-            prev_boxes_matched = prev_out['pred_boxes'][i, prev_out_ind[target_ind_matching.to(prev_out_ind.device)]]
-            taken = set(int(v) for v in prev_out_ind.tolist())
+            # random false positives next to matched detections (:97-158); the candidate boxes
+            # come to the host once per sample (the reference re-gathers them on the device and
+            # copies the distance weights to the host once per false positive)
+            boxes_host = prev_out['pred_boxes'][i].detach().float().cpu()
+            out_ind_host = prev_out_ind.cpu()
+            prev_boxes_matched = boxes_host[out_ind_host[target_ind_matching.cpu()]]
+            taken = set(out_ind_host.tolist())
             not_prev_out_ind = [ind for ind in range(num_q_all) if ind not in taken]
             random_false_out_ind = []
             prev_target_ind_for_fps = torch.randperm(num_prev_target_ind)[:num_prev_target_ind_for_fps]
             for j in prev_target_ind_for_fps:
-                prev_boxes_unmatched = prev_out['pred_boxes'][i, not_prev_out_ind]
                 if len(prev_boxes_matched) > j:
-                    prev_box_matched = prev_boxes_matched[j]
-                    box_weights = prev_box_matched.unsqueeze(dim=0)[:, :2] - prev_boxes_unmatched[:, :2]
+                    prev_boxes_unmatched = boxes_host[not_prev_out_ind]
+                    box_weights = prev_boxes_matched[j].unsqueeze(dim=0)[:, :2] - prev_boxes_unmatched[:, :2]
                     box_weights = box_weights[:, 0] ** 2 + box_weights[:, 0] ** 2   # (sic, :128)
                     box_weights = torch.sqrt(box_weights)
-                    random_false_out_idx = not_prev_out_ind.pop(torch.multinomial(box_weights.cpu(), 1).item())
+                    random_false_out_idx = not_prev_out_ind.pop(torch.multinomial(box_weights, 1).item())
                 else:
                     random_false_out_idx = not_prev_out_ind.pop(torch.randperm(len(not_prev_out_ind))[0])
                 random_false_out_ind.append(random_false_out_idx)
-            prev_out_ind = torch.tensor(prev_out_ind.tolist() + random_false_out_ind).long()
+            prev_out_ind = torch.tensor(out_ind_host.tolist() + random_false_out_ind).long()
             target_ind_matching = torch.cat([target_ind_matching,
-                                             torch.tensor([False, ] * len(random_false_out_ind)).bool().to(device)])
+                                             torch.zeros(len(random_false_out_ind), dtype=torch.bool, device=device)])
 
         # track query masks (:174-184); queries are prepended to the object queries
-        track_queries_mask = torch.ones_like(target_ind_matching).bool()
-        track_queries_fal_pos_mask = torch.zeros_like(target_ind_matching).bool()
-        track_queries_fal_pos_mask[~target_ind_matching] = True
+        tail = torch.zeros(model.num_queries, dtype=torch.bool, device=device)
         prev_out_ind = prev_out_ind.to(device)
         target['track_query_hs_embeds'] = prev_out['hs_embed'][i, prev_out_ind]
         target['track_query_boxes'] = prev_out['pred_boxes'][i, prev_out_ind].detach()
-        target['track_queries_mask'] = torch.cat([
-            track_queries_mask, torch.tensor([False, ] * model.num_queries).to(device)]).bool()
-        target['track_queries_fal_pos_mask'] = torch.cat([
-            track_queries_fal_pos_mask, torch.tensor([False, ] * model.num_queries).to(device)]).bool()
+        target['track_queries_mask'] = torch.cat([torch.ones_like(target_ind_matching, dtype=torch.bool), tail])
+        target['track_queries_fal_pos_mask'] = torch.cat([~target_ind_matching.to(device), tail])
 
 
 def _has_dropout(model):
