@@ -120,7 +120,15 @@ def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_d
     K = x.shape[-1]
     lead = x.shape[:-1]
     x2 = x.reshape(-1, K)
-    if x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16:
+    kp = (-K) % 8
+    if kp:
+        # the GEMM's K must be 8-aligned (16-byte K chunks): zero-pad the inputs (KineT's
+        # 4 / 1 / 20 / 5 input features); the padded weight copy is cached
+        x2 = torch.nn.functional.pad(x2, (0, kp))
+        if x_add is not None:
+            x_add = torch.nn.functional.pad(x_add.reshape(-1, K), (0, kp))
+        K += kp
+    elif x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16:
         x2 = x2.contiguous()
     a2 = None
     if x_add is not None:
@@ -130,7 +138,11 @@ def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_d
             if a2.stride() != x2.stride():
                 raise RuntimeError('linear: x_add must match x layout')
     M = x2.shape[0]
-    w = weight_as(weight, x.dtype)
+    if kp:
+        w = cached(weight, ('w_padk', x.dtype, kp),
+                   lambda t: torch.nn.functional.pad(t.detach().to(x.dtype), (0, kp)).contiguous())
+    else:
+        w = weight_as(weight, x.dtype)
     Nout = w.shape[0]
     odt = out_dtype or x.dtype
     if out is None:

@@ -5,25 +5,34 @@ mirroring src/trackformer/models/__init__.py:16-71 (deformable branch).
     model, criterion, postprocessors = build_model(args)
     model.set_compute_dtype(torch.bfloat16)        # optional perf mode (default fp32)
 
-`args` is the reference's Namespace (cfgs/train.yaml + named configs).  Only the
-deformable image branch is on this path; `args.kine` / vanilla DETR / masks raise.
+`args` is the reference's Namespace (cfgs/train.yaml + named configs).  The deformable image
+branch (the hot path) and the KineT kinematic branch (`args.kine`, :72-107,
+kinet_amd/models/kinet.py) are built; vanilla DETR / masks raise.
 """
 import torch
 
 from kinet_amd.models.backbone import build_backbone
-from kinet_amd.models.deformable_detr import DeformableDETR, DeformablePostProcess
+from kinet_amd.models.deformable_detr import DeformableDETR, DeformablePostProcess, PostProcess
 from kinet_amd.models.deformable_transformer import build_deforamble_transformer
 from kinet_amd.models.detr_tracking import DeformableDETRTracking
-from kinet_amd.models.misc import NestedTensor, nested_tensor_from_tensor_list
+from kinet_amd.models.misc import NestedTensor, NestedTensorKinet, nested_tensor_from_tensor_list
 
 NUM_CLASSES = {'coco': 91, 'coco_panoptic': 250, 'coco_person': 20, 'mot': 20, 'mot_crowdhuman': 20,
-               'crowdhuman': 20, 'mot_coco_person': 20}
+               'crowdhuman': 20, 'mot_coco_person': 20, 'mot_kine': 1}
 
 
 def build_model(args):
     if args.dataset not in NUM_CLASSES:
         raise NotImplementedError(args.dataset)
     num_classes = NUM_CLASSES[args.dataset]
+    if getattr(args, 'kine', False) and not args.deformable:
+        from kinet_amd.models.criterion import build_criterion
+        from kinet_amd.models.kinet import build_kinet
+        from kinet_amd.models.matcher import build_matcher
+        matcher = build_matcher(args)
+        model = build_kinet(args, num_classes)
+        post = {'bbox': DeformablePostProcess() if args.focal_loss else PostProcess()}
+        return model, build_criterion(args, num_classes, matcher), post
     if not args.deformable:
         raise NotImplementedError('vanilla DETR (config 1) is outside the MSDeformAttn hot path')
     if getattr(args, 'masks', False):
@@ -68,5 +77,5 @@ def build_model(args):
     return model, criterion, postprocessors
 
 
-__all__ = ['build_model', 'DeformableDETR', 'DeformableDETRTracking', 'DeformablePostProcess',
-           'NestedTensor', 'nested_tensor_from_tensor_list']
+__all__ = ['build_model', 'DeformableDETR', 'DeformableDETRTracking', 'DeformablePostProcess', 'PostProcess',
+           'NestedTensor', 'NestedTensorKinet', 'nested_tensor_from_tensor_list']

@@ -2,7 +2,7 @@
 
 DEFAULTS are the keys of cfgs/train.yaml that build_model and the detector read; NAMED
 are the named configs layered on top (cfgs/train_deformable.yaml, train_multi_frame.yaml,
-train_tracking.yaml, train_mot17.yaml, train_full_res.yaml).  `load_args(*names, **kw)`
+train_tracking.yaml, train_mot17.yaml, train_full_res.yaml, train_kinet.yaml).  `load_args(*names, **kw)`
 returns the argparse.Namespace build_model expects (util/misc.py:668-674 equivalent).
 """
 from argparse import Namespace
@@ -11,7 +11,10 @@ DEFAULTS = dict(
     lr=0.0002, lr_backbone_names=['backbone.0'], lr_backbone=0.00002,
     lr_linear_proj_names=['reference_points', 'sampling_offsets'], lr_linear_proj_mult=0.1, lr_track=0.0001, batch_size=2,
     weight_decay=0.0001, epochs=50, lr_drop=40, clip_max_norm=0.1,
-    deformable=False, kine=False, with_box_refine=False, two_stage=False, freeze_detr=False,
+    deformable=False, kine=False, used_ordered_queries=False, use_empty_start=False, use_encoder_only=False,
+    use_encoding_tracklets=False, use_encoding_dets=False, encoding_dim_detections=32, encoding_dim_tracklets=32,
+    max_number_detection=60, use_class=False, ratio_add_tracklets=1.0,
+    with_box_refine=False, two_stage=False, freeze_detr=False,
     backbone='resnet50', dilation=False, position_embedding='sine', num_feature_levels=1,
     enc_layers=6, dec_layers=6, dim_feedforward=2048, hidden_dim=256, activation='relu', dropout=0.1,
     nheads=8, num_queries=100, pre_norm=False, dec_n_points=4, enc_n_points=4,
@@ -36,6 +39,12 @@ NAMED = {
                            track_query_false_positive_eos_weight=True),
     'train_mot17': dict(dataset='mot', epochs=50, lr_drop=10),
     'train_full_res': dict(img_transform={'max_size': 1920, 'val_width': 1080}),
+    # the KineT model; `tracking` comes from train_tracking as in the reference runs
+    'train_kinet': dict(dataset='mot_kine', kine=True, position_embedding='sine', multi_frame_encoding=True,
+                        track_prev_frame_range=5, use_encoding_tracklets=False, use_encoding_dets=False,
+                        encoding_dim_detections=32, encoding_dim_tracklets=8, track_query_false_negative_prob=0.2,
+                        num_queries=150, hidden_dim=288, activation='relu', batch_size=8, epochs=500, lr_drop=50,
+                        lr_linear_proj_mult=0.5, lr=0.0001, dec_layers=1, enc_layers=1),
 }
 
 # cfgs/track.yaml:28-49, the tracker thresholds as shipped

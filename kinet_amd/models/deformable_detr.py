@@ -390,3 +390,27 @@ class DeformablePostProcess(nn.Module):
                 for k, v in results[i].items():
                     results[i][k] = v[mask]
         return results
+
+
+class PostProcess(nn.Module):
+    """detr.py:891-934 (softmax classifier, the last class is no-object): used by the KineT
+    model, which trains without focal loss."""
+
+    @torch.no_grad()
+    def forward(self, outputs, target_sizes, results_mask=None):
+        out_logits, out_bbox = outputs['pred_logits'], outputs['pred_boxes']
+        assert len(out_logits) == len(target_sizes)
+        assert target_sizes.shape[1] == 2
+        prob = F.softmax(out_logits, -1)
+        scores, labels = prob[..., :-1].max(-1)
+        boxes = box_cxcywh_to_xyxy(out_bbox)
+        img_h, img_w = target_sizes.unbind(1)
+        scale_fct = torch.stack([img_w, img_h, img_w, img_h], dim=1)
+        boxes = boxes * scale_fct[:, None, :]
+        results = [{'scores': s, 'labels': l, 'boxes': b, 'scores_no_object': s_n_o}
+                   for s, l, b, s_n_o in zip(scores, labels, boxes, prob[..., -1])]
+        if results_mask is not None:
+            for i, mask in enumerate(results_mask):
+                for k, v in results[i].items():
+                    results[i][k] = v[mask]
+        return results

@@ -41,6 +41,21 @@ class NestedTensor(object):
         return tensor
 
 
+class NestedTensorKinet(object):
+    """util/misc.py:445-459: the KineT model's input -- detections and their metadata, each a
+    NestedTensor of (B, n, c) with a (B, n) padding mask."""
+
+    def __init__(self, detections, metadata, img=None):
+        self.detections = detections
+        self.metadata = metadata
+
+    def to(self, device):
+        return NestedTensorKinet(self.detections.to(device), self.metadata.to(device))
+
+    def __repr__(self):
+        return str(self.detections) + '\n ' + str(self.metadata)
+
+
 def nested_tensor_from_tensor_list(tensor_list: List[Tensor]):
     """util/misc.py:387-405: zero-pad to the max (H, W), mask True on padding."""
     if tensor_list[0].ndim != 3:

@@ -1,0 +1,135 @@
+"""KineT kinematic model (kinet_amd/models/kinet.py) against the reference
+KinetTracking (detr.py:288-425, transformer.py:85-185, backbone.py:111-216,
+detr_tracking.py:524-883), fixture tests/golden/kinet.npz from make_golden.py `kinet`:
+  * the shipped 1/1-layer config and a 2/2-layer variant (aux outputs), no tracklet queries,
+    padded batch of 2 -- f32 kinet kernels within 2e-4 of the reference (CPU fp32);
+  * K = 6 tracklet queries: the reference forward raises there (recorded in the fixture); ours
+    is pinned against the reference DualKinematicTransformer + heads run on metadata queries
+    built from query_embed_metadata (the evident intent, see kinet.py);
+  * the autograd path equals the fused inference path and back-propagates; bf16 stays within
+    stated bounds of f32."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+ATOL = 2e-4
+
+
+def _args(layers):
+    from kinet_amd.models.config import load_args
+    over = {} if layers == 1 else dict(enc_layers=2, dec_layers=2)
+    return load_args('train_kinet', tracking=True, device='cuda', **over)
+
+
+def _keys(golden_dir, name):
+    return [(ln.split()[0], [int(s) for s in ln.split()[1:]]) for ln in open(os.path.join(golden_dir, name))]
+
+
+@pytest.mark.parametrize('layers', [1, 2])
+def test_kinet_state_dict_matches_reference(golden_dir, layers):
+    from kinet_amd.models import build_model
+    model, crit, post = build_model(_args(layers))
+    ref = _keys(golden_dir, f'kinet_l{layers}.keys.txt')
+    mine = [(k, list(v.shape)) for k, v in model.state_dict().items()]
+    assert mine == ref
+    assert 'bbox' in post and crit is not None
+
+
+def test_kinet_shipped_config_builds():
+    """cfgs/train_kinet.yaml as shipped ('sine' position embedding) -- a TypeError in the
+    reference (position_encoding.py:193 vs :151) -- builds the detection embedding here."""
+    from kinet_amd.models import build_model
+    model, _, _ = build_model(_args(1))
+    assert model.backbone_det[1].max_detections == 60 and model.backbone_det[1].num_pos_feats == 144
+
+
+def _model(golden_dir, layers):
+    from weights import make_state_dict
+    from kinet_amd.models import build_model
+    model, _, _ = build_model(_args(layers))
+    keys = _keys(golden_dir, f'kinet_l{layers}.keys.txt')
+    model.load_state_dict(make_state_dict({k: s for k, s in keys}, seed=91 if layers == 1 else 92))
+    model = model.cuda()
+    model.tracking()
+    return model
+
+
+def _samples(d):
+    from kinet_amd.models import NestedTensor, NestedTensorKinet
+    mask = torch.from_numpy(d['mask']).cuda()
+    return NestedTensorKinet(NestedTensor(torch.from_numpy(d['dets']).cuda(), mask),
+                             NestedTensor(torch.from_numpy(d['meta']).cuda(), mask))
+
+
+def _close(a, b, atol=ATOL):
+    a = a.detach().float().cpu().numpy()
+    assert a.shape == b.shape, (a.shape, b.shape)
+    np.testing.assert_allclose(a, b, atol=atol, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('layers', [1, 2])
+def test_kinet_forward_matches_reference(golden_dir, layers):
+    d = np.load(os.path.join(golden_dir, 'kinet.npz'))
+    model = _model(golden_dir, layers)
+    tag = f'l{layers}'
+    with torch.no_grad():
+        out, _, features, src, hs = model(_samples(d), None)
+    _close(out['pred_logits'], d[f'{tag}_pred_logits'])
+    _close(out['pred_boxes'], d[f'{tag}_pred_boxes'])
+    _close(src, d[f'{tag}_src'])
+    _close(hs, d[f'{tag}_hs'])
+    assert len(out['aux_outputs']) == layers - 1
+    for i, aux in enumerate(out['aux_outputs']):
+        _close(aux['pred_logits'], d[f'{tag}_aux{i}_pred_logits'])
+        _close(aux['pred_boxes'], d[f'{tag}_aux{i}_pred_boxes'])
+
+
+@pytest.mark.gpu
+def test_kinet_tracklet_queries(golden_dir):
+    d = np.load(os.path.join(golden_dir, 'kinet.npz'))
+    assert bool(d['k_ref_raises'])          # the reference forward itself raises for K > 0
+    model = _model(golden_dir, 1)
+    trk_det, trk_meta = torch.from_numpy(d['k_trk_det']).cuda(), torch.from_numpy(d['k_trk_meta']).cuda()
+    targets = [{'track_query_hs_embeds_det': trk_det[b], 'track_query_hs_embeds_meta': trk_meta[b]}
+               for b in range(trk_det.shape[0])]
+    with torch.no_grad():
+        out, *_ = model(_samples(d), targets)
+    _close(out['pred_logits'], d['k_pred_logits'])
+    _close(out['pred_boxes'], d['k_pred_boxes'])
+
+
+@pytest.mark.gpu
+def test_kinet_autograd_path(golden_dir):
+    d = np.load(os.path.join(golden_dir, 'kinet.npz'))
+    model = _model(golden_dir, 2)
+    with torch.no_grad():
+        ref, *_ = model(_samples(d), None)
+    out, *_ = model(_samples(d), None)                     # grad enabled: kinet autograd Functions
+    _close(out['pred_logits'], ref['pred_logits'].cpu().numpy(), 1e-5)
+    _close(out['pred_boxes'], ref['pred_boxes'].cpu().numpy(), 1e-5)
+    loss = out['pred_logits'].square().mean() + out['pred_boxes'].sum() + out['aux_outputs'][0]['pred_boxes'].sum()
+    loss.backward()
+    grads = {n: p.grad for n, p in model.named_parameters() if p.requires_grad}
+    # unused by this graph: IntertwinedBranch.linear2 (never applied in the reference either) and
+    # the tracklet projections (no tracklet queries here)
+    used = {n: g for n, g in grads.items() if '_branch.linear2.' not in n and 'input_proj_tracklets' not in n}
+    assert all(g is not None and torch.isfinite(g).all() for g in used.values()), \
+        [n for n, g in used.items() if g is None]
+    assert grads['backbone_det.0.layers.0.linear1.weight'].abs().sum() > 0
+    assert grads['transformer.transformer_metadata.encoder.layers.0.self_attn.in_proj_weight'].abs().sum() > 0
+
+
+@pytest.mark.gpu
+def test_kinet_bf16(golden_dir):
+    d = np.load(os.path.join(golden_dir, 'kinet.npz'))
+    model = _model(golden_dir, 1)
+    with torch.no_grad():
+        ref, *_ = model(_samples(d), None)
+        model.set_compute_dtype(torch.bfloat16)
+        out, *_ = model(_samples(d), None)
+    # bf16 operands, f32 accumulation: logits / boxes stay within these max-abs bounds of f32
+    assert (out['pred_logits'] - ref['pred_logits']).abs().max().item() < 0.1
+    assert (out['pred_boxes'] - ref['pred_boxes']).abs().max().item() < 0.02
