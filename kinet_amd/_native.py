@@ -119,10 +119,15 @@ def trace_end():
     return t
 
 
+_fns = {}
+
+
 def call(name, *args, work=None):
     """Invoke a C-ABI entry point and raise RuntimeError on a non-zero status.
     `work` ({'flops': .., 'bytes': ..}) annotates the launch for the tracer."""
-    fn = getattr(lib(), name)
+    fn = _fns.get(name)
+    if fn is None:
+        fn = _fns[name] = getattr(lib(), name)
     if _trace is not None:
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
@@ -138,11 +143,25 @@ def call(name, *args, work=None):
 
 
 def ptr(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    # c_void_p argtypes take plain ints: no ctypes object per pointer argument
+    return None if t is None else t.data_ptr()
+
+
+_raw_stream = getattr(torch._C, '_cuda_getCurrentRawStream', None)
 
 
 def stream(device=None):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The current HIP stream of `device` as an int handle (the caller's stream, as
+    at::cuda::getCurrentCUDAStream() in the reference)."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        else:
+            idx = device.index if isinstance(device, torch.device) else int(device)
+            if idx is None:
+                idx = torch.cuda.current_device()
+        return _raw_stream(idx)
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 def dtype_code(dt):

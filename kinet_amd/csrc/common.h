@@ -56,6 +56,12 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
     return r;
 }
 
+// VEC elements of T as one aligned vector (16-byte loads / stores)
+template <typename T, int VEC>
+struct alignas(sizeof(T) * VEC) VecT {
+    T v[VEC];
+};
+
 template <typename T> struct Cvt;
 template <> struct Cvt<float> {
     __device__ static float from(float v) { return v; }

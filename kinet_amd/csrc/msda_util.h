@@ -6,11 +6,6 @@
 
 namespace kinet {
 
-template <typename T, int VEC>
-struct alignas(sizeof(T) * VEC) VecT {
-    T v[VEC];
-};
-
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 

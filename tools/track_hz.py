@@ -74,10 +74,31 @@ def main():
         n_tracks += len(tracker.get_results())
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    # where a frame's time goes: the detector forward alone with K ~ the mean track-query count
+    # (device-synchronised per frame), and its host enqueue time (no sync)
+    kq = max(1, int(round(sum(tq) / len(tq))))
+    tgt = [{'track_query_boxes': torch.rand(kq, 4, generator=g, device=dev) * 0.5 + 0.1,
+            'track_query_hs_embeds': torch.randn(kq, model.hidden_dim, generator=g, device=dev),
+            'image_id': torch.tensor([1], device=dev)}]
+    with torch.no_grad():
+        _, _, feats, _, _ = model(frames[0])
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(20):
+            model(frames[i % 4], tgt, feats)
+            torch.cuda.synchronize()
+        det_ms = (time.perf_counter() - t1) / 20 * 1e3
+        t1 = time.perf_counter()
+        for i in range(20):
+            model(frames[i % 4], tgt, feats)
+        host_ms = (time.perf_counter() - t1) / 20 * 1e3
+        torch.cuda.synchronize()
     print(json.dumps({'metric': 'tracking Hz (track.py:209-214), one frame per step', 'value': n_frames / el,
                       'unit': 'frames/s', 'frames': n_frames, 'seqs': a.seqs, 'seconds': el,
                       'tracks_per_seq': n_tracks / a.seqs, 'mean_track_queries': sum(tq) / len(tq),
                       'dtype': a.dtype, 'frame': [3, a.height, a.width],
+                      'detector_ms_per_frame_synced': det_ms, 'detector_host_enqueue_ms': host_ms,
+                      'tracker_ms_per_frame': el / n_frames * 1e3,
                       'config': 'config3 tracking stack (multi-frame deformable, d=288, 500 queries), '
                                 'cfgs/track.yaml tracker_cfg'}))
 
