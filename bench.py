@@ -68,6 +68,8 @@ def parse():
     ap.add_argument('--no-train', action='store_true', help='skip the config-4 training sub-benchmark')
     ap.add_argument('--train-steps', type=int, default=4)
     ap.add_argument('--cpu-seconds', type=float, default=20.0, help='bound on the CPU baseline sample')
+    ap.add_argument('--gemm-flags', type=int, default=0,
+                    help='diagnostic kernel-selection flags (kinet_gemm_set_flags, csrc/gemm.hip) for A/B runs')
     a = ap.parse_args()
     wl = WORKLOADS[a.workload]
     for k, wk in (('batch', 'batch'), ('streams', 'streams'), ('height', 'h'), ('width', 'w'), ('dtype', 'dtype')):
@@ -98,6 +100,48 @@ def build(dev, dtype, wl):
         model.tracking()
     model.set_compute_dtype(dtype)
     return model
+
+
+def roofline_split(trace, steps_traced, peak_tflops):
+    """GEMM / conv launches split at the ridge point (dense MFMA peak / HBM peak, flop per
+    byte): the compute-bound ones held against the MFMA peak, the HBM-bound ones (1x1 convs and
+    K <= 256 projections over hundreds of thousands of rows) against HBM -- plus the fused FFN
+    and the multi-tap (3x3 / 7x1) convolutions on their own, the kernels north_star's MFMA
+    target names.  Algorithmic flops / bytes per launch over HIP-event launch times."""
+    ridge = peak_tflops * 1e12 / (HBM_PEAK_GBS * 1e9)
+    acc = {k: {'launches': 0, 'ms': 0.0, 'flops': 0.0, 'bytes': 0.0} for k in ('compute', 'hbm', 'ffn', 'conv_kxk')}
+    for name, work, s, e in trace:
+        fam = work.get('family')
+        fl, by = work.get('flops', 0.0), work.get('bytes', 0.0)
+        if fam not in ('gemm', 'conv') or not fl or not by:
+            continue
+        ms = s.elapsed_time(e)
+        keys = ['compute' if fl / by >= ridge else 'hbm']
+        shape = work.get('shape', ())
+        if shape and shape[0] == 'ffn':
+            keys.append('ffn')
+        if fam == 'conv' and len(shape) >= 6 and shape[5] > 1:
+            keys.append('conv_kxk')
+        for k in keys:
+            a = acc[k]
+            a['launches'] += 1
+            a['ms'] += ms
+            a['flops'] += fl
+            a['bytes'] += by
+    out = {'ridge_flop_per_byte': ridge}
+    for k, a in acc.items():
+        if not a['launches']:
+            continue
+        t = a['ms'] * 1e-3
+        ent = {'launches_per_step': a['launches'] / steps_traced, 'ms_per_step': a['ms'] / steps_traced}
+        if k == 'hbm':
+            ent.update(achieved=a['bytes'] / t / 1e9, unit='GB/s', peak=HBM_PEAK_GBS,
+                       frac=a['bytes'] / t / 1e9 / HBM_PEAK_GBS)
+        else:
+            ent.update(achieved=a['flops'] / t / 1e12, unit='TFLOP/s', peak=peak_tflops,
+                       frac=a['flops'] / t / 1e12 / peak_tflops)
+        out[k] = ent
+    return out
 
 
 def summarize_trace(trace, steps_traced=1):
@@ -201,6 +245,8 @@ def main():
     wl = WORKLOADS[a.workload]
     from kinet_amd import _native
     from kinet_amd.models import nested_tensor_from_tensor_list
+    if a.gemm_flags:
+        _native.lib().kinet_gemm_set_flags(a.gemm_flags)
     model = build(dev, dtype, wl)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     # one independent batch per in-flight slot (distinct requests, all resident in HBM)
@@ -269,6 +315,7 @@ def main():
     trace = _native.trace_end()
     torch.cuda.synchronize()
     fam, msda = summarize_trace(trace, 3)
+    split = roofline_split(trace, 3, MFMA_PEAK_TFLOPS[a.dtype])
 
     # config-4 training step (BASELINE configs[3]): every rank runs the DDP step, gradients
     # all-reduced over RCCL -- the path whose 1 -> 8 GPU scaling north_star targets
@@ -328,6 +375,7 @@ def main():
                        'parallelism': f'replicas x{world}'},
             'roofline': roofline,
             'roofline_mfma': mfma_roof,
+            'roofline_gemm_conv_split': split,
             'msda_ms_per_call': {'encoder': msda_enc_ms, 'decoder': msda_dec_ms},
             'device_ms_per_step_by_family': {k: round(v['ms'], 4) for k, v in fam.items()},
             'cpu_baseline': cpu,

@@ -38,7 +38,8 @@ namespace {
 // diagnostic kernel-selection flags (kinet_gemm_set_flags), by value: 2 = the 8-wave LDS-DMA
 // tiles (gemm_dma.h) wherever eligible; 4 = never the resident-weight kernel (gemm_rw.hip);
 // 8 = resident-weight kernel from M >= 256; 16 = LDS-DMA staging for the 4-wave tiles;
-// 32 = never the dedicated stem convolution (stem.hip)
+// 32 = never the dedicated stem convolution (stem.hip); 64 = no full-rounds split of the
+// multi-tap convolutions
 int kinet_gemm_flags = 0;
 // diagnostic tile override for gemm_kernel (kinet_gemm_force_tile; 0 = heuristic)
 int force_bm = 0, force_bn = 0;
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
     }
     const int mt = bid / nNt, nt = bid - (bid / nNt) * nNt;
-    const int m0 = mt * BM, n0 = nt * BN;
+    const int m0 = p.m_begin + mt * BM, n0 = nt * BN;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave % WGM, wn = wave / WGM;
@@ -471,51 +472,83 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         bm = force_bm;
         bn = force_bn;
     }
-    const int nMt = (a.M + bm - 1) / bm, nNt = (a.N + bn - 1) / bn;
-    const long nblk = (long)nMt * nNt;
-    KINET_CHECK_ARG(nblk < (1L << 31), "gemm: too many tiles");
-    const int nslice = a.kchunk ? (a.K + a.kchunk - 1) / a.kchunk : 1;
-    dim3 grid((unsigned)nblk, (unsigned)nslice), block(256);
     // LDS-DMA staging (opt-in, flag 16): measured 0-10 % slower than the register-staged
     // kernel on the detector's conv / GEMM shapes at batch 8 (tools/sweep_conv.py), so the
     // register path stays the default; A2 (load-time add) needs the register path anyway
     const bool dma = a.A2 == nullptr && (kinet_gemm_flags & 16);
-    // 8-wave LDS-DMA tiles (16-bit operands, no load-time A2 add; LayerNorm on 256-wide rows)
-    if constexpr (sizeof(T) == 2) {
-        if (a.A2 == nullptr && (bm == 256 || bn == 256)) {
-            const dim3 blk(512);
-            if (ln)
-                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 256, 2, 4, CONV, true, 2>), grid, blk, 0, stream, a, nNt);
-            else if (bm == 256 && bn == 256)
-                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 256, 2, 4, CONV, false, 2>), grid, blk, 0, stream, a, nNt);
-            else if (bm == 256)
-                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 128, 4, 2, CONV, false>), grid, blk, 0, stream, a, nNt);
-            else
-                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 128, 256, 2, 4, CONV, false>), grid, blk, 0, stream, a, nNt);
-            KINET_LAUNCH_CHECK();
-            return KINET_OK;
+    const int nslice = a.kchunk ? (a.K + a.kchunk - 1) / a.kchunk : 1;
+    // one launch of the tile grid over rows [g.m_begin, g.m_begin + mtiles * BM)
+    auto run = [&](const GemmArgs& g, int tbm, int tbn, long mtiles) -> int {
+        const int nNt = (g.N + tbn - 1) / tbn;
+        const long nblk = mtiles * nNt;
+        KINET_CHECK_ARG(nblk < (1L << 31), "gemm: too many tiles");
+        dim3 grid((unsigned)nblk, (unsigned)nslice), block(256);
+        // 8-wave LDS-DMA tiles (16-bit operands, no load-time A2 add; LayerNorm on 256-wide rows)
+        if constexpr (sizeof(T) == 2) {
+            if (g.A2 == nullptr && (tbm == 256 || tbn == 256)) {
+                const dim3 blk(512);
+                if (ln)
+                    hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 256, 2, 4, CONV, true, 2>), grid, blk, 0, stream, g, nNt);
+                else if (tbm == 256 && tbn == 256)
+                    hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 256, 2, 4, CONV, false, 2>), grid, blk, 0, stream, g, nNt);
+                else if (tbm == 256)
+                    hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 256, 128, 4, 2, CONV, false>), grid, blk, 0, stream, g, nNt);
+                else
+                    hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 128, 256, 2, 4, CONV, false>), grid, blk, 0, stream, g, nNt);
+                KINET_LAUNCH_CHECK();
+                return KINET_OK;
+            }
         }
-    }
 #define L_(BM_, BN_, WM_, WN_, LN_)                                                                             \
     do {                                                                                                        \
         if (dma) hipLaunchKernelGGL((gemm_dma_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0,   \
-                                    stream, a, nNt);                                                            \
-        else hipLaunchKernelGGL((gemm_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0, stream, a, \
+                                    stream, g, nNt);                                                            \
+        else hipLaunchKernelGGL((gemm_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0, stream, g, \
                                 nNt);                                                                           \
     } while (0)
-    if (ln) {
-        if (bm == 32 && bn == 256) L_(32, 256, 1, 4, true);
-        else if (bm == 32) L_(32, 320, 1, 4, true);
-        else if (bn == 256) L_(64, 256, 1, 4, true);
-        else L_(64, 320, 1, 4, true);
-    } else if (bm == 32) L_(32, 64, 2, 2, false);
-    else if (bm == 128 && bn == 128) L_(128, 128, 2, 2, false);
-    else if (bm == 128 && bn == 64) L_(128, 64, 2, 2, false);
-    else if (bm == 64 && bn == 128) L_(64, 128, 2, 2, false);
-    else L_(64, 64, 2, 2, false);
+        if (ln) {
+            if (tbm == 32 && tbn == 256) L_(32, 256, 1, 4, true);
+            else if (tbm == 32) L_(32, 320, 1, 4, true);
+            else if (tbn == 256) L_(64, 256, 1, 4, true);
+            else L_(64, 320, 1, 4, true);
+        } else if (tbm == 32) L_(32, 64, 2, 2, false);
+        else if (tbm == 128 && tbn == 128) L_(128, 128, 2, 2, false);
+        else if (tbm == 128 && tbn == 64) L_(128, 64, 2, 2, false);
+        else if (tbm == 64 && tbn == 128) L_(64, 128, 2, 2, false);
+        else L_(64, 64, 2, 2, false);
 #undef L_
-    KINET_LAUNCH_CHECK();
-    return KINET_OK;
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    };
+    // Multi-tap convolutions (3x3, 7x1): whole rounds of one-per-CU 8-wave 256-row tiles (the
+    // faster main loop: half the LDS reads per MFMA and half the L2 bytes per flop of the
+    // 4-wave tiles), then the rows left over -- less than a round -- on the 4-wave tiles in a
+    // second launch, instead of a partly filled last round of 8-wave tiles (flag 64: off)
+    if constexpr (sizeof(T) == 2) {
+        if (CONV && !ln && a.A2 == nullptr && a.kchunk == 0 && !force_bm && !bm8 && !(kinet_gemm_flags & 64) &&
+            a.K > a.Cin && a.N >= 256 && a.M >= 8192) {
+            // (256x256 tiles only: at N = 128 the 8-wave 256x128 tile measured no faster per
+            // round than the 4-wave 128x128 one, tools/gemm_probe.py)
+            const int tn = 256;
+            const int nN8 = (a.N + tn - 1) / tn;
+            const long mt_all = (a.M + 255) / 256;
+            long mfull = (mt_all * nN8 / 256) * 256 / nN8;   // m-tiles that fill whole rounds
+            if (mfull > mt_all) mfull = mt_all;
+            // less than one round but at least half of one: a single partial round of 8-wave
+            // tiles still beats the 4-wave grid (layer-4 3x3 at batch 16: 119 vs 128 us)
+            if (mfull == 0 && mt_all * nN8 >= 128) mfull = mt_all;
+            if (mfull >= 1) {
+                int rc = run(a, 256, tn, mfull);
+                if (rc) return rc;
+                const long rem = a.M - mfull * 256;
+                if (rem <= 0) return KINET_OK;
+                GemmArgs g = a;
+                g.m_begin = (int)(mfull * 256);
+                return run(g, 64, 128, (rem + 63) / 64);   // less than a round: the smaller tile
+            }
+        }
+    }
+    return run(a, bm, bn, (a.M + bm - 1) / bm);
 }
 
 template <bool CONV>

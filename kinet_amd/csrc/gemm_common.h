@@ -33,6 +33,9 @@ struct GemmArgs {
     // tile goes to C + blockIdx.y * c_slice (no epilogue; splitk_finalize applies it)
     int kchunk;
     long c_slice;
+    // first output row of this launch's tile grid (gemm_kernel / gemm_dma_kernel): a problem
+    // split into a full-rounds launch and a remainder launch runs the same M and strides
+    int m_begin;
     int Hin, Win, Cin, Hout, Wout, KW, stride, pad;
     int stride_w, pad_w;   // horizontal stride / padding (== stride / pad for square convs)
 };

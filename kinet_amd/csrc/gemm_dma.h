@@ -69,7 +69,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN == 4 ? 2 : 1) void gemm_d
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
     }
     const int mt = bid / nNt, nt = bid - (bid / nNt) * nNt;
-    const int m0 = mt * BM, n0 = nt * BN;
+    const int m0 = p.m_begin + mt * BM, n0 = nt * BN;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -503,3 +503,28 @@ def test_ffn_fused_no_norm_and_errors(K):
     lin1b, lin2b = torch.nn.Linear(128, 1024).cuda(), torch.nn.Linear(1024, 128).cuda()
     with pytest.raises(RuntimeError, match='D must be 256 or 288'):
         K.ffn_fused(torch.randn(10, 128, device='cuda').bfloat16(), lin1b, lin2b, None)
+
+
+@pytest.mark.parametrize('B,H,W,Cin,Cout,k,s,p', [
+    (16, 50, 84, 256, 256, 3, 1, 1),    # 263 tiles of 256x256: one full round + a 4-wave remainder launch
+    (8, 50, 84, 256, 256, 3, 1, 1),     # 132 tiles: one partial round of 8-wave tiles
+    (16, 25, 42, 512, 512, 3, 1, 1),    # layer-4 3x3 (N = 2 tile columns)
+])
+def test_conv_full_rounds_split_vs_fp32(K, B, H, W, Cin, Cout, k, s, p):
+    """Multi-tap convs split into whole rounds of 8-wave 256x256 tiles + the remainder rows on
+    the 4-wave tiles (csrc/gemm.hip launch): fused BN / residual / ReLU epilogue vs fp32."""
+    g = torch.Generator().manual_seed(H * W + Cin + Cout + B)
+    x = torch.randn(B, Cin, H, W, generator=g).bfloat16()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * (2.0 / (Cin * k * k)) ** 0.5).bfloat16()
+    scale = torch.rand(Cout, generator=g) + 0.5
+    bias = torch.randn(Cout, generator=g) * 0.1
+    xc, wc = x.cuda(), w.cuda()
+    y_ref = F.conv2d(xc.float(), wc.float(), stride=s, padding=p) * scale.cuda()[None, :, None, None] \
+        + bias.cuda()[None, :, None, None]
+    res = torch.randn(y_ref.shape, generator=g).bfloat16().cuda()
+    y_ref = F.relu(y_ref + res.float())
+    wp = K.pack_conv_weight(wc, torch.bfloat16)
+    y = K.conv2d_nhwc(xc.permute(0, 2, 3, 1).contiguous(), wp, s, p, scale=scale.cuda(), bias=bias.cuda(), relu=True,
+                      residual=res.permute(0, 2, 3, 1).contiguous())
+    err = (y.permute(0, 3, 1, 2).float() - y_ref).abs()
+    assert (err <= 1e-2 * y_ref.abs() + 2e-2).all(), err.max().item()

@@ -20,7 +20,8 @@ def main():
     L = _native.lib()
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
     dt = torch.bfloat16
-    variants = [('default', NO_RW, (0, 0)), ('reg128', NO_RW, (128, 128)), ('8wave', NO_RW | 2, (0, 0)),
+    variants = [('default', NO_RW, (0, 0)), ('nosplit', NO_RW | 64, (0, 0)), ('reg128', NO_RW, (128, 128)),
+                ('8wave', NO_RW | 2, (0, 0)),
                 ('dma256x128', NO_RW, (256, 128)), ('dma128x256', NO_RW, (128, 256)), ('dma256x256', NO_RW, (256, 256))]
     cases = []
     for M, N, Kd in [(4096, 4096, 4096), (B * 22223, 256, 1024), (B * 22223, 1024, 256)]:

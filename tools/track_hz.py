@@ -31,6 +31,7 @@ def main():
     ap.add_argument('--height', type=int, default=800)
     ap.add_argument('--width', type=int, default=1333)
     ap.add_argument('--objects', type=int, default=40, help='detections above threshold on frame 0')
+    ap.add_argument('--profile', action='store_true', help='cProfile the timed loop (top functions to stderr)')
     ap.add_argument('--dtype', default='f16', choices=['bf16', 'f16', 'f32'])
     a = ap.parse_args()
     from kinet_amd.models import build_model
@@ -64,6 +65,11 @@ def main():
         tracker.step({'img': frames[i % 4], 'orig_size': size, 'dets': [torch.zeros(0, 4)]})
     torch.cuda.synchronize()
     n_frames, n_tracks, tq = 0, 0, []
+    prof = None
+    if a.profile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for s in range(a.seqs):
         tracker.reset()
@@ -74,6 +80,10 @@ def main():
         n_tracks += len(tracker.get_results())
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats('tottime').print_stats(30)
     # where a frame's time goes: the detector forward alone with K ~ the mean track-query count
     # (device-synchronised per frame), and its host enqueue time (no sync)
     kq = max(1, int(round(sum(tq) / len(tq))))
