@@ -692,7 +692,9 @@ __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
     const T* __restrict__ value, const int64_t* __restrict__ shapes,
     const TL* __restrict__ loc, const TL* __restrict__ attw, const T* __restrict__ gout,
     GA* __restrict__ gvalue, TL* __restrict__ gloc, TL* __restrict__ gattw,
-    int S, int M, int D, int L, int Lq, int P, int QT, int LPQ) {
+    int S, int M, int D, int L, int Lq, int P, int QT, int LPQ, int NA) {
+    // LPQ lanes per (query, head) group, the first NA = D / VEC of them holding channels (NA <
+    // LPQ pads a group to a power of two so the per-sample sums reduce by shuffles)
     using Acc = typename Acc<T>::type;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LevelInfo& li = *reinterpret_cast<LevelInfo*>(smem);
@@ -751,21 +753,22 @@ __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
     const bool active = qi < QT && q < Lq;
     if (active) {
         const int m = g - qi * M;
-        const int c0 = lane * VEC;
+        const bool cl = lane < NA;                     // a channel-holding lane
+        const int c0 = (cl ? lane : 0) * VEC;
         const T* vb = value + (long)b * S * MD + c0;
         const VecT<T, VEC> gv = *reinterpret_cast<const VecT<T, VEC>*>(gout + ((long)b * Lq + q) * MD + (long)m * D + c0);
         Acc gc[VEC];
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) gc[j] = to_acc(gv.v[j], (Acc*)nullptr);
-        // the grad_value scatter uses a lane-STRIDED channel map (channel j*LPQ + lane): each
-        // atomic wave-instruction then adds LPQ contiguous dwords per (query, head) group
+        for (int j = 0; j < VEC; ++j) gc[j] = cl ? to_acc(gv.v[j], (Acc*)nullptr) : (Acc)0;
+        // the grad_value scatter uses a lane-STRIDED channel map (channel j*NA + lane): each
+        // atomic wave-instruction then adds NA contiguous dwords per (query, head) group
         // instead of dwords VEC apart (1-2 64-byte atomic requests per group, not 3-4)
-        GA* gvs = gvalue + (long)b * S * MD + lane;
+        GA* gvs = gvalue + (long)b * S * MD + (cl ? lane : 0);
         Acc gs[VEC];
         {
-            const T* go = gout + ((long)b * Lq + q) * MD + (long)m * D + lane;
+            const T* go = gout + ((long)b * Lq + q) * MD + (long)m * D + (cl ? lane : 0);
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) gs[j] = to_acc(go[j * LPQ], (Acc*)nullptr);
+            for (int j = 0; j < VEC; ++j) gs[j] = cl ? to_acc(go[j * NA], (Acc*)nullptr) : (Acc)0;
         }
         const int sbase = (qi * M + m) * LP;
         for (int s = 0; s < LP; ++s) {
@@ -776,7 +779,7 @@ __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
                 Acc v[4][VEC];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    if (t.off[k] >= 0) {
+                    if (cl && t.off[k] >= 0) {
                         const VecT<T, VEC> vv = *reinterpret_cast<const VecT<T, VEC>*>(vb + t.off[k]);
 #pragma unroll
                         for (int j = 0; j < VEC; ++j) v[k][j] = to_acc(vv.v[j], (Acc*)nullptr);
@@ -798,10 +801,10 @@ __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
                 // grad_value scatter (cuh:285-304): 4 taps x VEC channels (lane-strided, see gs)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    if (t.off[k] >= 0) {
+                    if (cl && t.off[k] >= 0) {
                         const Acc wk = wt[k] * t.a;
 #pragma unroll
-                        for (int j = 0; j < VEC; ++j) atomicAdd(gvs + t.off[k] + j * LPQ, (GA)(gs[j] * wk));
+                        for (int j = 0; j < VEC; ++j) atomicAdd(gvs + t.off[k] + j * NA, (GA)(gs[j] * wk));
                     }
                 }
             }
@@ -926,15 +929,26 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
     }
     if (nval) KINET_CHECK_HIP(hipMemsetAsync(acc_buf, 0, nval * sizeof(GA), stream));
     if (N > 0 && Lq > 0) {
-        const bool pow2 = (c.lpq & (c.lpq - 1)) == 0 && c.lpq <= 64;
-        const size_t nsamp = (size_t)c.qt * M * L * P;
+        // groups padded to a power of two (reductions by shuffles instead of LDS atomics) unless
+        // flag 8 asks for the packed groups
+        int lpq = c.lpq, qt = c.qt;
+        if ((lpq & (lpq - 1)) != 0 && !(msda_flags & 8)) {
+            int p2 = 1;
+            while (p2 < lpq) p2 <<= 1;
+            if (p2 <= 64 && (kThreads / p2) / M >= 1) {
+                lpq = p2;
+                qt = (kThreads / p2) / M;
+            }
+        }
+        const bool pow2 = (lpq & (lpq - 1)) == 0 && lpq <= 64;
+        const size_t nsamp = (size_t)qt * M * L * P;
         const size_t lds = sizeof(LevelInfo) + nsamp * sizeof(BwdTap<Acc>) + (pow2 ? 0 : nsamp * 3 * sizeof(Acc));
         KINET_CHECK_ARG(lds <= 160 * 1024, "msda backward: LDS request %zu too large", lds);
-        dim3 grid((Lq + c.qt - 1) / c.qt, N);
+        dim3 grid((Lq + qt - 1) / qt, N);
 #define KB(VEC, P2)                                                                                          \
     hipLaunchKernelGGL((msda_bwd_kernel<T, TL, GA, VEC, P2>), grid, dim3(kThreads), lds, stream,            \
                        (const T*)value, shapes, (const TL*)loc, (const TL*)attw, (const T*)gout, acc_buf,   \
-                       (TL*)gloc, (TL*)gattw, S, M, D, L, Lq, P, c.qt, c.lpq)
+                       (TL*)gloc, (TL*)gattw, S, M, D, L, Lq, P, qt, lpq, c.lpq)
 #define KBV(VEC) if (pow2) { KB(VEC, 1); } else { KB(VEC, 0); }
         switch (c.vec) {
             case 1: KBV(1); break;
