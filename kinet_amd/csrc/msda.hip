@@ -687,7 +687,7 @@ struct BwdTap {
     A H, W;
 };
 
-template <typename T, typename TL, typename GA, int VEC, int POW2>
+template <typename T, typename TL, typename GA, int VEC, int POW2, int ALN>
 __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
     const T* __restrict__ value, const int64_t* __restrict__ shapes,
     const TL* __restrict__ loc, const TL* __restrict__ attw, const T* __restrict__ gout,
@@ -760,15 +760,26 @@ __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
         Acc gc[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) gc[j] = cl ? to_acc(gv.v[j], (Acc*)nullptr) : (Acc)0;
-        // the grad_value scatter uses a lane-STRIDED channel map (channel j*NA + lane): each
-        // atomic wave-instruction then adds NA contiguous dwords per (query, head) group
-        // instead of dwords VEC apart (1-2 64-byte atomic requests per group, not 3-4)
-        GA* gvs = gvalue + (long)b * S * MD + (cl ? lane : 0);
+        // grad_value scatter channel maps. Float atomics leave the chip as one 64-byte request
+        // per line a wave-instruction touches, so the map decides the request count:
+        //  - lane-STRIDED (channel j*NA + lane): each wave-instruction adds NA contiguous dwords
+        //    per (query, head) group instead of dwords VEC apart;
+        //  - ALN (16-lane groups, head rows at a fixed dword offset sh in their 64-byte line, i.e.
+        //    M*D % 16 == 0): instruction j adds the j-th line the head row touches, channel
+        //    16*j + lane - sh, so every request carries a whole line of the row (D=36: 3.25
+        //    requests per corner instead of 6)
+        const int sh = ALN ? ((m * D) & 15) : 0;
+        GA* gvs = gvalue + (long)b * S * MD + (ALN ? lane - sh : (cl ? lane : 0));
         Acc gs[VEC];
+        bool gok[VEC];
         {
-            const T* go = gout + ((long)b * Lq + q) * MD + (long)m * D + (cl ? lane : 0);
+            const T* go = gout + ((long)b * Lq + q) * MD + (long)m * D;
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) gs[j] = cl ? to_acc(go[j * NA], (Acc*)nullptr) : (Acc)0;
+            for (int j = 0; j < VEC; ++j) {
+                const int ch = ALN ? 16 * j + lane - sh : (cl ? lane : 0) + j * NA;
+                gok[j] = ALN ? (ch >= 0 && ch < D) : cl;
+                gs[j] = gok[j] ? to_acc(go[ch], (Acc*)nullptr) : (Acc)0;
+            }
         }
         const int sbase = (qi * M + m) * LP;
         for (int s = 0; s < LP; ++s) {
@@ -801,10 +812,11 @@ __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
                 // grad_value scatter (cuh:285-304): 4 taps x VEC channels (lane-strided, see gs)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    if (cl && t.off[k] >= 0) {
+                    if (t.off[k] >= 0) {
                         const Acc wk = wt[k] * t.a;
 #pragma unroll
-                        for (int j = 0; j < VEC; ++j) atomicAdd(gvs + t.off[k] + j * NA, (GA)(gs[j] * wk));
+                        for (int j = 0; j < VEC; ++j)
+                            if (gok[j]) atomicAdd(gvs + t.off[k] + j * (ALN ? 16 : NA), (GA)(gs[j] * wk));
                     }
                 }
             }
@@ -941,19 +953,25 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
             }
         }
         const bool pow2 = (lpq & (lpq - 1)) == 0 && lpq <= 64;
+        const bool aln = sizeof(GA) == 4 && lpq == 16 && c.vec == 4 && (M * D) % 16 == 0 && D <= 48 &&
+                         !(msda_flags & 16);
         const size_t nsamp = (size_t)qt * M * L * P;
         const size_t lds = sizeof(LevelInfo) + nsamp * sizeof(BwdTap<Acc>) + (pow2 ? 0 : nsamp * 3 * sizeof(Acc));
         KINET_CHECK_ARG(lds <= 160 * 1024, "msda backward: LDS request %zu too large", lds);
         dim3 grid((Lq + qt - 1) / qt, N);
-#define KB(VEC, P2)                                                                                          \
-    hipLaunchKernelGGL((msda_bwd_kernel<T, TL, GA, VEC, P2>), grid, dim3(kThreads), lds, stream,            \
+#define KB(VEC, P2, AL)                                                                                      \
+    hipLaunchKernelGGL((msda_bwd_kernel<T, TL, GA, VEC, P2, AL>), grid, dim3(kThreads), lds, stream,            \
                        (const T*)value, shapes, (const TL*)loc, (const TL*)attw, (const T*)gout, acc_buf,   \
                        (TL*)gloc, (TL*)gattw, S, M, D, L, Lq, P, qt, lpq, c.lpq)
-#define KBV(VEC) if (pow2) { KB(VEC, 1); } else { KB(VEC, 0); }
+#define KBV(VEC) if (pow2) { KB(VEC, 1, 0); } else { KB(VEC, 0, 0); }
         switch (c.vec) {
             case 1: KBV(1); break;
             case 2: KBV(2); break;
-            case 4: if (16 / sizeof(T) >= 4) { KBV(4); } break;
+            case 4:
+                if (16 / sizeof(T) >= 4) {
+                    if (aln) { KB(4, 1, 1); } else { KBV(4); }
+                }
+                break;
             case 8: if (16 / sizeof(T) >= 8) { KBV(8); } break;
         }
 #undef KBV
