@@ -24,6 +24,11 @@ enum kinet_dtype {
     KINET_BF16 = 1,
     KINET_F16 = 2,
     KINET_F64 = 3,
+    /* f32 storage, products computed as three bf16 MFMA passes (hi*hi + hi*lo + lo*hi of the
+     * split x = hi + lo; ~2^-17 relative error per product, f32 accumulation) -- torch's
+     * "high" float32 matmul precision.  Accepted as the input dtype of the GEMM / convolution
+     * entry points (kinet_gemm.h) and kinet_gemm_tn; outputs are f32. */
+    KINET_F32_X3 = 4,
 };
 
 enum kinet_status {

@@ -86,6 +86,7 @@ template <typename T> __device__ __forceinline__ float to_acc(T v, float*) { ret
 inline size_t dtype_size(int dt) {
     switch (dt) {
         case KINET_F32: return 4;
+        case KINET_F32_X3: return 4;
         case KINET_F64: return 8;
         case KINET_BF16: return 2;
         case KINET_F16: return 2;

@@ -39,8 +39,10 @@ namespace {
 // tiles (gemm_dma.h) wherever eligible; 4 = never the resident-weight kernel (gemm_rw.hip);
 // 8 = resident-weight kernel from M >= 256; 16 = LDS-DMA staging for the 4-wave tiles;
 // 32 = never the dedicated stem convolution (stem.hip); 64 = no full-rounds split of the
-// multi-tap convolutions
-int kinet_gemm_flags = 0;
+// multi-tap convolutions; 128 = KINET_F32_X3 weight-gradient GEMM splitting at fragment-read time
+}  // namespace
+int kinet_gemm_flags = 0;   // declared in gemm_common.h (read by grad.hip too)
+namespace {
 // diagnostic tile override for gemm_kernel (kinet_gemm_force_tile; 0 = heuristic)
 int force_bm = 0, force_bn = 0;
 
@@ -353,9 +355,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
         char* xl = lds + buf * STAGE;
         char* wl = xl + BM * ROWB;
 #pragma unroll
-        for (int i = 0; i < XR; ++i) *reinterpret_cast<u32x4*>(xl + swz(sr + 32 * i, sc)) = xs[i];
+        for (int i = 0; i < XR; ++i) *reinterpret_cast<u32x4*>(xl + swz(sr + 32 * i, sc)) = Mma<T>::stage(xs[i]);
 #pragma unroll
-        for (int i = 0; i < WR; ++i) *reinterpret_cast<u32x4*>(wl + swz(sr + 32 * i, sc)) = ws[i];
+        for (int i = 0; i < WR; ++i) *reinterpret_cast<u32x4*>(wl + swz(sr + 32 * i, sc)) = Mma<T>::stage(ws[i]);
     };
 
     f32x4 acc[TN][TM];
@@ -367,16 +369,38 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
     auto compute = [&](int buf) {
         const char* xl = lds + buf * STAGE;
         const char* wl = xl + BM * ROWB;
+        if constexpr (std::is_same<T, f32x3_t>::value) {
+            // KINET_F32_X3 on v_mfma_f32_16x16x32_bf16: lane group g takes chunks 2g, 2g+1
+            const int c0 = 2 * (lane >> 4);
+            u32x4 b0[TM], b1[TM], a0[TN], a1[TN];
+#pragma unroll
+            for (int t = 0; t < TM; ++t) {
+                const int r = wm * WTM + t * 16 + (lane & 15);
+                b0[t] = *reinterpret_cast<const u32x4*>(xl + swz(r, c0));
+                b1[t] = *reinterpret_cast<const u32x4*>(xl + swz(r, c0 + 1));
+            }
+#pragma unroll
+            for (int t = 0; t < TN; ++t) {
+                const int r = wn * WTN + t * 16 + (lane & 15);
+                a0[t] = *reinterpret_cast<const u32x4*>(wl + swz(r, c0));
+                a1[t] = *reinterpret_cast<const u32x4*>(wl + swz(r, c0 + 1));
+            }
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int b = 0; b < TM; ++b) Mma<f32x3_t>::run32(acc[a][b], a0[a], a1[a], b0[b], b1[b]);
+            return;
+        }
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             const int ch = kk * 4 + (lane >> 4);
-            u32x4 bfr[TM], afr[TN];
+            typename Mma<T>::Frag bfr[TM], afr[TN];
 #pragma unroll
             for (int t = 0; t < TM; ++t)
-                bfr[t] = *reinterpret_cast<const u32x4*>(xl + swz(wm * WTM + t * 16 + (lane & 15), ch));
+                bfr[t] = Mma<T>::frag(*reinterpret_cast<const u32x4*>(xl + swz(wm * WTM + t * 16 + (lane & 15), ch)));
 #pragma unroll
             for (int t = 0; t < TN; ++t)
-                afr[t] = *reinterpret_cast<const u32x4*>(wl + swz(wn * WTN + t * 16 + (lane & 15), ch));
+                afr[t] = Mma<T>::frag(*reinterpret_cast<const u32x4*>(wl + swz(wn * WTN + t * 16 + (lane & 15), ch)));
 #pragma unroll
             for (int a = 0; a < TN; ++a)
 #pragma unroll
@@ -475,7 +499,8 @@ int launch(const GemmArgs& a, hipStream_t stream) {
     // LDS-DMA staging (opt-in, flag 16): measured 0-10 % slower than the register-staged
     // kernel on the detector's conv / GEMM shapes at batch 8 (tools/sweep_conv.py), so the
     // register path stays the default; A2 (load-time add) needs the register path anyway
-    const bool dma = a.A2 == nullptr && (kinet_gemm_flags & 16);
+    // (not for KINET_F32_X3: its operands are split into bf16 hi / lo on the way into LDS)
+    const bool dma = a.A2 == nullptr && (kinet_gemm_flags & 16) && !std::is_same<T, f32x3_t>::value;
     const int nslice = a.kchunk ? (a.K + a.kchunk - 1) / a.kchunk : 1;
     // one launch of the tile grid over rows [g.m_begin, g.m_begin + mtiles * BM)
     auto run = [&](const GemmArgs& g, int tbm, int tbn, long mtiles) -> int {
@@ -501,9 +526,11 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         }
 #define L_(BM_, BN_, WM_, WN_, LN_)                                                                             \
     do {                                                                                                        \
-        if (dma) hipLaunchKernelGGL((gemm_dma_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0,   \
-                                    stream, g, nNt);                                                            \
-        else hipLaunchKernelGGL((gemm_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0, stream, g, \
+        if constexpr (!std::is_same<T, f32x3_t>::value) {                                                     \
+            if (dma) { hipLaunchKernelGGL((gemm_dma_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0, \
+                                          stream, g, nNt); break; }                                             \
+        }                                                                                                       \
+        hipLaunchKernelGGL((gemm_kernel<T, TO, BM_, BN_, WM_, WN_, CONV, LN_>), grid, block, 0, stream, g, \
                                 nNt);                                                                           \
     } while (0)
         if (ln) {
@@ -571,6 +598,8 @@ int dispatch(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t s) {
     if (in_dtype == KINET_F16 && out_dtype == KINET_F16) return launch<f16_t, f16_t, CONV>(a, s);
     if (in_dtype == KINET_F16 && out_dtype == KINET_F32) return launch<f16_t, float, CONV>(a, s);
     if (in_dtype == KINET_F32 && out_dtype == KINET_F32) return launch<float, float, CONV>(a, s);
+    if (in_dtype == KINET_F32_X3 && (out_dtype == KINET_F32 || out_dtype == KINET_F32_X3))
+        return launch<f32x3_t, float, CONV>(a, s);
     set_error("gemm: unsupported dtypes in=%d out=%d", in_dtype, out_dtype);
     return KINET_ERR_ARG;
 }
@@ -642,7 +671,7 @@ template <bool CONV>
 int run_splitk(const GemmArgs& user, int in_dtype, int out_dtype, float* ws, int ksplit, hipStream_t s) {
     KINET_CHECK_ARG(ksplit >= 1 && ws != nullptr, "split-K: need ksplit >= 1 and a workspace");
     KINET_CHECK_ARG(user.ln_g == nullptr || user.N <= 1024, "split-K: LayerNorm rows up to 1024 columns");
-    const int step = in_dtype == KINET_F32 ? 32 : 64;
+    const int step = dtype_size(in_dtype) == 4 ? 32 : 64;
     int kchunk = (user.K + ksplit - 1) / ksplit;
     kchunk = (kchunk + step - 1) / step * step;
     const int nslice = (user.K + kchunk - 1) / kchunk;

@@ -48,6 +48,7 @@ bool launch_rw_conv(const GemmArgs& a, int in_dtype, hipStream_t stream);
 // with its input rows shared through LDS; false = not that geometry
 bool launch_stem_conv(const GemmArgs& a, int dtype, hipStream_t stream);
 extern int rw_min_m;
+extern int kinet_gemm_flags;   // gemm.hip (diagnostic selection flags; 128 = the read-time-split KINET_F32_X3 TN kernel)
 
 namespace {
 
@@ -57,9 +58,15 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 
+// Fragment interface: the register-staged main loops pass every 16-byte chunk of K-contiguous
+// elements through stage() on its way into LDS, read one u32x4 per lane and operand tile back,
+// turn it into Mma<T>::Frag (frag) and feed the fragments to run().
 template <typename T> struct Mma;
 template <> struct Mma<bf16_t> {
     static constexpr int EPC = 8;
+    typedef u32x4 Frag;
+    __device__ __forceinline__ static Frag frag(const u32x4& x) { return x; }
+    __device__ __forceinline__ static u32x4 stage(const u32x4& x) { return x; }
     __device__ __forceinline__ static void run(f32x4& c, const u32x4& a, const u32x4& b) {
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
     }
@@ -76,6 +83,9 @@ template <> struct Mma<bf16_t> {
 };
 template <> struct Mma<f16_t> {
     static constexpr int EPC = 8;
+    typedef u32x4 Frag;
+    __device__ __forceinline__ static Frag frag(const u32x4& x) { return x; }
+    __device__ __forceinline__ static u32x4 stage(const u32x4& x) { return x; }
     __device__ __forceinline__ static void run(f32x4& c, const u32x4& a, const u32x4& b) {
         c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
     }
@@ -85,6 +95,9 @@ template <> struct Mma<f16_t> {
 };
 template <> struct Mma<float> {
     static constexpr int EPC = 4;
+    typedef u32x4 Frag;
+    __device__ __forceinline__ static Frag frag(const u32x4& x) { return x; }
+    __device__ __forceinline__ static u32x4 stage(const u32x4& x) { return x; }
     // lanes hold 4 consecutive k of a 16-wide k block; MFMA j sums k = 4*(lane>>4) + j over
     // the 4 lane groups, so the 4 MFMAs together cover the block exactly once.
     __device__ __forceinline__ static void run(f32x4& c, const u32x4& a, const u32x4& b) {
@@ -94,6 +107,54 @@ template <> struct Mma<float> {
     }
     __device__ __forceinline__ static u32x4 add(const u32x4& x, const u32x4& y) {
         return __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, x) + __builtin_bit_cast(f32x4, y));
+    }
+};
+
+// f32 operands multiplied as three bf16 MFMA passes (KINET_F32_X3; torch's "high" float32
+// matmul precision): x = hi + lo with hi = bf16(x) (round to nearest even) and lo =
+// bf16(x - hi), a*b ~= hi_a*hi_b + hi_a*lo_b + lo_a*hi_b in f32 accumulation.  The dropped
+// lo_a*lo_b term and the rounding of lo leave ~2^-17 relative error per product (exact f32
+// MFMA: 2^-24; TF32: 2^-11) at 3 x 8 MFMA cycles per 16x16x16 block instead of 4 x 32 for
+// v_mfma_f32_16x16x4_f32.  Same K layout as Mma<float> (4 consecutive k per lane = the
+// A/B operand map of v_mfma_f32_16x16x16_bf16).
+struct f32x3_t { float v; };
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+struct X3Frag { s16x4 hi, lo; };
+__device__ __forceinline__ X3Frag split_x3(const f32x4& x) {
+    const bf16x4v h = __builtin_convertvector(x, bf16x4v);
+    const f32x4 r = x - __builtin_convertvector(h, f32x4);
+    return X3Frag{__builtin_bit_cast(s16x4, h), __builtin_bit_cast(s16x4, __builtin_convertvector(r, bf16x4v))};
+}
+template <> struct Mma<f32x3_t> {
+    static constexpr int EPC = 4;
+    typedef X3Frag Frag;
+    // split once per element on the way into LDS (not once per wave that reads it): the chunk
+    // of 4 f32 becomes {hi of the 4 (8 bytes), lo of the 4 (8 bytes)} in the same 16 bytes
+    __device__ __forceinline__ static u32x4 stage(const u32x4& x) {
+        const X3Frag f = split_x3(__builtin_bit_cast(f32x4, x));
+        const uint2 h = __builtin_bit_cast(uint2, f.hi), l = __builtin_bit_cast(uint2, f.lo);
+        return u32x4{h.x, h.y, l.x, l.y};
+    }
+    __device__ __forceinline__ static Frag frag(const u32x4& x) {
+        return X3Frag{__builtin_bit_cast(s16x4, uint2{x[0], x[1]}), __builtin_bit_cast(s16x4, uint2{x[2], x[3]})};
+    }
+    __device__ __forceinline__ static void run(f32x4& c, const Frag& a, const Frag& b) {
+        c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a.lo, b.hi, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a.hi, b.lo, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a.hi, b.hi, c, 0, 0, 0);
+    }
+    __device__ __forceinline__ static u32x4 add(const u32x4& x, const u32x4& y) { return Mma<float>::add(x, y); }
+    // the 16x16x32 form: a lane's 8 consecutive k = two staged chunks {hi4, lo4}
+    __device__ __forceinline__ static void run32(f32x4& c, const u32x4& a0, const u32x4& a1, const u32x4& b0,
+                                                 const u32x4& b1) {
+        const bf16x8 ah = __builtin_bit_cast(bf16x8, u32x4{a0[0], a0[1], a1[0], a1[1]});
+        const bf16x8 al = __builtin_bit_cast(bf16x8, u32x4{a0[2], a0[3], a1[2], a1[3]});
+        const bf16x8 bh = __builtin_bit_cast(bf16x8, u32x4{b0[0], b0[1], b1[0], b1[1]});
+        const bf16x8 bl = __builtin_bit_cast(bf16x8, u32x4{b0[2], b0[3], b1[2], b1[3]});
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
     }
 };
 

@@ -179,13 +179,13 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN == 4 ? 2 : 1) void gemm_d
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             const int ch = kk * 4 + (lane >> 4);
-            u32x4 bfr[TM], afr[TN];
+            typename Mma<T>::Frag bfr[TM], afr[TN];
 #pragma unroll
             for (int t = 0; t < TM; ++t)
-                bfr[t] = *reinterpret_cast<const u32x4*>(xl + swz(wm * WTM + t * 16 + (lane & 15), ch));
+                bfr[t] = Mma<T>::frag(*reinterpret_cast<const u32x4*>(xl + swz(wm * WTM + t * 16 + (lane & 15), ch)));
 #pragma unroll
             for (int t = 0; t < TN; ++t)
-                afr[t] = *reinterpret_cast<const u32x4*>(wl + swz(wn * WTN + t * 16 + (lane & 15), ch));
+                afr[t] = Mma<T>::frag(*reinterpret_cast<const u32x4*>(wl + swz(wn * WTN + t * 16 + (lane & 15), ch)));
 #pragma unroll
             for (int a = 0; a < TN; ++a)
 #pragma unroll

@@ -23,6 +23,7 @@
 
 #include "../../include/kinet_grad.h"
 #include "common.h"
+#include "gemm_common.h"   // split_x3 / Mma<f32x3_t> (KINET_F32_X3)
 
 namespace kinet {
 namespace {
@@ -143,7 +144,7 @@ __device__ __forceinline__ void tn_load4<float>(const float* p, int valid, float
     }
 }
 
-template <typename T>
+template <typename T, bool X3>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                       float* __restrict__ C, int M, int N, int K, long lda,
                                                       long ldb, long ldc, int kc, long slice) {
@@ -176,18 +177,39 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const T* __restrict__ A, c
         for (int k0 = k_begin; k0 < k_end; k0 += TN_BK) {
             const bool more = k0 + TN_BK < k_end;
             if (more) load(k0 + TN_BK);
+            if constexpr (X3) {
+                // KINET_F32_X3: lane group g holds k = 4g..4g+3 of the 16-deep step (the operand
+                // map of v_mfma_f32_16x16x16_bf16), split once into bf16 hi + lo, 3 MFMAs a tile
+                const int kr = 4 * (lane >> 4);
+                X3Frag a[2], b[2];
 #pragma unroll
-            for (int kk = 0; kk < TN_BK; kk += 4) {
-                const int kr = kk + (lane >> 4);
-                float a[2], b[2];
+                for (int i = 0; i < 2; ++i) {
+                    const int c = wm + i * 16 + (lane & 15);
+                    a[i] = split_x3(tn_f32x4{As[buf][kr][c], As[buf][kr + 1][c], As[buf][kr + 2][c], As[buf][kr + 3][c]});
+                }
 #pragma unroll
-                for (int i = 0; i < 2; ++i) a[i] = As[buf][kr][wm + i * 16 + (lane & 15)];
-#pragma unroll
-                for (int j = 0; j < 2; ++j) b[j] = Bs[buf][kr][wn + j * 16 + (lane & 15)];
+                for (int j = 0; j < 2; ++j) {
+                    const int c = wn + j * 16 + (lane & 15);
+                    b[j] = split_x3(tn_f32x4{Bs[buf][kr][c], Bs[buf][kr + 1][c], Bs[buf][kr + 2][c], Bs[buf][kr + 3][c]});
+                }
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < 2; ++j) Mma<f32x3_t>::run(acc[i][j], a[i], b[j]);
+            } else {
+#pragma unroll
+                for (int kk = 0; kk < TN_BK; kk += 4) {
+                    const int kr = kk + (lane >> 4);
+                    float a[2], b[2];
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) a[i] = As[buf][kr][wm + i * 16 + (lane & 15)];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) b[j] = Bs[buf][kr][wn + j * 16 + (lane & 15)];
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+                }
             }
             if (more) {
                 stash(buf ^ 1);
@@ -197,6 +219,127 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const T* __restrict__ A, c
         }
     }
     // C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm + i * 16 + (lane >> 4) * 4 + r, n = n0 + wn + j * 16 + (lane & 15);
+                if (m < M && n < N) Cz[(long)m * ldc + n] = acc[i][j][r];
+            }
+}
+
+// KINET_F32_X3 TN GEMM: the same 64 x 64 tile and split-K contract as gemm_tn_kernel, K-steps of
+// 32, f32 operands split into bf16 hi / lo ONCE on the way into LDS.  Loader: thread t of each
+// 128-thread half (A, then B) reads a 4 (k) x 4 (m) block -- 4 coalesced float4 rows -- transposes
+// it in registers and writes per m one 16-byte chunk {hi of k0..k0+3, lo of k0..k0+3} at LDS
+// (m, k-quad), XOR-swizzled like the main GEMM's tiles; lane (r, g) of a 16x16x16 fragment reads
+// exactly that chunk (ds_read_b128).  3 MFMAs per 16x16x16 block (Mma<f32x3_t>).
+constexpr int TX_BK = 32;
+__global__ __launch_bounds__(256) void gemm_tn_x3_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                         float* __restrict__ C, int M, int N, int K, long lda,
+                                                         long ldb, long ldc, int kc, long slice, int vec4,
+                                                         int tiles_m, int tiles, int ks) {
+    constexpr int TILE = TN_BM * TX_BK * 4;    // bytes of one operand's LDS image (64 rows x 128 B)
+    __shared__ __attribute__((aligned(16))) char lds[2][2][TILE];
+    // XCD-aware K-slice placement: block b runs on XCD b % 8.  With ks a multiple of 8 every
+    // K-slice's tiles go to ONE XCD, so the slice's rows of A and B are fetched into that XCD's
+    // L2 once and shared by all its tiles (which walk K together), instead of every XCD
+    // re-reading every slice (measured: the 64 x 64 tiles were Infinity-Cache-bandwidth bound)
+    const int b = blockIdx.x;
+    int z, tile;
+    if ((ks & 7) == 0) {   // (an odd ks from the launcher disables the placement)
+        const int j = b >> 3;
+        z = (b & 7) + 8 * (j / tiles);
+        tile = j - (j / tiles) * tiles;
+    } else {
+        z = b / tiles;
+        tile = b - z * tiles;
+    }
+    const int m0 = (tile % tiles_m) * TN_BM, n0 = (tile / tiles_m) * TN_BN;
+    const int k_begin = z * kc, k_end = min(K, k_begin + kc);
+    float* Cz = C + (long)z * slice;
+    const int t = threadIdx.x;
+    const int op = t >> 7;                            // 0: A, 1: B
+    const int mq = t & 15, kq = (t >> 4) & 7;         // m-quad (4 columns), k-quad (4 rows)
+    const float* src = op ? B : A;
+    const long ld = op ? ldb : lda;
+    const int c0 = (op ? n0 : m0) + mq * 4;
+    const int lim = op ? N : M;
+    const int cvalid = max(0, min(4, lim - c0));
+    const int wave = t >> 6, lane = t & 63;
+    const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
+    tn_f32x4 acc[2][2] = {};
+    // branch-free staging loads (a conditional load costs a vmcnt(0) drain per branch): buffer
+    // loads whose K-tail rows get an offset past num_records (the range check returns zeros);
+    // columns past M / N read whatever follows -- they only reach output rows / columns that
+    // are never stored
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)min((long)K * ld * 4, (long)INT_MAX), 0x00020000);
+    const unsigned cbad = c0 < lim ? 0u : 0x80000000u;
+    (void)vec4;
+    auto load = [&](int k0, u32x4 (&v)[4]) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int k = k0 + kq * 4 + r;
+            const unsigned off = (unsigned)(((long)k * ld + c0) * 4) | (k < k_end ? cbad : 0x80000000u);
+            v[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        }
+    };
+    auto stash = [&](int buf, const u32x4 (&v)[4]) {
+        char* L = lds[buf][op];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = mq * 4 + i;
+            *reinterpret_cast<u32x4*>(L + swz(m, kq)) = Mma<f32x3_t>::stage(u32x4{v[0][i], v[1][i], v[2][i], v[3][i]});
+        }
+    };
+    auto compute = [&](int buf) {
+        // v_mfma_f32_16x16x32_bf16: lane group g takes the k-quads 2g, 2g+1
+        const char* La = lds[buf][0];
+        const char* Lb = lds[buf][1];
+        const int q0 = 2 * (lane >> 4);
+        u32x4 a0[2], a1[2], b0[2], b1[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int r = wm + i * 16 + (lane & 15);
+            a0[i] = *reinterpret_cast<const u32x4*>(La + swz(r, q0));
+            a1[i] = *reinterpret_cast<const u32x4*>(La + swz(r, q0 + 1));
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = wn + j * 16 + (lane & 15);
+            b0[j] = *reinterpret_cast<const u32x4*>(Lb + swz(r, q0));
+            b1[j] = *reinterpret_cast<const u32x4*>(Lb + swz(r, q0 + 1));
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) Mma<f32x3_t>::run32(acc[i][j], a0[i], a1[i], b0[j], b1[j]);
+    };
+    // two register staging sets, loads issued two K-steps ahead (as gemm.hip's main loop):
+    // step kt loads kt+2 into the set that held kt, computes kt, stashes kt+1, one barrier;
+    // steps past the end load zeros (range check) and multiply them
+    const int nk = (k_end - k_begin + TX_BK - 1) / TX_BK;
+    if (nk > 0) {
+        u32x4 v0[4], v1[4];
+        load(k_begin, v0);
+        load(k_begin + TX_BK, v1);
+        stash(0, v0);
+        __syncthreads();
+        for (int kt = 0; kt < nk; kt += 2) {
+            load(k_begin + (kt + 2) * TX_BK, v0);
+            compute(0);
+            stash(1, v1);
+            __syncthreads();
+            if (kt + 1 >= nk) break;
+            load(k_begin + (kt + 3) * TX_BK, v1);
+            compute(1);
+            stash(0, v0);
+            __syncthreads();
+        }
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -638,6 +781,7 @@ extern "C" int64_t kinet_gemm_tn_workspace(int M, int N, int K) {
     if (tiles <= 0 || K <= 0) return 0;
     int ks = (int)std::min<long long>(64, std::max<long long>(1, 1024 / tiles));
     ks = std::min(ks, std::max(1, K / 64));
+    if (ks >= 8) ks = std::min(64, (ks + 7) & ~7);   // whole K-slices per XCD (gemm_tn_x3_kernel)
     return ks > 1 ? (int64_t)ks * M * N : 0;
 }
 
@@ -665,13 +809,23 @@ extern "C" int kinet_gemm_tn(const void* A, const void* B, float* C, int M, int 
     }
     dim3 grid((M + TN_BM - 1) / TN_BM, (N + TN_BN - 1) / TN_BN, ks);
     if (dtype == KINET_F32)
-        hipLaunchKernelGGL(gemm_tn_kernel<float>, grid, dim3(256), 0, s, (const float*)A, (const float*)B, out, M, N, K,
+        hipLaunchKernelGGL((gemm_tn_kernel<float, false>), grid, dim3(256), 0, s, (const float*)A, (const float*)B, out, M, N, K,
+                           (long)lda, (long)ldb, ldo, kc, slice);
+    else if (dtype == KINET_F32_X3 && !(kinet_gemm_flags & 128) &&
+             ((long long)K + 2 * TX_BK) * std::max(lda, ldb) * 4 < (1LL << 31)) {   // 31-bit buffer offsets
+        const int vec4 = (lda % 4 == 0) && (ldb % 4 == 0) && ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0);
+        const int tm = (M + TN_BM - 1) / TN_BM, tiles = tm * ((N + TN_BN - 1) / TN_BN);
+        hipLaunchKernelGGL(gemm_tn_x3_kernel, dim3((unsigned)(tiles * ks)), dim3(256), 0, s, (const float*)A,
+                           (const float*)B, out, M, N, K, (long)lda, (long)ldb, ldo, kc, slice, vec4, tm, tiles,
+                           (kinet_gemm_flags & 256) ? ks | 1 : ks);   // flag 256: no XCD placement
+    } else if (dtype == KINET_F32_X3)   // flag 128: split at fragment-read time (the 16-deep kernel)
+        hipLaunchKernelGGL((gemm_tn_kernel<float, true>), grid, dim3(256), 0, s, (const float*)A, (const float*)B, out, M, N, K,
                            (long)lda, (long)ldb, ldo, kc, slice);
     else if (dtype == KINET_BF16)
-        hipLaunchKernelGGL(gemm_tn_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)A, (const bf16_t*)B, out, M, N,
+        hipLaunchKernelGGL((gemm_tn_kernel<bf16_t, false>), grid, dim3(256), 0, s, (const bf16_t*)A, (const bf16_t*)B, out, M, N,
                            K, (long)lda, (long)ldb, ldo, kc, slice);
     else if (dtype == KINET_F16)
-        hipLaunchKernelGGL(gemm_tn_kernel<f16_t>, grid, dim3(256), 0, s, (const f16_t*)A, (const f16_t*)B, out, M, N,
+        hipLaunchKernelGGL((gemm_tn_kernel<f16_t, false>), grid, dim3(256), 0, s, (const f16_t*)A, (const f16_t*)B, out, M, N,
                            K, (long)lda, (long)ldb, ldo, kc, slice);
     else {
         set_error("gemm_tn: unsupported dtype %d", dtype);

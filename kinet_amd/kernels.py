@@ -111,6 +111,19 @@ def ksplit_for(M, N, K, ln=False):
     return ks if ks >= 2 else 1
 
 
+KINET_F32_X3 = 4   # include/kinet_common.h
+
+
+def mm_code(dt):
+    """Input dtype code of a GEMM / convolution: f32 operands follow
+    torch.get_float32_matmul_precision() -- 'highest' (torch's default): exact f32 MFMA;
+    'high' / 'medium': three bf16 MFMA passes per product (KINET_F32_X3, ~2^-17 relative
+    error per product; torch's own 'high' mode is this same bf16x3 split or TF32)."""
+    if dt == torch.float32 and torch.get_float32_matmul_precision() != 'highest':
+        return KINET_F32_X3
+    return N.dtype_code(dt)
+
+
 def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_dtype=None,
            scale=None, out=None, x_add=None, ln=None):
     """y = LN?(relu?((x [+ x_add]) @ W^T * scale + bias + residual)); rows with row_mask -> 0.
@@ -170,12 +183,12 @@ def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_d
     if ks > 1:
         ws = torch.empty(ks * M * Nout, dtype=torch.float32, device=x.device)
         N.call('kinet_gemm_splitk', N.ptr(x2), N.ptr(w), N.ptr(out), M, Nout, K, x2.stride(0), K, ldc,
-               N.dtype_code(x.dtype), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(r), ldr, int(relu),
+               mm_code(x.dtype), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(r), ldr, int(relu),
                N.ptr(g), N.ptr(b), eps, N.dtype_code(odt), N.ptr(mask), N.ptr(ws), ks, N.stream(x.device),
                work=work)
         return out.view(*lead, Nout) if out.is_contiguous() else out
     N.call('kinet_gemm_ex', N.ptr(x2), N.ptr(a2), N.ptr(w), N.ptr(out), M, Nout, K, x2.stride(0), K, ldc,
-           N.dtype_code(x.dtype), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(r), ldr, int(relu),
+           mm_code(x.dtype), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(r), ldr, int(relu),
            N.ptr(g), N.ptr(b), eps, N.dtype_code(odt), N.ptr(mask), N.stream(x.device), work=work)
     return out.view(*lead, Nout) if out.is_contiguous() else out
 
@@ -290,7 +303,7 @@ def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, res
     work = {'family': 'conv', 'flops': 2.0 * B * Ho * Wo * Cout * KH * KW * Cin,
             'shape': (B, H, W, Cin, Cout, KH, sh),
             'bytes': (B * H * W * Cin + Cout * KH * KW * Cin + B * Ho * Wo * Cout * (2 if r is not None else 1)) * e}
-    tail = (N.dtype_code(x.dtype), N.ptr(scale), N.ptr(bias), N.ptr(r), Cout if r is not None else 0, int(relu), ldy)
+    tail = (mm_code(x.dtype), N.ptr(scale), N.ptr(bias), N.ptr(r), Cout if r is not None else 0, int(relu), ldy)
     if sh != sw or ph != pw:
         if ksplit not in (None, 1):
             raise RuntimeError('conv2d: split-K needs equal strides / pads')
@@ -597,7 +610,7 @@ def gemm_tn(a, b, out=None, accumulate=False):
         nws = max(nws, M * Nn)
     ws = torch.empty(max(1, nws), dtype=torch.float32, device=a.device) if nws else None
     N.call('kinet_gemm_tn', N.ptr(a), N.ptr(b), N.ptr(out), M, Nn, K_, a.stride(0), b.stride(0), out.stride(0),
-           N.dtype_code(a.dtype), int(accumulate), N.ptr(ws), N.stream(a.device),
+           mm_code(a.dtype), int(accumulate), N.ptr(ws), N.stream(a.device),
            work={'family': 'gemm', 'flops': 2.0 * M * Nn * K_, 'shape': ('tn', M, Nn, K_)})
     return out
 

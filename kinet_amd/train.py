@@ -118,14 +118,26 @@ def setup_ddp(model, device):
 
 
 def benchmark_train(steps=5, warmup=2, batch=2, height=800, width=1333, prev_dtype=torch.bfloat16, device=None,
-                    dropout=None):
+                    dropout=None, matmul_precision='high'):
     """Config-4 training throughput (BASELINE.json configs[3], cfgs/train_mot17.yaml: `mot17
     deformable multi_frame tracking`, d=288, 500 queries, two-pass track-query training,
     focal + L1 + GIoU with aux losses, AdamW, clip 0.1) on synthetic (current, prev) frame
     pairs; DDP over the initialised process group when there is one.  Returns a dict with
     frames/s (current frames of the whole job), images/s (= 2x) and s/step; the timed region
     is bracketed by a barrier + device synchronisation and the elapsed time is the max over
-    ranks."""
+    ranks.  matmul_precision: torch.set_float32_matmul_precision for the run -- 'high' runs
+    the f32 grad frame's GEMMs / convs / weight gradients as three bf16 MFMA passes
+    (KINET_F32_X3, ~2^-17 relative error per product; the reference's own cuDNN convs run
+    TF32, 2^-11, by default), 'highest' on the exact f32 MFMA."""
+    prev_prec = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(matmul_precision)
+    try:
+        return _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dropout, matmul_precision)
+    finally:
+        torch.set_float32_matmul_precision(prev_prec)
+
+
+def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dropout, matmul_precision):
     import time
     from kinet_amd.models import build_model
     from kinet_amd.models.config import load_args
@@ -174,4 +186,6 @@ def benchmark_train(steps=5, warmup=2, batch=2, height=800, width=1333, prev_dty
                                    'fwd+bwd, AdamW)', 'batch_per_gpu': batch, 'hidden_dim': args.hidden_dim,
                        'num_queries': args.num_queries, 'dropout': args.dropout,
                        'prev_frame_dtype': str(prev_dtype).replace('torch.', ''),
-                       'grad_frame_dtype': 'f32', 'parallelism': f'ddp{world} (RCCL all-reduce)'}}
+                       'grad_frame_dtype': 'f32', 'f32_matmul_precision': matmul_precision +
+                       (' (bf16x3 MFMA products)' if matmul_precision != 'highest' else ' (exact f32 MFMA)'),
+                       'parallelism': f'ddp{world} (RCCL all-reduce)'}}

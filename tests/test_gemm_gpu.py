@@ -528,3 +528,65 @@ def test_conv_full_rounds_split_vs_fp32(K, B, H, W, Cin, Cout, k, s, p):
                       residual=res.permute(0, 2, 3, 1).contiguous())
     err = (y.permute(0, 3, 1, 2).float() - y_ref).abs()
     assert (err <= 1e-2 * y_ref.abs() + 2e-2).all(), err.max().item()
+
+
+# ---- KINET_F32_X3: f32 operands as three bf16 MFMA passes (torch float32_matmul_precision 'high')
+@pytest.fixture
+def x3_precision():
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision('high')
+    yield
+    torch.set_float32_matmul_precision(prev)
+
+
+def _x3_bound(a64, b64):
+    # per-product error <= ~2^-16 |a||b| (hi/lo split of both operands, lo*lo dropped), plus
+    # f32 accumulation: bound by 4e-5 * (|A| @ |B|) elementwise
+    return 4e-5 * (a64.abs() @ b64.abs()) + 1e-6
+
+
+@pytest.mark.parametrize('M,N,Kd', [(37, 91, 256), (1000, 1024, 256), (513, 256, 1024), (4200, 384, 2048)])
+def test_linear_f32_x3_vs_f64(K, x3_precision, M, N, Kd):
+    g = torch.Generator().manual_seed(M + N + Kd)
+    x = torch.randn(M, Kd, generator=g, dtype=torch.float64)
+    w = torch.randn(N, Kd, generator=g, dtype=torch.float64) / Kd ** 0.5
+    ref = x @ w.T
+    y = K.linear(x.float().cuda(), w.float().cuda())
+    torch.cuda.synchronize()
+    err = (y.double().cpu() - ref).abs()
+    # f32 rounding of the operands themselves is part of the bound (2^-24 each)
+    assert (err <= _x3_bound(x, w.T) + 2e-7 * (x.abs() @ w.abs().T)).all(), err.max().item()
+    # and it is not the exact-f32 path: that one is ~100x tighter
+    torch.set_float32_matmul_precision('highest')
+    y2 = K.linear(x.float().cuda(), w.float().cuda())
+    torch.set_float32_matmul_precision('high')
+    torch.cuda.synchronize()
+    assert (y2.double().cpu() - ref).abs().max() < err.max() or err.max() == 0
+
+
+@pytest.mark.parametrize('ks', [1, 3])
+def test_conv_f32_x3_vs_f64(K, x3_precision, ks):
+    g = torch.Generator().manual_seed(5 + ks)
+    B, H, W, Cin, Cout = 2, 23, 31, 64, 128
+    x = torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / (9 * Cin) ** 0.5
+    ref = F.conv2d(x, w, padding=1)
+    bound = 4e-5 * F.conv2d(x.abs(), w.abs(), padding=1) + 1e-6
+    xn = x.float().permute(0, 2, 3, 1).contiguous().cuda()
+    wp = w.float().permute(0, 2, 3, 1).contiguous().cuda()
+    y = K.conv2d_nhwc(xn, wp, 1, 1, ksplit=ks)
+    torch.cuda.synchronize()
+    err = (y.double().cpu().permute(0, 3, 1, 2) - ref).abs()
+    assert (err <= bound).all(), err.max().item()
+
+
+@pytest.mark.parametrize('Kd,M,N', [(40000, 256, 288), (999, 70, 33)])
+def test_gemm_tn_f32_x3_vs_f64(K, x3_precision, Kd, M, N):
+    g = torch.Generator().manual_seed(Kd)
+    a = torch.randn(Kd, M, generator=g, dtype=torch.float64)
+    b = torch.randn(Kd, N, generator=g, dtype=torch.float64)
+    ref = a.T @ b
+    y = K.gemm_tn(a.float().cuda(), b.float().cuda())
+    torch.cuda.synchronize()
+    err = (y.double().cpu() - ref).abs()
+    assert (err <= _x3_bound(a.T, b)).all(), err.max().item()

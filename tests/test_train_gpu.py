@@ -40,7 +40,17 @@ def _batch(d):
     return imgs, targets
 
 
-def test_train_step_matches_reference(golden_dir):
+@pytest.fixture(params=['highest', 'high'])
+def matmul_precision(request):
+    # 'high': every f32 GEMM / conv / weight-gradient GEMM as three bf16 MFMA passes
+    # (KINET_F32_X3) -- the training benchmark's setting; same tolerances as exact f32
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(request.param)
+    yield request.param
+    torch.set_float32_matmul_precision(prev)
+
+
+def test_train_step_matches_reference(golden_dir, matmul_precision):
     from kinet_amd.models import nested_tensor_from_tensor_list
     from kinet_amd.train import weighted_loss
     d = np.load(os.path.join(golden_dir, 'train_step_small.npz'))
@@ -62,6 +72,7 @@ def test_train_step_matches_reference(golden_dir):
     np.testing.assert_allclose(total.item(), float(d['loss_total']), rtol=1e-3)
     total.backward()
     params = dict(model.named_parameters(remove_duplicate=False))
+    bad = []
     for k in d.files:
         if not k.startswith('grad:'):
             continue
@@ -69,13 +80,20 @@ def test_train_step_matches_reference(golden_dir):
         assert g is not None, k
         ref = torch.from_numpy(d[k])
         err = (g.cpu() - ref).abs().max().item()
-        print(f'[grad] {k}: max err {err:.3e} rel {err / (ref.abs().max().item() + 1e-12):.3e}')
+        print(f'[grad] {matmul_precision} {k}: max err {err:.3e} rel {err / (ref.abs().max().item() + 1e-12):.3e}')
         # gradients below the encoder pass the MSDA location derivative, which is one-sided at
         # integer pixel coordinates (a 1-ulp location difference can flip it), and then ~10
         # conv layers: the backbone's deepest trainable weight lands at ~2e-3 of its scale
         # (heads / decoder: ~1e-7 .. 1e-6; encoder / input_proj: ~1.5e-4; measured on MI355X)
         rel = 5e-3 if 'backbone' in k else 2e-3
-        assert err <= rel * ref.abs().max().item() + 1e-5, (k, err, ref.abs().max().item())
+        if matmul_precision != 'highest' and ('backbone' in k or 'sampling_offsets' in k):
+            # bf16x3 products move the forward by ~1e-5 relative, enough to carry a few sampling
+            # locations across a pixel knot; measured 5.7e-3 (encoder sampling_offsets) and
+            # 4.2e-3 (backbone) of scale vs <= 2e-6 on the exact path, everything else <= 4e-4
+            rel = 1e-2
+        if err > rel * ref.abs().max().item() + 1e-5:
+            bad.append((k, err, ref.abs().max().item()))
+    assert not bad, bad
 
 
 def test_train_steps_reduce_loss(golden_dir):

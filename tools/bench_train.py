@@ -34,6 +34,8 @@ def main():
     ap.add_argument('--width', type=int, default=1333)
     ap.add_argument('--prev-dtype', default='bf16', choices=['bf16', 'f32'],
                     help='compute dtype of the no-grad previous-frame pass (HIP path)')
+    ap.add_argument('--matmul-precision', default='high', choices=['highest', 'high'],
+                    help="f32 GEMMs of the grad frame: 'high' = bf16x3 MFMA products, 'highest' = exact f32")
     a = ap.parse_args()
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -44,7 +46,8 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
     from kinet_amd.train import benchmark_train
     res = benchmark_train(a.steps, a.warmup, a.batch, a.height, a.width,
-                          torch.bfloat16 if a.prev_dtype == 'bf16' else torch.float32, dev)
+                          torch.bfloat16 if a.prev_dtype == 'bf16' else torch.float32, dev,
+                          matmul_precision=a.matmul_precision)
     if rank == 0:
         print(json.dumps(res))
     if world > 1:
