@@ -39,7 +39,8 @@ namespace {
 // tiles (gemm_dma.h) wherever eligible; 4 = never the resident-weight kernel (gemm_rw.hip);
 // 8 = resident-weight kernel from M >= 256; 16 = LDS-DMA staging for the 4-wave tiles;
 // 32 = never the dedicated stem convolution (stem.hip); 64 = no full-rounds split of the
-// multi-tap convolutions; 128 = KINET_F32_X3 weight-gradient GEMM splitting at fragment-read time
+// multi-tap convolutions; 128 = KINET_F32_X3 weight-gradient GEMM splitting at fragment-read time;
+// 256 = no XCD placement of that GEMM's K-slices; 512 = the wave-per-row attention backward
 }  // namespace
 int kinet_gemm_flags = 0;   // declared in gemm_common.h (read by grad.hip too)
 namespace {

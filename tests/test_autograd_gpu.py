@@ -125,7 +125,8 @@ def test_group_norm_fwd_bwd():
         _close(a, r, name=n)
 
 
-@pytest.mark.parametrize('E,heads,Lq,mask', [(256, 8, 300, False), (288, 8, 520, True)])
+@pytest.mark.parametrize('E,heads,Lq,mask', [(256, 8, 300, False), (288, 8, 520, True), (512, 8, 77, True),
+                                            (288, 8, 65, False)])
 def test_mha_core_fwd_bwd(E, heads, Lq, mask):
     from kinet_amd import autograd as A
     B = 2
