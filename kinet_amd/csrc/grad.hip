@@ -377,6 +377,44 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
     ws[(long)blockIdx.y * cols + c] = s;
 }
 
+// f32, 4-column vectors: lane = 4 columns (one float4 per row), the 4 waves take rows
+// r0 + w, r0 + w + 4, ... with two independent accumulators each, combined in a fixed order
+// through LDS (deterministic); one row-chunk per blockIdx.y like colsum_partial_kernel
+__global__ __launch_bounds__(256) void colsum_partial_vec_kernel(const float* __restrict__ A, float* __restrict__ ws,
+                                                                 int rows, int cols, long lda, int rc) {
+    __shared__ float4 part[4][64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c4 = blockIdx.x * 64 + lane;
+    const bool cv = c4 * 4 < cols;
+    const int r0 = blockIdx.y * rc, r1 = min(rows, r0 + rc);
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+    if (cv) {
+        const float* p = A + c4 * 4;
+        int r = r0 + wave;
+        for (; r + 4 < r1; r += 8) {
+            const float4 x = *reinterpret_cast<const float4*>(p + (long)r * lda);
+            const float4 y = *reinterpret_cast<const float4*>(p + (long)(r + 4) * lda);
+            s0.x += x.x; s0.y += x.y; s0.z += x.z; s0.w += x.w;
+            s1.x += y.x; s1.y += y.y; s1.z += y.z; s1.w += y.w;
+        }
+        if (r < r1) {
+            const float4 x = *reinterpret_cast<const float4*>(p + (long)r * lda);
+            s0.x += x.x; s0.y += x.y; s0.z += x.z; s0.w += x.w;
+        }
+    }
+    part[wave][lane] = make_float4(s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w);
+    __syncthreads();
+    if (wave == 0 && cv) {
+        float4 t = part[0][lane];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            const float4 u = part[w][lane];
+            t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        }
+        *reinterpret_cast<float4*>(ws + (long)blockIdx.y * cols + c4 * 4) = t;
+    }
+}
+
 // one workgroup per column: thread t sums chunks t, t+256, ... in order, then a fixed-order
 // LDS tree (deterministic; a serial per-column loop over ~10^3 partials was 50 us a call)
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ ws, float* __restrict__ out,
@@ -1044,7 +1082,10 @@ extern "C" int kinet_colsum(const void* A, float* out, int rows, int cols, int64
     const int chunks = (int)(kinet_colsum_workspace(rows, cols) / cols);
     const int rc = (rows + chunks - 1) / chunks;
     dim3 g1((cols + 255) / 256, chunks);
-    if (dtype == KINET_F32) hipLaunchKernelGGL(colsum_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)A, workspace, rows, cols, (long)lda, rc);
+    if (dtype == KINET_F32 && cols % 4 == 0 && lda % 4 == 0 && ((uintptr_t)A & 15) == 0)
+        hipLaunchKernelGGL(colsum_partial_vec_kernel, dim3((cols / 4 + 63) / 64, chunks), dim3(256), 0, s,
+                           (const float*)A, workspace, rows, cols, (long)lda, rc);
+    else if (dtype == KINET_F32) hipLaunchKernelGGL(colsum_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)A, workspace, rows, cols, (long)lda, rc);
     else if (dtype == KINET_BF16) hipLaunchKernelGGL(colsum_partial_kernel<bf16_t>, g1, dim3(256), 0, s, (const bf16_t*)A, workspace, rows, cols, (long)lda, rc);
     else if (dtype == KINET_F16) hipLaunchKernelGGL(colsum_partial_kernel<f16_t>, g1, dim3(256), 0, s, (const f16_t*)A, workspace, rows, cols, (long)lda, rc);
     else { set_error("colsum: unsupported dtype %d", dtype); return KINET_ERR_ARG; }

@@ -173,3 +173,16 @@ def test_multihead_attention_matches_module():
     for n, a, r in zip(['y', 'dx', 'dWin', 'dWout'], got, [y2.detach(), x2.grad, mod.in_proj_weight.grad,
                                                            mod.out_proj.weight.grad]):
         _close(a, r, rel=2e-4, name=n)
+
+
+@pytest.mark.parametrize('rows,cols', [(44446, 288), (1000, 1024), (777, 90), (5, 12), (70000, 256)])
+def test_colsum_vs_f64_and_deterministic(rows, cols):
+    from kinet_amd import kernels as K
+    g = torch.Generator().manual_seed(rows + cols)
+    a = torch.randn(rows, cols, generator=g, dtype=torch.float64)
+    out = K.colsum(a.float().cuda())
+    out2 = K.colsum(a.float().cuda())
+    torch.cuda.synchronize()
+    ref = a.sum(0)
+    assert torch.equal(out, out2)
+    assert ((out.double().cpu() - ref).abs() <= 1e-6 * a.abs().sum(0) + 1e-6).all()
