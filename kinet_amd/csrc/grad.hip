@@ -748,9 +748,11 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
 // Tiled attention backward (default; flag 512 selects the wave-per-row kernels above).  The
 // wave-per-row kernels read every key row per query through per-lane strided loads (and every
 // P / dS column per key), ~0.9 ms per decoder self-attention at config 4.  Here a lane owns
-// one query (q2) or one key (kv2), the four waves of a workgroup split the other dimension,
+// one query (q2) or one key (kv2), the eight waves of a workgroup split the other dimension,
 // and that dimension's rows are staged in LDS in chunks of 64 and read as broadcasts.
 constexpr int AT_T = 64;
+// waves per workgroup splitting the other dimension: 8, or 4 for head dims past 36 (LDS)
+template <int MD> constexpr int at_nw() { return MD <= 36 ? 8 : 4; }
 template <int MD>
 __device__ __forceinline__ float dot_lds(const float (&x)[MD], const float* row) {
     float s = 0.f;
@@ -761,24 +763,36 @@ __device__ __forceinline__ float dot_lds(const float (&x)[MD], const float* row)
     }
     return s;
 }
-// stage rows [r0, r0 + 64) of a (rows, ld) matrix, columns [c0, c0 + D), into an LDS [64][MD]
-// image, zero past the last row / column
-template <int MD>
-__device__ __forceinline__ void stage_rows(float (*dst)[MD], const float* src, long ld, int r0, int rows, int c0, int D) {
-    for (int e = threadIdx.x; e < AT_T * MD; e += 256) {
-        const int r = e / MD, d = e - (e / MD) * MD, rr = r0 + r;
-        dst[r][d] = (rr < rows && d < D) ? src[(long)rr * ld + c0 + d] : 0.f;
+// the same 64-row chunk held in registers (this thread's elements), so the next chunk's
+// global loads are in flight while the current one is computed
+template <int MD, int AT_NT>
+struct RowChunk {
+    static constexpr int N = (AT_T * MD + AT_NT - 1) / AT_NT;
+    float v[N];
+    __device__ __forceinline__ void load(const float* src, long ld, int r0, int rows, int c0, int D) {
+#pragma unroll
+        for (int u = 0; u < N; ++u) {
+            const int e = threadIdx.x + AT_NT * u, r = e / MD, d = e - (e / MD) * MD, rr = r0 + r;
+            v[u] = (e < AT_T * MD && rr < rows && d < D) ? src[(long)rr * ld + c0 + d] : 0.f;
+        }
     }
-}
+    __device__ __forceinline__ void store(float (*dst)[MD]) const {
+#pragma unroll
+        for (int u = 0; u < N; ++u) {
+            const int e = threadIdx.x + AT_NT * u;
+            if (e < AT_T * MD) dst[e / MD][e - (e / MD) * MD] = v[u];
+        }
+    }
+};
 
 // pass 1: lane = query i; softmax statistics, then di_i = sum_j P_ij dP_ij, then dS_ij and
 // dQ_i = scale * sum_j dS_ij K_j; P and dS rows stored to the workspace for pass 2
-template <int MD>
-__global__ __launch_bounds__(256) void attn_bwd_q2_kernel(AttnArgs a) {
+template <int MD, int AT_NW = at_nw<MD>(), int AT_NT = 64 * AT_NW>
+__global__ __launch_bounds__(AT_NT) void attn_bwd_q2_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) float Ks[AT_T][MD];
     __shared__ __attribute__((aligned(16))) float Vs[AT_T][MD];
-    __shared__ float st[4][AT_T][2];
-    __shared__ float red[4][AT_T][MD + 1];
+    __shared__ float st[AT_NW][AT_T][2];
+    __shared__ float red[AT_NW][AT_T][MD + 1];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
     const int i = blockIdx.x * AT_T + lane;
@@ -798,18 +812,32 @@ __global__ __launch_bounds__(256) void attn_bwd_q2_kernel(AttnArgs a) {
     const uint8_t* km = a.key_mask ? a.key_mask + (long)b * a.Lk : nullptr;
     float* Prow = a.P + ((long)bh * a.Lq + (iv ? i : 0)) * a.Lk;
     float* Srow = a.dS + ((long)bh * a.Lq + (iv ? i : 0)) * a.Lk;
-    const int r0 = wave * (AT_T / 4);
+    const int r0 = wave * (AT_T / AT_NW);
     auto score = [&](int r, int j) {
         const float sc = dot_lds<MD>(qv, Ks[r]) * a.scale;
         return (km && km[j]) ? -INFINITY : sc;
     };
     // phase A: running max / sum over this wave's keys of every chunk
     float m = -INFINITY, l = 0.f;
-    for (int j0 = 0; j0 < a.Lk; j0 += AT_T) {
-        __syncthreads();
-        stage_rows<MD>(Ks, Kb, a.ldk, j0, a.Lk, h * a.D, a.D);
-        __syncthreads();
-        for (int r = r0; r < r0 + AT_T / 4 && j0 + r < a.Lk; ++r) {
+    RowChunk<MD, AT_NT> ck, cv;
+    // chunk loop with the next chunk's loads issued before the current chunk is computed
+    auto chunks = [&](bool withV, auto&& body) {
+        ck.load(Kb, a.ldk, 0, a.Lk, h * a.D, a.D);
+        if (withV) cv.load(Vb, a.ldv, 0, a.Lk, h * a.D, a.D);
+        for (int j0 = 0; j0 < a.Lk; j0 += AT_T) {
+            __syncthreads();
+            ck.store(Ks);
+            if (withV) cv.store(Vs);
+            __syncthreads();
+            if (j0 + AT_T < a.Lk) {
+                ck.load(Kb, a.ldk, j0 + AT_T, a.Lk, h * a.D, a.D);
+                if (withV) cv.load(Vb, a.ldv, j0 + AT_T, a.Lk, h * a.D, a.D);
+            }
+            body(j0);
+        }
+    };
+    chunks(false, [&](int j0) {
+        for (int r = r0; r < r0 + AT_T / AT_NW && j0 + r < a.Lk; ++r) {
             const float sc = score(r, j0 + r);
             if (sc == -INFINITY) continue;
             if (sc > m) {
@@ -819,46 +847,40 @@ __global__ __launch_bounds__(256) void attn_bwd_q2_kernel(AttnArgs a) {
                 l += __expf(sc - m);
             }
         }
-    }
+    });
     st[wave][lane][0] = m;
     st[wave][lane][1] = l;
     __syncthreads();
     float mx = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) mx = fmaxf(mx, st[w][lane][0]);
+    for (int w = 0; w < AT_NW; ++w) mx = fmaxf(mx, st[w][lane][0]);
     float sum = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w)
+    for (int w = 0; w < AT_NW; ++w)
         if (st[w][lane][0] != -INFINITY) sum += st[w][lane][1] * __expf(st[w][lane][0] - mx);
     const float rs = sum > 0.f ? 1.f / sum : 0.f;
     auto prob = [&](float sc) { return (mx == -INFINITY || sc == -INFINITY) ? 0.f : __expf(sc - mx) * rs; };
     // phase B: di = sum_j P_ij (dO_i . V_j); P stored
     float di = 0.f;
-    for (int j0 = 0; j0 < a.Lk; j0 += AT_T) {
-        __syncthreads();
-        stage_rows<MD>(Ks, Kb, a.ldk, j0, a.Lk, h * a.D, a.D);
-        stage_rows<MD>(Vs, Vb, a.ldv, j0, a.Lk, h * a.D, a.D);
-        __syncthreads();
-        for (int r = r0; r < r0 + AT_T / 4 && j0 + r < a.Lk; ++r) {
+    chunks(true, [&](int j0) {
+        for (int r = r0; r < r0 + AT_T / AT_NW && j0 + r < a.Lk; ++r) {
             const float p = prob(score(r, j0 + r));
             di += p * dot_lds<MD>(ov, Vs[r]);
             if (iv) Prow[j0 + r] = p;
         }
-    }
+    });
     __syncthreads();
     st[wave][lane][0] = di;
     __syncthreads();
-    di = st[0][lane][0] + st[1][lane][0] + st[2][lane][0] + st[3][lane][0];
+    di = 0.f;
+#pragma unroll
+    for (int w = 0; w < AT_NW; ++w) di += st[w][lane][0];
     // phase C: dS_ij = P_ij (dP_ij - di), dQ_i partial over this wave's keys
     float dq[MD];
 #pragma unroll
     for (int d = 0; d < MD; ++d) dq[d] = 0.f;
-    for (int j0 = 0; j0 < a.Lk; j0 += AT_T) {
-        __syncthreads();
-        stage_rows<MD>(Ks, Kb, a.ldk, j0, a.Lk, h * a.D, a.D);
-        stage_rows<MD>(Vs, Vb, a.ldv, j0, a.Lk, h * a.D, a.D);
-        __syncthreads();
-        for (int r = r0; r < r0 + AT_T / 4 && j0 + r < a.Lk; ++r) {
+    chunks(true, [&](int j0) {
+        for (int r = r0; r < r0 + AT_T / AT_NW && j0 + r < a.Lk; ++r) {
             const float p = prob(score(r, j0 + r));
             const float ds = p * (dot_lds<MD>(ov, Vs[r]) - di);
             if (iv) Srow[j0 + r] = ds;
@@ -871,25 +893,29 @@ __global__ __launch_bounds__(256) void attn_bwd_q2_kernel(AttnArgs a) {
                 dq[d + 3] += ds * k.w;
             }
         }
-    }
+    });
+    __syncthreads();
 #pragma unroll
     for (int d = 0; d < MD; ++d) red[wave][lane][d] = dq[d];
     __syncthreads();
-    for (int e = threadIdx.x; e < AT_T * MD; e += 256) {
+    for (int e = threadIdx.x; e < AT_T * MD; e += AT_NT) {
         const int li = e / MD, d = e - (e / MD) * MD, ii = blockIdx.x * AT_T + li;
-        if (ii < a.Lq && d < a.D)
-            a.dQ[((long)b * a.Lq + ii) * a.ldq + h * a.D + d] =
-                (red[0][li][d] + red[1][li][d] + red[2][li][d] + red[3][li][d]) * a.scale;
+        if (ii < a.Lq && d < a.D) {
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < AT_NW; ++w) v += red[w][li][d];
+            a.dQ[((long)b * a.Lq + ii) * a.ldq + h * a.D + d] = v * a.scale;
+        }
     }
 }
 
 // pass 2: lane = key j; dK_j = scale * sum_i dS_ij Q_i, dV_j = sum_i P_ij dO_i (P / dS rows read
 // coalesced across the 64 keys of the tile)
-template <int MD>
-__global__ __launch_bounds__(256) void attn_bwd_kv2_kernel(AttnArgs a) {
+template <int MD, int AT_NW = at_nw<MD>(), int AT_NT = 64 * AT_NW>
+__global__ __launch_bounds__(AT_NT) void attn_bwd_kv2_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) float Qs[AT_T][MD];
     __shared__ __attribute__((aligned(16))) float Os[AT_T][MD];
-    __shared__ float red[4][AT_T][MD + 1];
+    __shared__ float red[AT_NW][AT_T][MD + 1];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
     const int j = blockIdx.x * AT_T + lane;
@@ -901,13 +927,20 @@ __global__ __launch_bounds__(256) void attn_bwd_kv2_kernel(AttnArgs a) {
     float dk[MD], dv[MD];
 #pragma unroll
     for (int d = 0; d < MD; ++d) dk[d] = dv[d] = 0.f;
-    const int r0 = wave * (AT_T / 4);
+    const int r0 = wave * (AT_T / AT_NW);
+    RowChunk<MD, AT_NT> cq, co;
+    cq.load(Qb, a.ldq, 0, a.Lq, h * a.D, a.D);
+    co.load(Ob, a.ldo, 0, a.Lq, h * a.D, a.D);
     for (int i0 = 0; i0 < a.Lq; i0 += AT_T) {
         __syncthreads();
-        stage_rows<MD>(Qs, Qb, a.ldq, i0, a.Lq, h * a.D, a.D);
-        stage_rows<MD>(Os, Ob, a.ldo, i0, a.Lq, h * a.D, a.D);
+        cq.store(Qs);
+        co.store(Os);
         __syncthreads();
-        for (int r = r0; r < r0 + AT_T / 4 && i0 + r < a.Lq; ++r) {
+        if (i0 + AT_T < a.Lq) {
+            cq.load(Qb, a.ldq, i0 + AT_T, a.Lq, h * a.D, a.D);
+            co.load(Ob, a.ldo, i0 + AT_T, a.Lq, h * a.D, a.D);
+        }
+        for (int r = r0; r < r0 + AT_T / AT_NW && i0 + r < a.Lq; ++r) {
             const long ro = (long)(i0 + r) * a.Lk;
             const float p = jv ? Pc[ro] : 0.f, ds = jv ? Sc[ro] : 0.f;
 #pragma unroll
@@ -925,10 +958,12 @@ __global__ __launch_bounds__(256) void attn_bwd_kv2_kernel(AttnArgs a) {
 #pragma unroll
         for (int d = 0; d < MD; ++d) red[wave][lane][d] = pass ? dv[d] : dk[d];
         __syncthreads();
-        for (int e = threadIdx.x; e < AT_T * MD; e += 256) {
+        for (int e = threadIdx.x; e < AT_T * MD; e += AT_NT) {
             const int lj = e / MD, d = e - (e / MD) * MD, jj = blockIdx.x * AT_T + lj;
             if (jj < a.Lk && d < a.D) {
-                const float v = red[0][lj][d] + red[1][lj][d] + red[2][lj][d] + red[3][lj][d];
+                float v = 0.f;
+#pragma unroll
+                for (int w = 0; w < AT_NW; ++w) v += red[w][lj][d];
                 if (pass) a.dV[((long)b * a.Lk + jj) * a.ldv + h * a.D + d] = v;
                 else a.dK[((long)b * a.Lk + jj) * a.ldk + h * a.D + d] = v * a.scale;
             }
@@ -1182,9 +1217,9 @@ extern "C" int kinet_mha_backward(const float* Q, int ldq, const float* K, int l
         const dim3 gq((Lq + AT_T - 1) / AT_T, batch * heads), gk((Lk + AT_T - 1) / AT_T, batch * heads);
 #define AT2(MD_)                                                                  \
     do {                                                                          \
-        hipLaunchKernelGGL(attn_bwd_q2_kernel<MD_>, gq, dim3(256), 0, s, a);      \
+        hipLaunchKernelGGL(attn_bwd_q2_kernel<MD_>, gq, dim3(64 * at_nw<MD_>()), 0, s, a);      \
         KINET_LAUNCH_CHECK();                                                     \
-        hipLaunchKernelGGL(attn_bwd_kv2_kernel<MD_>, gk, dim3(256), 0, s, a);     \
+        hipLaunchKernelGGL(attn_bwd_kv2_kernel<MD_>, gk, dim3(64 * at_nw<MD_>()), 0, s, a);     \
     } while (0)
         if (head_dim <= 32) AT2(32);
         else if (head_dim <= 36) AT2(36);

@@ -753,53 +753,82 @@ extern "C" int kinet_box_refine(const float* tmp, const float* ref, int ref_dim,
 // ---------------------------------------------------------------------------------
 namespace kinet {
 namespace {
+// a workgroup owns 64 consecutive pixels: 4 threads per pixel split its column / row
+// cumulative counts of unmasked pixels (the reference's two cumsums), the (z, y, x) embedding
+// arguments go through LDS, then the 256 threads write the 64 x C outputs channel-fastest
+// (coalesced NHWC rows)
+constexpr int SE_PIX = 64;
 template <typename TO>
 __global__ __launch_bounds__(256) void sine_embed_kernel(const uint8_t* __restrict__ mask, const float* __restrict__ dim_t,
                                                          const float* __restrict__ level_embed, TO* __restrict__ out,
                                                          int B, int H, int W, int npf, int three_d, int frame,
                                                          int frames, int normalize, float scale, long out_bs) {
+    __shared__ float arg[SE_PIX][3];
     const long total = (long)B * H * W;
     const int C = (three_d ? 3 : 2) * npf;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const int w = (int)(i % W);
-        const long r = i / W;
-        const int h = (int)(r % H), b = (int)(r / H);
-        const uint8_t* mb = mask + (long)b * H * W;
-        // cumulative counts of unmasked pixels along the column (y) and the row (x)
-        float ycum = 0.f, ytot = 0.f, xcum = 0.f, xtot = 0.f;
-        for (int k = 0; k < H; ++k) {
-            const float v = mb[(long)k * W + w] ? 0.f : 1.f;
-            ytot += v;
-            if (k <= h) ycum += v;
-        }
-        for (int k = 0; k < W; ++k) {
-            const float v = mb[(long)h * W + k] ? 0.f : 1.f;
-            xtot += v;
-            if (k <= w) xcum += v;
-        }
-        const bool valid = !mb[(long)h * W + w];
-        float ye = ycum, xe = xcum, ze = valid ? (float)(frame + 1) : 0.f;
-        if (normalize) {
-            const float eps = 1e-6f;
-            if (three_d) {   // :49-51, no -0.5 offset
-                ze = ze / ((valid ? (float)frames : 0.f) + eps) * scale;
-                ye = ye / (ytot + eps) * scale;
-                xe = xe / (xtot + eps) * scale;
-            } else {         // :106-108
-                ye = (ye - 0.5f) / (ytot + eps) * scale;
-                xe = (xe - 0.5f) / (xtot + eps) * scale;
+    for (long p0 = (long)blockIdx.x * SE_PIX; p0 < total; p0 += (long)gridDim.x * SE_PIX) {
+        {
+            const int pl = threadIdx.x >> 2, part = threadIdx.x & 3;
+            const long i = p0 + pl;
+            float ycum = 0.f, ytot = 0.f, xcum = 0.f, xtot = 0.f;
+            int h = 0, w = 0, b = 0;
+            if (i < total) {
+                w = (int)(i % W);
+                const long r = i / W;
+                h = (int)(r % H);
+                b = (int)(r / H);
+                const uint8_t* mb = mask + (long)b * H * W;
+                for (int k = part; k < H; k += 4) {
+                    const float v = mb[(long)k * W + w] ? 0.f : 1.f;
+                    ytot += v;
+                    if (k <= h) ycum += v;
+                }
+                for (int k = part; k < W; k += 4) {
+                    const float v = mb[(long)h * W + k] ? 0.f : 1.f;
+                    xtot += v;
+                    if (k <= w) xcum += v;
+                }
+            }
+#pragma unroll
+            for (int o = 1; o < 4; o <<= 1) {   // the 4 threads of a pixel are adjacent lanes
+                ycum += __shfl_xor(ycum, o);
+                ytot += __shfl_xor(ytot, o);
+                xcum += __shfl_xor(xcum, o);
+                xtot += __shfl_xor(xtot, o);
+            }
+            if (part == 0 && i < total) {
+                const bool valid = !mask[(long)b * H * W + (long)h * W + w];
+                float ye = ycum, xe = xcum, ze = valid ? (float)(frame + 1) : 0.f;
+                if (normalize) {
+                    const float eps = 1e-6f;
+                    if (three_d) {   // position_encoding.py:49-51, no -0.5 offset
+                        ze = ze / ((valid ? (float)frames : 0.f) + eps) * scale;
+                        ye = ye / (ytot + eps) * scale;
+                        xe = xe / (xtot + eps) * scale;
+                    } else {         // :106-108
+                        ye = (ye - 0.5f) / (ytot + eps) * scale;
+                        xe = (xe - 0.5f) / (xtot + eps) * scale;
+                    }
+                }
+                arg[pl][0] = three_d ? ze : ye;
+                arg[pl][1] = three_d ? ye : xe;
+                arg[pl][2] = xe;
             }
         }
-        TO* o = out + (long)b * out_bs + ((long)h * W + w) * C;
+        __syncthreads();
+        const int np = (int)min((long)SE_PIX, total - p0);
         // channel order: [z (3-d only) | y | x], each interleaving sin (even) / cos (odd)
-        for (int c = 0; c < C; ++c) {
+        for (int e = threadIdx.x; e < np * C; e += 256) {
+            const int pl = e / C, c = e - pl * C;
+            const long i = p0 + pl;
             const int part = c / npf, k = c - part * npf;
-            const float e = three_d ? (part == 0 ? ze : part == 1 ? ye : xe) : (part == 0 ? ye : xe);
-            const float a = e / dim_t[k];
+            const float a = arg[pl][part] / dim_t[k];
             float v = (k & 1) ? cosf(a) : sinf(a);
             if (level_embed) v += level_embed[c];
-            o[c] = Cvt<TO>::from(v);
+            const long b = i / ((long)H * W), hw = i - b * H * W;
+            out[b * out_bs + hw * C + c] = Cvt<TO>::from(v);
         }
+        __syncthreads();
     }
 }
 }  // namespace
@@ -816,7 +845,7 @@ extern "C" int kinet_sine_position_embed(const uint8_t* mask, const float* dim_t
                     frame, frames);
     const long n = (long)B * H * W;
     if (n == 0) return KINET_OK;
-    const int grid = (int)std::min<long>((n + 255) / 256, 4096);
+    const int grid = (int)std::min<long>((n + SE_PIX - 1) / SE_PIX, 8192);
     hipStream_t s = (hipStream_t)stream;
 #define SE(TO) hipLaunchKernelGGL(sine_embed_kernel<TO>, dim3(grid), dim3(256), 0, s, mask, dim_t, level_embed, (TO*)out, \
                                   B, H, W, num_pos_feats, three_d, frame, frames, normalize, scale, (long)out_batch_stride)
