@@ -41,7 +41,7 @@ from torch import nn
 from kinet_amd import autograd as A
 from kinet_amd import kernels as K
 from kinet_amd.models.deformable_detr import MLP
-from kinet_amd.models.misc import NestedTensor
+from kinet_amd.models.misc import NestedTensor, NestedTensorKinet
 
 
 # ----------------------------------------------------------------------------- op helpers
@@ -474,6 +474,40 @@ class KinetTracking(KinematicDetectorTransformer):
                     '(detr.py:397-399, see kinet_amd/models/kinet.py); train with ratio_add_tracklets = 0')
             self.generate_empty_tracklets(targets)
         return super().forward(samples, targets)
+
+
+def graph_kinet_forward(model, samples, targets=None, warmup=3):
+    """A HIP-graph replay (kinet_amd/graph.py) of the no-grad inference forward of `model` for
+    the signature of (samples, targets): batch, detection slots, tracklet-query count, dtypes.
+    Returns call(samples, targets) -> the forward's output dict (graph-owned buffers,
+    overwritten by the next call).  The batch-1 tracking forward is launch-bound eager
+    (~1 ms host for ~0.1 ms of kernels); replay removes the per-kernel host cost."""
+    from kinet_amd.graph import GraphedCall
+    B = samples.detections.tensors.shape[0]
+    has_trk = targets is not None and len(targets[0]['track_query_hs_embeds_det']) > 0
+
+    def flat(smp, tgs):
+        ts = [smp.detections.tensors, smp.detections.mask, smp.metadata.tensors, smp.metadata.mask]
+        if has_trk:
+            ts += [torch.stack([t['track_query_hs_embeds_det'] for t in tgs]),
+                   torch.stack([t['track_query_hs_embeds_meta'] for t in tgs])]
+        return ts
+
+    def fn(d, dm, m, mm, *trk):
+        smp = NestedTensorKinet(NestedTensor(d, dm), NestedTensor(m, mm))
+        tgs = None
+        if has_trk:
+            tgs = [{'track_query_hs_embeds_det': trk[0][i], 'track_query_hs_embeds_meta': trk[1][i]}
+                   for i in range(B)]
+        return model(smp, tgs)[0]
+
+    gc = GraphedCall(fn, flat(samples, targets), warmup)
+
+    def call(smp, tgs=None):
+        if (tgs is not None and len(tgs[0]['track_query_hs_embeds_det']) > 0) != has_trk:
+            raise ValueError('graph_kinet_forward: tracklet queries present / absent unlike the recording')
+        return gc(*flat(smp, tgs))
+    return call
 
 
 def build_kinet(args, num_classes, matcher=None):

@@ -133,3 +133,37 @@ def test_kinet_bf16(golden_dir):
     # bf16 operands, f32 accumulation: logits / boxes stay within these max-abs bounds of f32
     assert (out['pred_logits'] - ref['pred_logits']).abs().max().item() < 0.1
     assert (out['pred_boxes'] - ref['pred_boxes']).abs().max().item() < 0.02
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_kinet_graph_replay_equals_eager(golden_dir, dtype):
+    """graph_kinet_forward (HIP-graph replay): bit-identical to the eager forward, for the
+    recorded inputs and for new ones with a different padding mask and new tracklet queries
+    (the mask embedding is recomputed inside the graph, not taken from the warm-up)."""
+    from kinet_amd.models.kinet import graph_kinet_forward
+    d = np.load(os.path.join(golden_dir, 'kinet.npz'))
+    model = _model(golden_dir, 2)
+    model.set_compute_dtype(dtype)
+    trk_det, trk_meta = torch.from_numpy(d['k_trk_det']).cuda(), torch.from_numpy(d['k_trk_meta']).cuda()
+
+    def tg(scale):
+        return [{'track_query_hs_embeds_det': trk_det[b] * scale, 'track_query_hs_embeds_meta': trk_meta[b] * scale}
+                for b in range(trk_det.shape[0])]
+    s0 = _samples(d)
+    with torch.no_grad():
+        call = graph_kinet_forward(model, s0, tg(1.0))
+        s1 = _samples(d)
+        m1 = s1.detections.mask.clone()
+        m1[:, -3:] = ~m1[:, -3:]
+        from kinet_amd.models import NestedTensor, NestedTensorKinet
+        s1 = NestedTensorKinet(NestedTensor(s1.detections.tensors.flip(1).contiguous(), m1),
+                               NestedTensor(s1.metadata.tensors.flip(1).contiguous(), m1))
+        for smp, t in ((s0, tg(1.0)), (s1, tg(0.5)), (s0, tg(1.0))):
+            ref, *_ = model(smp, t)
+            got = call(smp, t)
+            torch.cuda.synchronize()
+            assert torch.equal(got['pred_logits'], ref['pred_logits'])
+            assert torch.equal(got['pred_boxes'], ref['pred_boxes'])
+        with pytest.raises(ValueError):
+            call(s0, None)

@@ -59,7 +59,20 @@ def main():
                     model(s, tg)
                 torch.cuda.synchronize()
             el = (time.perf_counter() - t0) / a.iters
-            res[f'{name}_{str(dt).split(".")[-1]}'] = {'ms_per_forward': el * 1e3, 'frames_per_s': B / el}
+            key = f'{name}_{str(dt).split(".")[-1]}'
+            res[key] = {'ms_per_forward': el * 1e3, 'frames_per_s': B / el}
+            # the same forward replayed from a HIP graph (models/kinet.py graph_kinet_forward)
+            from kinet_amd.models.kinet import graph_kinet_forward
+            call = graph_kinet_forward(model, s, tg)
+            for _ in range(10):
+                call(s, tg)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.iters):
+                call(s, tg)
+            torch.cuda.synchronize()
+            el = (time.perf_counter() - t0) / a.iters
+            res[key + '_graph'] = {'ms_per_forward': el * 1e3, 'frames_per_s': B / el}
     print(json.dumps({'metric': 'KineT forward (cfgs/train_kinet.yaml model), frames/s', 'dets': a.dets,
                       'tracklets': a.tracklets, 'results': res}))
 
