@@ -38,7 +38,8 @@ MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'f16': 2500.0, 'f32': 157.3}   # dense
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command
 # (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950 per MI355X_MICROARCH.md "HBM")
 PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
-MSDA_KERNEL = 'msda_fused_fast_kernel'
+MSDA_ENC_KERNEL = 'msda_enc_lds_kernel'     # config-2 encoder calls (coarse levels in LDS)
+MSDA_KERNEL = 'msda_fused_fast_kernel'      # decoder calls
 
 WORKLOADS = {
     'config2': dict(cfgs=('train_deformable',), over={}, h=800, w=1333, batch=16, streams=3, dtype='bf16',
@@ -338,24 +339,32 @@ def main():
         msda_dec_ms = statistics.mean(m[2] for m in dec) if dec else None
         mfma_ms = sum(fam[f]['ms'] for f in ('gemm', 'conv') if f in fam)
         mfma_flops = sum(fam[f]['flops'] for f in ('gemm', 'conv') if f in fam)
-        # Headline roofline: the fused MSDA sampling kernel -- the operator this path is
-        # built around and the single kernel with the most device time in the rocprofv3
-        # summary (profiles/) -- over ALL its launches (6 encoder + 6 decoder per frame
-        # batch), so avg_launch_ms is the rocprof average of that kernel name.
+        # Headline roofline: the MSDA sampling kernel with the most device time in the
+        # rocprofv3 summary (profiles/).  config 2: msda_enc_lds_kernel, which runs the 6
+        # encoder calls per frame batch (avg_launch_ms = the rocprof average of that kernel
+        # name); the 6 decoder calls run msda_fused_fast_kernel, reported beside it.
+        # config 5 (D=36): the generic msda_fused_kernel over all its launches.
         msda_roof = None
         if msda:
-            tot_ms = sum(m[2] for m in msda)
-            tot_bytes = sum(m[3] for m in msda)
-            ach = tot_bytes / (tot_ms * 1e-3) / 1e9
-            traffic, src = pmc_traffic(MSDA_KERNEL) if a.workload == 'config2' else (None, None)
-            kname = MSDA_KERNEL + '<bf16_t, 4, 4>' if a.workload == 'config2' else 'msda_fused_kernel<f16_t, 4> (D=36)'
-            msda_roof = {'bound': 'hbm', 'kernel': kname + ' (encoder + decoder launches)',
-                         'achieved': ach, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': ach / HBM_PEAK_GBS,
-                         'traffic': traffic, 'traffic_source': src,
-                         'algorithmic_bytes_per_launch': tot_bytes / len(msda),
-                         'avg_launch_ms': tot_ms / len(msda), 'launches_per_step': len(msda) / 3,
-                         'encoder_launch': {'ms': msda_enc_ms, 'bytes': enc[0][3] if enc else None},
-                         'decoder_launch': {'ms': msda_dec_ms, 'bytes': dec[0][3] if dec else None}}
+            def roof(launches, kname, pmc_name):
+                t_ms = sum(m[2] for m in launches)
+                t_b = sum(m[3] for m in launches)
+                ach_ = t_b / (t_ms * 1e-3) / 1e9
+                traffic, src = pmc_traffic(pmc_name) if (pmc_name and a.workload == 'config2') else (None, None)
+                return {'bound': 'hbm', 'kernel': kname, 'achieved': ach_, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                        'frac': ach_ / HBM_PEAK_GBS, 'traffic': traffic, 'traffic_source': src,
+                        'algorithmic_bytes_per_launch': t_b / len(launches),
+                        'avg_launch_ms': t_ms / len(launches), 'launches_per_step': len(launches) / 3}
+            if a.workload == 'config2' and enc and dec:
+                msda_roof = roof(enc, MSDA_ENC_KERNEL + '<f16_t, bf16_t, f16_t> (encoder launches, Lq = S = %d)'
+                                 % enc[0][0], MSDA_ENC_KERNEL)
+                msda_roof['decoder_kernel'] = roof(dec, MSDA_KERNEL + '<f16_t, bf16_t, f16_t, 4, 4> (decoder launches)',
+                                                   MSDA_KERNEL)
+                msda_roof['all_msda_launches'] = roof(msda, 'encoder + decoder launches', None)
+            else:
+                msda_roof = roof(msda, 'msda_fused_kernel<f16_t, 4> (D=36, encoder + decoder launches)', None)
+            msda_roof['encoder_launch'] = {'ms': msda_enc_ms, 'bytes': enc[0][3] if enc else None}
+            msda_roof['decoder_launch'] = {'ms': msda_dec_ms, 'bytes': dec[0][3] if dec else None}
         mfma_ach = mfma_flops / (mfma_ms * 1e-3) / 1e12 if mfma_ms else 0.0
         mfma_roof = {'bound': 'mfma', 'kernel': 'all GEMM + conv launches (gemm_kernel, gemm_rw_kernel)',
                      'achieved': mfma_ach, 'peak': MFMA_PEAK_TFLOPS[dt_name], 'unit': 'TFLOP/s',
