@@ -39,7 +39,8 @@ constexpr int kMaxLevels = 16;
 // diagnostic flags (kinet_msda_set_flags): bit 0 = never use msda_fused_fast_kernel; bit 1 = its
 // 4-head x 4-sample-group variant, bit 2 = 4 heads x 2 (the default is 2 heads x 2; timing studies);
 // bit 5 = never use msda_enc_lds_kernel (encoder calls then take msda_fused_fast_kernel); bit 6 =
-// msda_enc_lds_kernel with every tap product accumulated in f32 (no f16 per-level partial sums)
+// msda_enc_lds_kernel with every tap product accumulated in f32 (no f16 per-level partial sums);
+// bit 7 = half as many query chunks per head map (one round of workgroups; timing studies)
 int msda_flags = 0;
 
 struct LevelInfo {
@@ -753,6 +754,22 @@ __device__ __forceinline__ uint32_t pk_fma_whi(uint32_t acc, uint32_t v, uint32_
     return acc;
 }
 
+__device__ __forceinline__ uint32_t pk_mul_wlo(uint32_t v, uint32_t w) {
+    uint32_t d;
+    asm("v_pk_mul_f16 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(d) : "v"(v), "v"(w));
+    return d;
+}
+
+// corners 1-3 of a level's first sample (corner 0 started the sum with a multiply)
+__device__ __forceinline__ void mac_sample16_tail(uint32_t (&h)[4], const u32x4v (&v)[4], uint32_t w01, uint32_t w23) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        h[j] = pk_fma_whi(h[j], v[1][j], w01);
+        h[j] = pk_fma_wlo(h[j], v[2][j], w23);
+        h[j] = pk_fma_whi(h[j], v[3][j], w23);
+    }
+}
+
 // one sample's 4 corners x 8 channels into the running f16 pairs of its level
 __device__ __forceinline__ void mac_sample16(uint32_t (&h)[4], const u32x4v (&v)[4], uint32_t w01, uint32_t w23) {
 #pragma unroll
@@ -771,17 +788,8 @@ __device__ __forceinline__ void flush16(f32x2 (&acc)[4], uint32_t (&h)[4]) {
     for (int j = 0; j < 4; ++j) {
         acc[j][0] = fma_mix16_lo_lo(acc[j][0], h[j], one);
         acc[j][1] = fma_mix16_hi_lo(acc[j][1], h[j], one);
-        h[j] = 0u;
     }
 }
-
-template <int LC>
-struct EncLane {   // per-lane phase-1 constants: lane = (query of 4, sample of 16), level fixed
-    int H, W, pbase;
-    float Hf, Wf, rH, rW;
-    bool lok;
-    uint32_t z;
-};
 
 // ACC16: the 16 bilinear taps of one level (P points x 4 corners) are summed as f16 pairs
 // by v_pk_fma_f16 (2 MACs per instruction, 11-bit significand -- above the bf16 compute
@@ -793,8 +801,8 @@ __device__ __forceinline__ void enc_lds_tiles(const FastLevels& lv, const EncSta
                                               const __amdgpu_buffer_rsrc_t& ro, int ld_off,
                                               const __amdgpu_buffer_rsrc_t& rr, const __amdgpu_buffer_rsrc_t& rq,
                                               TO* __restrict__ out,
-                                              int b, int m, int M, int Lq, const int* __restrict__ torder, int tb,
-                                              int te, int wave, int lane) {
+                                              int b, int m, int M, int Lq, const int* __restrict__ torder, int chunk,
+                                              int nchunk, int ntile, int wave, int lane) {
     constexpr int L = 4, P = 4, LP = 16, D = 32, QT = 16, NW = kEncWaves;
     constexpr int NG = LC * P, NL = LP - NG;
     // phase-1 lane constants, hoisted out of the tile loop: lane = (query lane >> 2, level
@@ -816,7 +824,9 @@ __device__ __forceinline__ void enc_lds_tiles(const FastLevels& lv, const EncSta
     const uint32_t lg_off = (uint32_t)(M * LP * 2 + m * LP + l * P) * (uint32_t)sizeof(TL);
     const uint32_t of_off = (uint32_t)((m * LP + l * P) * 2) * (uint32_t)sizeof(TL);
     const float rscale = 0.5f / (float)P;
-    for (int t = tb + wave; t < te; t += NW) {
+    // this workgroup's 16-tile groups are chunk, chunk + nchunk, ...: the workgroups of one
+    // head map sweep the (row-ordered) tiles side by side and share its rows in L2
+    for (int t = chunk * NW + wave; t < ntile; t += nchunk * NW) {
         const int bx = torder ? torder[t] : t;
         const int q0 = bx * QT;
         // the previous tile's record reads are done before this tile overwrites them
@@ -828,7 +838,7 @@ __device__ __forceinline__ void enc_lds_tiles(const FastLevels& lv, const EncSta
         const int q = q0 + qi;
         const bool ok = q < Lq;
         const uint32_t row = (uint32_t)(b * Lq + (ok ? q : Lq - 1));
-        const uint32_t ob = row * rowstride;
+        const uint32_t ob = __umul24(row, rowstride);   // row < 2^24 (host check)
         float lg[P], ox[P], oy[P];
         if constexpr (std::is_same<TL, float>::value) {
             const u32x4v o0 = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(ro, ob + of_off, 0, 0));
@@ -901,7 +911,7 @@ __device__ __forceinline__ void enc_lds_tiles(const FastLevels& lv, const EncSta
             // corners are +64 B); a corner outside the level keeps its address -- a
             // neighbouring pixel, a margin row, or past the buffer's range (reads 0) -- and
             // gets weight 0
-            const uint32_t o00 = valid ? (uint32_t)(pbase + (hl * W + wl) * 64) : zoff;
+            const uint32_t o00 = valid ? (uint32_t)(pbase + (__mul24(hl, W) + wl) * 64) : zoff;
             const float av = valid ? a : 0.f;
             // corner weights associated as msda_fused_fast_kernel's
             const float w0 = (h0 && c0) ? hh * hw * av : 0.f, w1 = (h0 && c1) ? hh * lw * av : 0.f;
@@ -919,8 +929,10 @@ __device__ __forceinline__ void enc_lds_tiles(const FastLevels& lv, const EncSta
         const int qo = qi;   // phase 2's query of this lane is phase 1's
         const unsigned cb = (unsigned)(lane & 3) * 16u;
         const int cq = lane & 3;
+        // ACC16: one f32 sum (the level sums are added in a fixed order); otherwise the
+        // fine-level and the LDS-level taps accumulate in two f32 sums
         f32x2 accg[4] = {}, accl[4] = {};
-        uint32_t hg[4] = {0u, 0u, 0u, 0u}, hl16[4] = {0u, 0u, 0u, 0u};
+        uint32_t hg[4], hl16[4];
         constexpr int NMAX = NG > NL ? NG : NL;
         const char* vm = reinterpret_cast<const char*>(vmap) + cb;
         auto issue = [&](int s, u32x4v (&v)[4], uint4& rg) {
@@ -931,47 +943,70 @@ __device__ __forceinline__ void enc_lds_tiles(const FastLevels& lv, const EncSta
             v[2] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, a1, 0, 0));
             v[3] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, a1 + 64u, 0, 0));
         };
-        auto consume = [&](int s, const u32x4v (&v)[4], const uint4& rg) {
+        // POS: the sample's point index within its level (0 starts the level's f16 sum with a
+        // multiply, P - 1 adds it into f32)
+        auto mac = [&](auto pos, uint32_t (&h)[4], f32x2 (&acc)[4], const u32x4v (&v)[4], uint32_t w01,
+                       uint32_t w23) {
+            constexpr int POS = decltype(pos)::value;
             if constexpr (ACC16) {
-                mac_sample16(hg, v, rg.z, rg.w);
-                if ((s + 1) % P == 0) flush16(accg, hg);
+                if constexpr (POS == 0) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) h[j] = pk_mul_wlo(v[0][j], w01);
+                    mac_sample16_tail(h, v, w01, w23);
+                } else {
+                    mac_sample16(h, v, w01, w23);
+                }
+                if constexpr (POS == P - 1) flush16(accg, h);
             } else {
-                mac_sample<T>(accg, v, rg.z, rg.w);
+                mac_sample<T>(acc, v, w01, w23);
             }
         };
-        auto lds_sample = [&](int s) {
+        auto lds_sample = [&](auto pos, int s) {
             const uint4 rl = wrec[s * QT + (qo ^ s)];
             u32x4v vl[4];
             vl[0] = *reinterpret_cast<const u32x4v*>(vm + rl.x);
             vl[1] = *reinterpret_cast<const u32x4v*>(vm + rl.x + 64);
             vl[2] = *reinterpret_cast<const u32x4v*>(vm + rl.y);
             vl[3] = *reinterpret_cast<const u32x4v*>(vm + rl.y + 64);
-            if constexpr (ACC16) {
-                mac_sample16(hl16, vl, rl.z, rl.w);
-                if ((s + 1) % P == 0) flush16(accg, hl16);   // one f32 sum: fixed flush order
-            } else {
-                mac_sample<T>(accl, vl, rl.z, rl.w);
-            }
+            mac(pos, hl16, accl, vl, rl.z, rl.w);
         };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
         u32x4v va[4], vb[4];
         uint4 rca, rcb;
         if constexpr (NG > 0) issue(0, va, rca);
-        // steps kept rolled: unrolled, the compiler hoists later gathers and spills
+        // one level of each stream per step (P = 4 samples), steps kept rolled: unrolled, the
+        // compiler hoists later gathers and spills
+        static_assert(P == 4 && NG % P == 0 && NL % P == 0, "levels of 4 points");
 #pragma unroll 1
-        for (int k = 0; k < NMAX; k += 2) {
+        for (int k = 0; k < NMAX; k += 4) {
             if (k + 1 < NG) issue(k + 1, vb, rcb);
-            if (k < NL) lds_sample(NG + k);
-            if (k < NG) consume(k, va, rca);
+            if (k < NL) lds_sample(I0{}, NG + k);
+            if (k < NG) mac(I0{}, hg, accg, va, rca.z, rca.w);
             if (k + 2 < NG) issue(k + 2, va, rca);
-            if (k + 1 < NL) lds_sample(NG + k + 1);
-            if (k + 1 < NG) consume(k + 1, vb, rcb);
+            if (k + 1 < NL) lds_sample(I1{}, NG + k + 1);
+            if (k + 1 < NG) mac(I1{}, hg, accg, vb, rcb.z, rcb.w);
+            __builtin_amdgcn_sched_barrier(0);   // keep the halves apart (register pressure)
+            if (k + 3 < NG) issue(k + 3, vb, rcb);
+            if (k + 2 < NL) lds_sample(I2{}, NG + k + 2);
+            if (k + 2 < NG) mac(I2{}, hg, accg, va, rca.z, rca.w);
+            if (k + 4 < NG) issue(k + 4, va, rca);
+            if (k + 3 < NL) lds_sample(I3{}, NG + k + 3);
+            if (k + 3 < NG) mac(I3{}, hg, accg, vb, rcb.z, rcb.w);
         }
         if (q < Lq) {
             VecT<TO, 8> o;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                o.v[2 * j] = Cvt<TO>::from(accg[j][0] + accl[j][0]);
-                o.v[2 * j + 1] = Cvt<TO>::from(accg[j][1] + accl[j][1]);
+                if constexpr (ACC16) {
+                    o.v[2 * j] = Cvt<TO>::from(accg[j][0]);
+                    o.v[2 * j + 1] = Cvt<TO>::from(accg[j][1]);
+                } else {
+                    o.v[2 * j] = Cvt<TO>::from(accg[j][0] + accl[j][0]);
+                    o.v[2 * j + 1] = Cvt<TO>::from(accg[j][1] + accl[j][1]);
+                }
             }
             *reinterpret_cast<VecT<TO, 8>*>(out + ((long)b * Lq + q) * M * D + (long)m * D + cq * 8) = o;
         }
@@ -1051,7 +1086,6 @@ __global__ __launch_bounds__(kEncWaves * 64) void msda_enc_lds_kernel(
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)hmap, (short)0, head_bytes, 0x00020000);
     const int ntile = (Lq + QT - 1) / QT;
-    const int tb = (int)((long)ntile * chunk / nchunk), te = (int)((long)ntile * (chunk + 1) / nchunk);
     uint4* wrec = rec + wave * (QT * LP);
     const int ldn = ld_off * (int)sizeof(TL);
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)offlog, (short)0, B * Lq * ldn, 0x00020000);
@@ -1061,7 +1095,7 @@ __global__ __launch_bounds__(kEncWaves * 64) void msda_enc_lds_kernel(
         __builtin_amdgcn_make_buffer_rsrc((void*)qmask, (short)0, qmask ? B * Lq : 0, 0x00020000);
 #define ENC_TILES(LCV, RD)                                                                                     \
     enc_lds_tiles<T, TO, TL, LCV, ACC16, RD>(lv, st, vmap, wrec, rv, ro, ld_off, rr, rq, out, b, m, M, Lq,       \
-                                             torder, tb, te, wave, lane)
+                                             torder, chunk, nchunk, ntile, wave, lane)
 #define ENC_LC(RD)                               \
     switch (st.lc) {                             \
         case 0: ENC_TILES(0, RD); break;         \
@@ -1441,10 +1475,15 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
                 // one workgroup per CU, enough query chunks per (frame, head) map to give
                 // every CU one workgroup
                 if (L == 4 && loc_out == nullptr && Lq >= kEncMinQueries && vss == 32 && !(msda_flags & 32) &&
-                    (long long)N * Lq * ld_off * (long long)sizeof(TL) < (1LL << 31) &&
+                    (long long)N * Lq * ld_off * (long long)sizeof(TL) < (1LL << 31) && (long long)N * Lq < (1LL << 24) &&
                     (long long)N * Lq * L * ref_dim * 4LL < (1LL << 31)) {
                     const int maps = N * M;
-                    int nchunk = (256 + maps - 1) / maps;
+                    // two rounds of one-per-CU workgroups: half as many head maps in flight
+                    // per XCD, whose fine-level rows then stay in its L2 (config 2, batch 16:
+                    // HBM fetch 0.88 -> 0.65 GB per call = the compulsory bytes); flag 128
+                    // keeps one round
+                    int nchunk = 2 * ((256 + maps - 1) / maps);
+                    if (msda_flags & 128) nchunk /= 2;
                     nchunk = std::max(1, std::min(nchunk, ntile / kEncWaves));
                     KINET_CHECK_ARG((long long)maps * nchunk < (1LL << 31), "msda fused: grid too large");
                     if (msda_flags & 64)
