@@ -1,0 +1,59 @@
+"""Per-launch table of one config-2 inference forward (bench.py's model and input), aggregated
+by (kernel entry point, shape): launches, average us, achieved TFLOP/s and GB/s from the
+algorithmic flops / bytes each launch reports, sorted by total time.  HIP events around every
+launch on one stream (kinet_amd._native.trace_begin / trace_end).
+
+usage: python tools/launch_table.py [--batch 16] [--top 40]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import bench  # noqa: E402
+from kinet_amd import _native  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=16)
+    ap.add_argument('--top', type=int, default=40)
+    a = ap.parse_args()
+    wl = bench.WORKLOADS['config2']
+    dev = torch.device('cuda', 0)
+    dt = {'bf16': torch.bfloat16, 'f16': torch.float16, 'f32': torch.float32}[wl['dtype']]
+    model = bench.build(dev, dt, wl)
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(a.batch, 3, wl['h'], wl['w'], device=dev, generator=g)
+    with torch.no_grad():
+        for _ in range(2):
+            model(list(x))
+    torch.cuda.synchronize()
+    _native.trace_begin()
+    with torch.no_grad():
+        model(list(x))
+    trace = _native.trace_end()
+    torch.cuda.synchronize()
+    agg = {}
+    tot = 0.0
+    for name, work, s, e in trace:
+        ms = s.elapsed_time(e)
+        tot += ms
+        key = (name, str(work.get('shape', '')))
+        r = agg.setdefault(key, [0, 0.0, 0.0, 0.0])
+        r[0] += 1
+        r[1] += ms
+        r[2] += work.get('flops', 0.0)
+        r[3] += work.get('bytes', 0.0)
+    print(f'total traced device time {tot:.3f} ms over {len(trace)} launches (batch {a.batch})')
+    for (name, shape), (n, ms, fl, by) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
+        t = ms * 1e-3
+        print(f'{ms / tot * 100:5.1f}% {n:3d} x {ms / n * 1e3:8.1f} us  {fl / t / 1e12 if t else 0:7.1f} TF/s '
+              f'{by / t / 1e9 if t else 0:7.0f} GB/s  {name} {shape}')
+
+
+if __name__ == '__main__':
+    main()
