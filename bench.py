@@ -71,6 +71,8 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=20.0, help='bound on the CPU baseline sample')
     ap.add_argument('--gemm-flags', type=int, default=0,
                     help='diagnostic kernel-selection flags (kinet_gemm_set_flags, csrc/gemm.hip) for A/B runs')
+    ap.add_argument('--msda-flags', type=int, default=0,
+                    help='diagnostic kernel-selection flags (kinet_msda_set_flags, csrc/msda.hip) for A/B runs')
     a = ap.parse_args()
     wl = WORKLOADS[a.workload]
     for k, wk in (('batch', 'batch'), ('streams', 'streams'), ('height', 'h'), ('width', 'w'), ('dtype', 'dtype')):
@@ -248,6 +250,8 @@ def main():
     from kinet_amd.models import nested_tensor_from_tensor_list
     if a.gemm_flags:
         _native.lib().kinet_gemm_set_flags(a.gemm_flags)
+    if a.msda_flags:
+        _native.lib().kinet_msda_set_flags(a.msda_flags)
     model = build(dev, dtype, wl)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     # one independent batch per in-flight slot (distinct requests, all resident in HBM)

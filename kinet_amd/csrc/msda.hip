@@ -36,9 +36,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxLevels = 16;
 
-// diagnostic flags (kinet_msda_set_flags): bit 0 = never use msda_fused_fast_kernel; bit 1 = its
-// 4-head x 4-sample-group variant, bit 2 = 4 heads x 2 (the default is 2 heads x 2; timing studies);
-// bit 5 = never use msda_enc_lds_kernel (encoder calls then take msda_fused_fast_kernel); bit 6 =
+// diagnostic flags (kinet_msda_set_flags): bit 0 = never use msda_fused_fast_kernel; bit 5 = never use msda_enc_lds_kernel (encoder calls then take msda_fused_fast_kernel); bit 6 =
 // msda_enc_lds_kernel with every tap product accumulated in f32 (no f16 per-level partial sums);
 // bit 7 = half as many query chunks per head map (one round of workgroups; timing studies)
 int msda_flags = 0;
@@ -1500,24 +1498,14 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
                 }
             }
             if (enc_lds) {
-            } else if (L == 4 && !(msda_flags & 6)) {
+            } else if (L == 4) {
                 // 2 heads (waves) per workgroup, 2 samples per gather group: 12.5 KiB LDS and
                 // 52 VGPRs, 12 workgroups per CU (encoder call 271 -> 258 us vs 4 heads x 4)
                 dim3 g2((Lq + 15) / 16, N, (M + 1) / 2);
                 hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 4, 4, 2, 2>), g2, dim3(128), 0, stream,
                                    (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v,
                                    ld_off, ref, ref_dim, qmask, loc_out, attw_out, (TO*)out, S, M, Lq, torder);
-            } else if (L == 4 && (msda_flags & 4)) {
-                dim3 g2((Lq + 15) / 16, N, (M + 3) / 4);
-                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 4, 4, 4, 2>), g2, dim3(256), 0, stream,
-                                   (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v,
-                                   ld_off, ref, ref_dim, qmask, loc_out, attw_out, (TO*)out, S, M, Lq, torder);
-            } else if (L == 4)
-                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 4, 4>), grid, dim3(kThreads), 0, stream,
-                                   (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v, ld_off,
-                                   ref, ref_dim, qmask, loc_out,
-                                   attw_out, (TO*)out, S, M, Lq, torder);
-            else
+            } else
                 hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 8, 4>), grid, dim3(kThreads), 0, stream,
                                    (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v, ld_off,
                                    ref, ref_dim, qmask, loc_out,

@@ -21,7 +21,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=16)
     ap.add_argument('--top', type=int, default=40)
+    ap.add_argument('--gemm-flags', type=int, default=0, help='kinet_gemm_set_flags value (A/B runs)')
+    ap.add_argument('--filter', default='', help='only rows whose shape contains this text')
     a = ap.parse_args()
+    if a.gemm_flags:
+        _native.lib().kinet_gemm_set_flags(a.gemm_flags)
     wl = bench.WORKLOADS['config2']
     dev = torch.device('cuda', 0)
     dt = {'bf16': torch.bfloat16, 'f16': torch.float16, 'f32': torch.float32}[wl['dtype']]
@@ -49,7 +53,8 @@ def main():
         r[2] += work.get('flops', 0.0)
         r[3] += work.get('bytes', 0.0)
     print(f'total traced device time {tot:.3f} ms over {len(trace)} launches (batch {a.batch})')
-    for (name, shape), (n, ms, fl, by) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
+    rows = [kv for kv in sorted(agg.items(), key=lambda kv: -kv[1][1]) if a.filter in kv[0][1]]
+    for (name, shape), (n, ms, fl, by) in rows[:a.top]:
         t = ms * 1e-3
         print(f'{ms / tot * 100:5.1f}% {n:3d} x {ms / n * 1e3:8.1f} us  {fl / t / 1e12 if t else 0:7.1f} TF/s '
               f'{by / t / 1e9 if t else 0:7.0f} GB/s  {name} {shape}')
