@@ -38,7 +38,7 @@ constexpr int kMaxLevels = 16;
 
 // diagnostic flags (kinet_msda_set_flags): bit 0 = never use msda_fused_fast_kernel; bit 5 = never use msda_enc_lds_kernel (encoder calls then take msda_fused_fast_kernel); bit 6 =
 // msda_enc_lds_kernel with every tap product accumulated in f32 (no f16 per-level partial sums);
-// bit 7 = half as many query chunks per head map (one round of workgroups; timing studies)
+// bit 7 = twice as many query chunks per head map (two rounds of workgroups; timing studies)
 int msda_flags = 0;
 
 struct LevelInfo {
@@ -1476,12 +1476,13 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
                     (long long)N * Lq * ld_off * (long long)sizeof(TL) < (1LL << 31) && (long long)N * Lq < (1LL << 24) &&
                     (long long)N * Lq * L * ref_dim * 4LL < (1LL << 31)) {
                     const int maps = N * M;
-                    // two rounds of one-per-CU workgroups: half as many head maps in flight
-                    // per XCD, whose fine-level rows then stay in its L2 (config 2, batch 16:
-                    // HBM fetch 0.88 -> 0.65 GB per call = the compulsory bytes); flag 128
-                    // keeps one round
-                    int nchunk = 2 * ((256 + maps - 1) / maps);
-                    if (msda_flags & 128) nchunk /= 2;
+                    // one round of one-per-CU workgroups.  Flag 128: two rounds, half as many
+                    // head maps in flight per XCD, whose fine-level rows then stay in its L2
+                    // (config 2, batch 16, alone: HBM fetch 0.88 -> 0.65 GB per call = the
+                    // compulsory bytes, 354 -> 351 us), but under the bench's 3-stream
+                    // concurrency its second round waits for whole CUs (rocprof: 402 vs 346 us)
+                    int nchunk = (256 + maps - 1) / maps;
+                    if (msda_flags & 128) nchunk *= 2;
                     nchunk = std::max(1, std::min(nchunk, ntile / kEncWaves));
                     KINET_CHECK_ARG((long long)maps * nchunk < (1LL << 31), "msda fused: grid too large");
                     if (msda_flags & 64)
