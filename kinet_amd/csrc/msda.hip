@@ -1481,7 +1481,18 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
                     // (config 2, batch 16, alone: HBM fetch 0.88 -> 0.65 GB per call = the
                     // compulsory bytes, 354 -> 351 us), but under the bench's 3-stream
                     // concurrency its second round waits for whole CUs (rocprof: 402 vs 346 us)
-                    int nchunk = (256 + maps - 1) / maps;
+                    // (the fewest chunks whose workgroups fill >= 90 % of their last round: at
+                    // batch 24, 192 maps x 2 = 1.5 rounds took 628 us for 1.5x the work of
+                    // batch 16's 342)
+                    const int base = (256 + maps - 1) / maps;
+                    int nchunk = base;
+                    for (int c = base; c <= 4 * base; ++c) {
+                        const long long wgs = (long long)maps * c, rounds = (wgs + 255) / 256;
+                        if (wgs * 10 >= rounds * 256 * 9) {
+                            nchunk = c;
+                            break;
+                        }
+                    }
                     if (msda_flags & 128) nchunk *= 2;
                     nchunk = std::max(1, std::min(nchunk, ntile / kEncWaves));
                     KINET_CHECK_ARG((long long)maps * nchunk < (1LL << 31), "msda fused: grid too large");
