@@ -17,7 +17,10 @@ tracking forward per frame with the previous frame's features (resident in HBM, 
 online tracker holds them) -- the HBM-stress case for MSDeformAttn (S = 43,110 per frame).
 
 Multi-GPU: frames are independent -> one replica per GPU, no data-path collective
-("scaling": "weak"); a barrier + max-over-ranks wall time brackets the timed region.
+("scaling": "weak"); a barrier + max-over-ranks wall time brackets the timed region.  The
+config-4 `train` sub-object runs its DDP step (RCCL gradient all-reduce) over the same ranks.
+`--gpus N` alone (no WORLD_SIZE from a launcher) starts N rank processes itself before any GPU
+call; n_gpus is the process group's size.
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -73,6 +76,8 @@ def parse():
                     help='diagnostic kernel-selection flags (kinet_gemm_set_flags, csrc/gemm.hip) for A/B runs')
     ap.add_argument('--msda-flags', type=int, default=0,
                     help='diagnostic kernel-selection flags (kinet_msda_set_flags, csrc/msda.hip) for A/B runs')
+    ap.add_argument('--cpu-stub', action='store_true',
+                    help='tests only: run the launch/timing skeleton with a tiny CPU model over gloo')
     a = ap.parse_args()
     wl = WORKLOADS[a.workload]
     for k, wk in (('batch', 'batch'), ('streams', 'streams'), ('height', 'h'), ('width', 'w'), ('dtype', 'dtype')):
@@ -81,16 +86,91 @@ def parse():
     return a
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`--gpus N` without an external launcher (no WORLD_SIZE in the environment): start N
+    worker processes of this script, one per GPU, each with RANK / LOCAL_RANK / WORLD_SIZE
+    and a 127.0.0.1 rendezvous -- as torch.distributed.run would (util/misc.py:515-538 reads
+    the same variables).  This parent has not touched the GPU (nothing before this call
+    initialises HIP) and stays alive as the children's supervisor: it waits for them, stops
+    the others when one fails (a peer blocked in a collective would otherwise hang) and
+    exits with the first non-zero status."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.2)
+    return rc
+
+
 def setup_dist(a):
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if a.cpu_stub:
+        if world > 1:
+            dist.init_process_group('gloo')
+        return world, rank, torch.device('cpu')
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        world = dist.get_world_size()   # the process group's own count, reported as n_gpus
     else:
         torch.cuda.set_device(0)
+    if world != a.gpus:
+        raise SystemExit(f'bench.py: --gpus {a.gpus} but the process group has {world} ranks')
     return world, rank, torch.device('cuda', local if world > 1 else 0)
+
+
+def stub_main(a, world, rank, dev):
+    """--cpu-stub: the launch / rendezvous / timing / reporting skeleton of main() with a
+    tiny CPU stand-in for the detector (tests only: checks that `--gpus N` yields N ranks
+    and an n_gpus = N line without a GPU)."""
+    x = torch.randn(a.batch, 64)
+    w = torch.randn(64, 64)
+    for _ in range(max(1, a.warmup)):
+        x = torch.tanh(x @ w)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        x = torch.tanh(x @ w)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        assert dist.get_world_size() == a.gpus
+    if rank == 0:
+        print(json.dumps({'metric': 'cpu stub', 'value': a.batch * a.steps * world / elapsed, 'unit': 'frames/s',
+                          'n_gpus': world, 'world_size': dist.get_world_size() if world > 1 else 1,
+                          'steps': a.steps, 'warmup': a.warmup, 'scaling': 'weak', 'stub': True}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def build(dev, dtype, wl):
@@ -243,7 +323,11 @@ def cpu_baseline(seconds):
 
 def main():
     a = parse()
+    if a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(a.gpus))
     world, rank, dev = setup_dist(a)
+    if a.cpu_stub:
+        return stub_main(a, world, rank, dev)
     dtype = {'bf16': torch.bfloat16, 'f16': torch.float16, 'f32': torch.float32}[a.dtype]
     wl = WORKLOADS[a.workload]
     from kinet_amd import _native
@@ -378,7 +462,8 @@ def main():
         roofline = msda_roof or mfma_roof
         line = {
             'metric': 'frames/sec (3x800x1333, 300 obj+track queries) at 1/2/4/8 GPUs; MSDeformAttn ms/call',
-            'value': value, 'unit': 'frames/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+            'value': value, 'unit': 'frames/s', 'n_gpus': world, 'world_size': world,
+            'steps': a.steps, 'warmup': a.warmup,
             'ms_per_step': elapsed / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': dt_name,
             'data': 'synthetic N(0,1) 3x%dx%d frames, random-init weights (reference init)' % (a.height, a.width),

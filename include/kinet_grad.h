@@ -64,14 +64,16 @@ int kinet_groupnorm_backward(const void* dy, const void* x, const float* gamma, 
                              float* dbeta, int N, int HW, int C, int groups, float eps, int dtype,
                              float* workspace, kinet_stream_t stream);
 
-/* Backward of kinet_mha_core (f32): given Q, K, V (row strides ld*), dO, writes dQ, dK, dV
- * (same layouts and strides as Q, K, V).  head_dim <= 64.  workspace:
- * kinet_mha_backward_workspace floats (the probabilities and their gradient). */
+/* Backward of kinet_mha_core / kinet_mha_core_dropout (f32): given Q, K, V (row strides ld*),
+ * dO, writes dQ, dK, dV (same layouts and strides as Q, K, V).  head_dim <= 64.  workspace:
+ * kinet_mha_backward_workspace floats (the dropped probabilities and the score gradient).
+ * dropout_p / dropout_seed: those of the forward (0 / NULL: no dropout); the keep mask is
+ * regenerated from the seed (include/kinet_ops.h kinet_dropout_mask). */
 int64_t kinet_mha_backward_workspace(int batch, int Lq, int Lk, int heads);
 int kinet_mha_backward(const float* Q, int ldq, const float* K, int ldk, const float* V, int ldv,
                        const float* dO, int ldo, float* dQ, float* dK, float* dV, int batch, int Lq, int Lk,
                        int heads, int head_dim, float scale, const uint8_t* key_mask, float* workspace,
-                       kinet_stream_t stream);
+                       float dropout_p, const int64_t* dropout_seed, kinet_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -54,6 +54,22 @@ int kinet_mha_core(const void* Q, int ldq, const void* Kt, int ldk, const void* 
                    void* O, int ldo, int batch, int Lq, int Lk, int heads, int head_dim,
                    float scale, int dtype, const uint8_t* key_mask, kinet_stream_t stream);
 
+/* kinet_mha_core with attention-probability dropout, the training form of
+ * nn.MultiheadAttention(d, heads, dropout=p) (deformable_transformer.py:345; torch applies
+ * F.dropout to the softmax output):
+ *   O[b, i, h] = sum_j softmax_j(...)[j] * Z[b, h, i, j] * V_bh[j],  Z in {0, 1/(1-p)}
+ * Z from kinet_dropout_mask's counter-based hash of (*dropout_seed, ((b*heads + h)*Lq + i)*Lk + j)
+ * (dropout_seed: a device int64, so drawing it needs no host sync).  Runs the FMA kernel. */
+int kinet_mha_core_dropout(const void* Q, int ldq, const void* Kt, int ldk, const void* V, int ldv,
+                           void* O, int ldo, int batch, int Lq, int Lk, int heads, int head_dim,
+                           float scale, int dtype, const uint8_t* key_mask, float dropout_p,
+                           const int64_t* dropout_seed, kinet_stream_t stream);
+
+/* The keep mask those kernels use: keep[idx] = 1 if element idx (0 <= idx < n) is kept at
+ * dropout probability p under *dropout_seed (tests, and callers that need the mask). */
+int kinet_dropout_mask(const int64_t* dropout_seed, int64_t n, float dropout_p, uint8_t* keep,
+                       kinet_stream_t stream);
+
 /* Diagnostic knob (no reference counterpart): 1 (default) = kinet_mha_core runs head_dim 32,
  * bf16/f16, Lk <= 384 on the MFMA kernel (attn.hip), 0 = always the FMA kernel.  Returns the
  * previous setting. */

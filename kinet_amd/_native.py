@@ -60,7 +60,9 @@ _SIGS = {
     'kinet_groupnorm_backward_workspace': [I, I, I, I],
     'kinet_groupnorm_backward': [P, P, P, P, P, P, I, I, I, I, F, I, P, P],
     'kinet_mha_backward_workspace': [I, I, I, I],
-    'kinet_mha_backward': [P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, F, P, P, P],
+    'kinet_mha_backward': [P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, F, P, P, F, P, P],
+    'kinet_mha_core_dropout': [P, I, P, I, P, I, P, I] + [I] * 5 + [F, I, P, F, P, P],
+    'kinet_dropout_mask': [P, I64, F, P, P],
     'kinet_last_error': [],
     'kinet_version': [],
 }

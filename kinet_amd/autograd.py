@@ -192,38 +192,47 @@ def conv_nhwc(x, weight, bias=None, stride=1, pad=0, scale=None, shift=None, rel
 # ---------------------------------------------------------------------------- attention
 class _MHACore(Function):
     @staticmethod
-    def forward(ctx, q, k, v, heads, scale, key_mask):
+    def forward(ctx, q, k, v, heads, scale, key_mask, dropout_p, seed):
         _f32(q)
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
-        o = K.mha_core(q, k, v, heads, scale, key_mask=key_mask)
+        o = K.mha_core(q, k, v, heads, scale, key_mask=key_mask, dropout_p=dropout_p, seed=seed)
         ctx.save_for_backward(q, k, v)
-        ctx.conf = (heads, scale, key_mask)
+        ctx.conf = (heads, scale, key_mask, dropout_p, seed)
         return o
 
     @staticmethod
     @once_differentiable
     def backward(ctx, do):
         q, k, v = ctx.saved_tensors
-        heads, scale, key_mask = ctx.conf
-        dq, dk, dv = K.mha_backward(q, k, v, do.contiguous().float(), heads, scale, key_mask)
-        return dq, dk, dv, None, None, None
+        heads, scale, key_mask, dropout_p, seed = ctx.conf
+        dq, dk, dv = K.mha_backward(q, k, v, do.contiguous().float(), heads, scale, key_mask, dropout_p, seed)
+        return dq, dk, dv, None, None, None, None, None
 
 
-def mha_core(q, k, v, heads, scale, key_mask=None):
-    """softmax(q k^T * scale, -inf at masked keys) v per head; q (B, Lq, E), k/v (B, Lk, E)."""
-    return _MHACore.apply(q, k, v, heads, scale, key_mask)
+def mha_core(q, k, v, heads, scale, key_mask=None, dropout_p=0.0, seed=None):
+    """softmax(q k^T * scale, -inf at masked keys) v per head; q (B, Lq, E), k/v (B, Lk, E).
+    dropout_p > 0: the probabilities are dropped (and the survivors scaled by 1/(1-p)) with
+    the keep mask of the device int64 `seed` (kernels.dropout_seed when None), regenerated
+    by the backward."""
+    if dropout_p > 0 and seed is None:
+        seed = K.dropout_seed(q.device)
+    return _MHACore.apply(q, k, v, heads, scale, key_mask, float(dropout_p), seed)
 
 
 def multihead_attention(mod, query, key, value, key_padding_mask=None):
     """nn.MultiheadAttention(query, key, value, key_padding_mask)[0] for batch-first inputs
     (the decoder self-attention, deformable_transformer.py:371, transposes to (L, B, E) and
     back around the call): in_proj split q|k|v (torch's packed in_proj_weight layout),
-    attention core, out_proj.  Attention-probability dropout is not applied (the configured
-    training runs use it only through nn.MultiheadAttention's `dropout`)."""
+    attention core, out_proj.  In training mode the attention probabilities are dropped with
+    the module's `dropout` probability (nn.MultiheadAttention(d, heads, dropout=p),
+    deformable_transformer.py:345), in the HIP core; the mask comes from torch's CUDA
+    generator state through a device seed, so it is not torch's own mask (parity by mask
+    statistics and by gradients under a fixed mask, tests/test_autograd_gpu.py)."""
     E = mod.embed_dim
     w, b = mod.in_proj_weight, mod.in_proj_bias
     q = linear(query, w[:E], b[:E])
     k = linear(key, w[E:2 * E], b[E:2 * E])
     v = linear(value, w[2 * E:], b[2 * E:])
-    o = mha_core(q, k, v, mod.num_heads, mod.head_dim ** -0.5, key_padding_mask)
+    p = mod.dropout if mod.training else 0.0
+    o = mha_core(q, k, v, mod.num_heads, mod.head_dim ** -0.5, key_padding_mask, dropout_p=p)
     return linear(o, mod.out_proj.weight, mod.out_proj.bias)

@@ -20,13 +20,27 @@ import argparse
 import torch
 
 
-def load_checkpoint(path, map_location='cpu'):
-    """The checkpoint dict ('model', and optionally 'optimizer', 'lr_scheduler', 'epoch', 'args')."""
+def _safe_globals():
+    """The non-tensor types a reference checkpoint holds (train.py:322-330): the argparse
+    `args`, and numpy scalars in `best_val_stats` (MOTA / IDF1 from the motmetrics summary,
+    engine.py:343) -- numpy.float64 etc. pickle as numpy's `scalar` reconstructor plus a dtype
+    object of one of numpy's DType classes.  Data-only reconstructors, no code."""
+    import numpy as np
     try:
-        torch.serialization.add_safe_globals([argparse.Namespace])
-    except AttributeError:   # pragma: no cover (older torch)
-        pass
-    return torch.load(path, map_location=map_location, weights_only=True)
+        from numpy._core.multiarray import scalar
+    except ImportError:   # pragma: no cover (numpy < 2)
+        from numpy.core.multiarray import scalar
+    dts = {type(np.dtype(t)) for t in (np.float16, np.float32, np.float64, np.int8, np.int16, np.int32, np.int64,
+                                       np.uint8, np.uint16, np.uint32, np.uint64, np.bool_)}
+    return [argparse.Namespace, scalar, np.dtype] + sorted(dts, key=lambda c: c.__name__)
+
+
+def load_checkpoint(path, map_location='cpu'):
+    """The checkpoint dict ('model', and optionally 'optimizer', 'lr_scheduler', 'epoch',
+    'args', 'vis_win_names', 'best_val_stats').  weights_only=True with a scoped allow-list
+    (torch.serialization.safe_globals, not the process-wide registry)."""
+    with torch.serialization.safe_globals(_safe_globals()):
+        return torch.load(path, map_location=map_location, weights_only=True)
 
 
 def strip_detr_prefix(state_dict):

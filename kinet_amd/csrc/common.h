@@ -118,4 +118,22 @@ __device__ __forceinline__ float group_reduce(float x) {
 // number of workgroups that fill the chip for a grid-stride kernel (256 CUs x 8)
 constexpr int kMaxGridStride = 2048;
 
+// Attention-probability dropout (nn.MultiheadAttention(dropout=p), deformable_transformer.py:345;
+// torch applies F.dropout to the softmax output): the keep decision of element
+// idx = ((b*H + h)*Lq + i)*Lk + j is a counter-based hash of (seed, idx) -- the splitmix64
+// finaliser, its top 24 bits the uniform draw u; kept iff u >= thresh, thresh = round(p * 2^24),
+// kept values scaled by 1 / (1 - p).  Forward, backward and kinet_dropout_mask regenerate the
+// same mask from the same seed (a device int64 drawn from torch's CUDA generator).
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+    uint64_t z = seed + idx * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (uint32_t)(z >> 40) >= thresh;
+}
+inline uint32_t dropout_thresh(float p) {
+    const double t = (double)p * 16777216.0 + 0.5;
+    return t >= 16777216.0 ? 16777216u : (t <= 0.0 ? 0u : (uint32_t)t);
+}
+
 }  // namespace kinet

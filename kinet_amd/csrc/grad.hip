@@ -622,8 +622,9 @@ __global__ __launch_bounds__(256) void gn_bwd_param_kernel(const float* __restri
 }
 
 // ------------------------------------------------------------------------- attention bwd
-// pass 1: one wave per (b, h, query i): P_ij, dS_ij = P_ij (dO_i.V_j - sum_j P_ij dO_i.V_j)
-// stored to ws, dQ_i = scale * sum_j dS_ij K_j
+// With dropout (scaled keep mask Z): O_i = sum_j P_ij Z_ij V_j, so dV_j = sum_i P_ij Z_ij dO_i,
+// dP_ij = Z_ij dO_i.V_j, di = dO_i.O_i = sum_j P_ij dP_ij, dS_ij = P_ij (dP_ij - di); the
+// workspace keeps P_ij Z_ij (for dV) and dS_ij (for dK).
 struct AttnArgs {
     const float *Q, *K, *V, *dO;
     float *dQ, *dK, *dV, *P, *dS;
@@ -631,123 +632,15 @@ struct AttnArgs {
     int ldq, ldk, ldv, ldo;   // row strides (elements); dQ/dK/dV use ldq/ldk/ldv
     int B, Lq, Lk, H, D;
     float scale;
+    const int64_t* dseed;     // attention-probability dropout (nullptr: none), common.h dropout_keep
+    uint32_t dthresh;
+    float dscale;
 };
 
 constexpr int ATT_MAXD = 64;
 
-// MD: compile-time bound on head_dim (32 or 64) so the per-lane vectors stay in registers
-template <int MD>
-__global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int i = blockIdx.x * 4 + wave;
-    const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-    if (i >= a.Lq) return;
-    const float* q = a.Q + ((long)b * a.Lq + i) * a.ldq + h * a.D;
-    const float* dO = a.dO + ((long)b * a.Lq + i) * a.ldo + h * a.D;
-    float* Prow = a.P + ((long)bh * a.Lq + i) * a.Lk;
-    float* Srow = a.dS + ((long)bh * a.Lq + i) * a.Lk;
-    float qv[MD], ov[MD];
-#pragma unroll
-    for (int d = 0; d < MD; ++d) {
-        qv[d] = d < a.D ? q[d] : 0.f;
-        ov[d] = d < a.D ? dO[d] : 0.f;
-    }
-    // scores and softmax (lanes over keys)
-    float mx = -INFINITY;
-    for (int j = lane; j < a.Lk; j += 64) {
-        const float* k = a.K + ((long)b * a.Lk + j) * a.ldk + h * a.D;
-        float s = 0.f;
-        #pragma unroll
-        for (int d = 0; d < MD; ++d)
-            if (d < a.D) s += qv[d] * k[d];
-        s *= a.scale;
-        if (a.key_mask && a.key_mask[(long)b * a.Lk + j]) s = -INFINITY;
-        Prow[j] = s;
-        mx = fmaxf(mx, s);
-    }
-    for (int o = 32; o; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    float sum = 0.f;
-    for (int j = lane; j < a.Lk; j += 64) {
-        const float e = mx == -INFINITY ? 0.f : __expf(Prow[j] - mx);
-        Prow[j] = e;
-        sum += e;
-    }
-    for (int o = 32; o; o >>= 1) sum += __shfl_xor(sum, o);
-    const float rs = sum > 0.f ? 1.f / sum : 0.f;
-    float di = 0.f;
-    for (int j = lane; j < a.Lk; j += 64) {
-        const float p = Prow[j] * rs;
-        Prow[j] = p;
-        const float* v = a.V + ((long)b * a.Lk + j) * a.ldv + h * a.D;
-        float dp = 0.f;
-        #pragma unroll
-        for (int d = 0; d < MD; ++d)
-            if (d < a.D) dp += ov[d] * v[d];
-        Srow[j] = dp;
-        di += p * dp;
-    }
-    for (int o = 32; o; o >>= 1) di += __shfl_xor(di, o);
-    float dq[MD];
-#pragma unroll
-    for (int d = 0; d < MD; ++d) dq[d] = 0.f;
-    for (int j = lane; j < a.Lk; j += 64) {
-        const float ds = Prow[j] * (Srow[j] - di);
-        Srow[j] = ds;
-        const float* k = a.K + ((long)b * a.Lk + j) * a.ldk + h * a.D;
-        #pragma unroll
-        for (int d = 0; d < MD; ++d)
-            if (d < a.D) dq[d] += ds * k[d];
-    }
-    float* dqo = a.dQ + ((long)b * a.Lq + i) * a.ldq + h * a.D;
-#pragma unroll
-    for (int d = 0; d < MD; ++d) {
-        float v = dq[d];
-        for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
-        if (lane == 0 && d < a.D) dqo[d] = v * a.scale;
-    }
-}
-
-// pass 2: one wave per (b, h, key j): dK_j = scale * sum_i dS_ij Q_i, dV_j = sum_i P_ij dO_i
-template <int MD>
-__global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int j = blockIdx.x * 4 + wave;
-    const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-    if (j >= a.Lk) return;
-    float dk[MD], dv[MD];
-#pragma unroll
-    for (int d = 0; d < MD; ++d) dk[d] = dv[d] = 0.f;
-    for (int i = lane; i < a.Lq; i += 64) {
-        const float p = a.P[((long)bh * a.Lq + i) * a.Lk + j];
-        const float ds = a.dS[((long)bh * a.Lq + i) * a.Lk + j];
-        const float* q = a.Q + ((long)b * a.Lq + i) * a.ldq + h * a.D;
-        const float* dO = a.dO + ((long)b * a.Lq + i) * a.ldo + h * a.D;
-#pragma unroll
-        for (int d = 0; d < MD; ++d)
-            if (d < a.D) {
-                dk[d] += ds * q[d];
-                dv[d] += p * dO[d];
-            }
-    }
-    float* dko = a.dK + ((long)b * a.Lk + j) * a.ldk + h * a.D;
-    float* dvo = a.dV + ((long)b * a.Lk + j) * a.ldv + h * a.D;
-#pragma unroll
-    for (int d = 0; d < MD; ++d) {
-        float x = dk[d], y = dv[d];
-        for (int o = 32; o; o >>= 1) {
-            x += __shfl_xor(x, o);
-            y += __shfl_xor(y, o);
-        }
-        if (lane == 0 && d < a.D) {
-            dko[d] = x * a.scale;
-            dvo[d] = y;
-        }
-    }
-}
-
-// Tiled attention backward (default; flag 512 selects the wave-per-row kernels above).  The
-// wave-per-row kernels read every key row per query through per-lane strided loads (and every
-// P / dS column per key), ~0.9 ms per decoder self-attention at config 4.  Here a lane owns
+// Tiled attention backward.  (Wave-per-row kernels, which read every key row per query through
+// per-lane strided loads, took ~0.9 ms per decoder self-attention at config 4.)  A lane owns
 // one query (q2) or one key (kv2), the eight waves of a workgroup split the other dimension,
 // and that dimension's rows are staged in LDS in chunks of 64 and read as broadcasts.
 constexpr int AT_T = 64;
@@ -860,13 +753,19 @@ __global__ __launch_bounds__(AT_NT) void attn_bwd_q2_kernel(AttnArgs a) {
         if (st[w][lane][0] != -INFINITY) sum += st[w][lane][1] * __expf(st[w][lane][0] - mx);
     const float rs = sum > 0.f ? 1.f / sum : 0.f;
     auto prob = [&](float sc) { return (mx == -INFINITY || sc == -INFINITY) ? 0.f : __expf(sc - mx) * rs; };
-    // phase B: di = sum_j P_ij (dO_i . V_j); P stored
+    // dropout keep scale of (i, j): 1 without dropout, else 0 or 1 / (1 - p)
+    const uint64_t dseed = a.dseed ? (uint64_t)*a.dseed : 0ull;
+    const uint64_t drow = ((uint64_t)bh * a.Lq + (uint64_t)(iv ? i : 0)) * (uint64_t)a.Lk;
+    auto zf = [&](int j) {
+        return a.dseed ? (dropout_keep(dseed, drow + (uint64_t)j, a.dthresh) ? a.dscale : 0.f) : 1.f;
+    };
+    // phase B: di = sum_j P_ij Z_ij (dO_i . V_j); P Z stored
     float di = 0.f;
     chunks(true, [&](int j0) {
         for (int r = r0; r < r0 + AT_T / AT_NW && j0 + r < a.Lk; ++r) {
-            const float p = prob(score(r, j0 + r));
-            di += p * dot_lds<MD>(ov, Vs[r]);
-            if (iv) Prow[j0 + r] = p;
+            const float pz = prob(score(r, j0 + r)) * zf(j0 + r);
+            di += pz * dot_lds<MD>(ov, Vs[r]);
+            if (iv) Prow[j0 + r] = pz;
         }
     });
     __syncthreads();
@@ -882,7 +781,7 @@ __global__ __launch_bounds__(AT_NT) void attn_bwd_q2_kernel(AttnArgs a) {
     chunks(true, [&](int j0) {
         for (int r = r0; r < r0 + AT_T / AT_NW && j0 + r < a.Lk; ++r) {
             const float p = prob(score(r, j0 + r));
-            const float ds = p * (dot_lds<MD>(ov, Vs[r]) - di);
+            const float ds = p * (zf(j0 + r) * dot_lds<MD>(ov, Vs[r]) - di);
             if (iv) Srow[j0 + r] = ds;
 #pragma unroll
             for (int d = 0; d < MD; d += 4) {
@@ -1206,34 +1105,28 @@ extern "C" int64_t kinet_mha_backward_workspace(int batch, int Lq, int Lk, int h
 extern "C" int kinet_mha_backward(const float* Q, int ldq, const float* K, int ldk, const float* V, int ldv,
                                   const float* dO, int ldo, float* dQ, float* dK, float* dV, int batch, int Lq, int Lk,
                                   int heads, int head_dim, float scale, const uint8_t* key_mask, float* workspace,
-                                  kinet_stream_t stream) {
+                                  float dropout_p, const int64_t* dropout_seed, kinet_stream_t stream) {
     KINET_CHECK_ARG(head_dim > 0 && head_dim <= ATT_MAXD && workspace, "mha_backward: head_dim %d (<= %d) / workspace",
                     head_dim, ATT_MAXD);
+    KINET_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || dropout_seed),
+                    "mha_backward: dropout p %g must be in [0, 1) with a seed", (double)dropout_p);
     if (batch == 0 || Lq == 0 || Lk == 0) return KINET_OK;
+    const bool drop = dropout_p > 0.f;
     AttnArgs a{Q, K, V, dO, dQ, dK, dV, workspace, workspace + (long)batch * heads * Lq * Lk, key_mask,
-               ldq, ldk, ldv, ldo, batch, Lq, Lk, heads, head_dim, scale};
+               ldq, ldk, ldv, ldo, batch, Lq, Lk, heads, head_dim, scale, drop ? dropout_seed : nullptr,
+               dropout_thresh(dropout_p), drop ? 1.f / (1.f - dropout_p) : 1.f};
     hipStream_t s = (hipStream_t)stream;
-    if (!(kinet_gemm_flags & 512)) {
-        const dim3 gq((Lq + AT_T - 1) / AT_T, batch * heads), gk((Lk + AT_T - 1) / AT_T, batch * heads);
+    const dim3 gq((Lq + AT_T - 1) / AT_T, batch * heads), gk((Lk + AT_T - 1) / AT_T, batch * heads);
 #define AT2(MD_)                                                                  \
     do {                                                                          \
         hipLaunchKernelGGL(attn_bwd_q2_kernel<MD_>, gq, dim3(64 * at_nw<MD_>()), 0, s, a);      \
         KINET_LAUNCH_CHECK();                                                     \
         hipLaunchKernelGGL(attn_bwd_kv2_kernel<MD_>, gk, dim3(64 * at_nw<MD_>()), 0, s, a);     \
     } while (0)
-        if (head_dim <= 32) AT2(32);
-        else if (head_dim <= 36) AT2(36);
-        else AT2(64);
+    if (head_dim <= 32) AT2(32);
+    else if (head_dim <= 36) AT2(36);
+    else AT2(64);
 #undef AT2
-    } else if (head_dim <= 32) {
-        hipLaunchKernelGGL(attn_bwd_q_kernel<32>, dim3((Lq + 3) / 4, batch * heads), dim3(256), 0, s, a);
-        KINET_LAUNCH_CHECK();
-        hipLaunchKernelGGL(attn_bwd_kv_kernel<32>, dim3((Lk + 3) / 4, batch * heads), dim3(256), 0, s, a);
-    } else {
-        hipLaunchKernelGGL(attn_bwd_q_kernel<64>, dim3((Lq + 3) / 4, batch * heads), dim3(256), 0, s, a);
-        KINET_LAUNCH_CHECK();
-        hipLaunchKernelGGL(attn_bwd_kv_kernel<64>, dim3((Lk + 3) / 4, batch * heads), dim3(256), 0, s, a);
-    }
     KINET_LAUNCH_CHECK();
     return KINET_OK;
 }

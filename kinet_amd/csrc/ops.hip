@@ -411,7 +411,8 @@ template <typename T, int D>
 __global__ __launch_bounds__(256) void mha_kernel(const T* __restrict__ Q, int ldq, const T* __restrict__ Kt, int ldk,
                                                   const T* __restrict__ V, int ldv, T* __restrict__ O, int ldo,
                                                   int Lq, int Lk, int heads, float scale,
-                                                  const uint8_t* __restrict__ kmask) {
+                                                  const uint8_t* __restrict__ kmask, const int64_t* __restrict__ dseed,
+                                                  uint32_t dthresh, float dscale) {
     constexpr int KT = 64;
     constexpr int QB = 16;                // queries per block
     constexpr int DPL = D / 4;            // dims per lane
@@ -433,6 +434,10 @@ __global__ __launch_bounds__(256) void mha_kernel(const T* __restrict__ Q, int l
         o[j] = 0.f;
     }
     float mx = -INFINITY, l = 0.f;
+    // dropout (training): probabilities of dropped keys leave the numerator only; the softmax
+    // normaliser l keeps every key (F.dropout after softmax)
+    const uint64_t seed = dseed ? (uint64_t)*dseed : 0ull;
+    const uint64_t drow = (((uint64_t)b * heads + h) * (uint64_t)Lq + (uint64_t)(qok ? qi : 0)) * (uint64_t)Lk;
     for (int k0 = 0; k0 < Lk; k0 += KT) {
         __syncthreads();
         for (int i = threadIdx.x; i < KT * D; i += 256) {
@@ -464,9 +469,11 @@ __global__ __launch_bounds__(256) void mha_kernel(const T* __restrict__ Q, int l
             const float corr = __expf(mx - nm);
             const float pexp = __expf(s - nm);
             l = l * corr + pexp;
+            const float pz = dseed ? (dropout_keep(seed, drow + (uint64_t)(k0 + kk), dthresh) ? pexp * dscale : 0.f)
+                                   : pexp;
             const float* vr = &vs[kk][sub * DPL];
 #pragma unroll
-            for (int j = 0; j < DPL; ++j) o[j] = o[j] * corr + pexp * vr[j];
+            for (int j = 0; j < DPL; ++j) o[j] = o[j] * corr + pz * vr[j];
             mx = nm;
         }
     }
@@ -710,23 +717,30 @@ extern "C" int kinet_mha_set_mfma(int enable) {
     return old;
 }
 
-extern "C" int kinet_mha_core(const void* Q, int ldq, const void* Kt, int ldk, const void* V, int ldv, void* O, int ldo,
-                              int batch, int Lq, int Lk, int heads, int head_dim, float scale, int dtype,
-                              const uint8_t* key_mask, kinet_stream_t stream) {
+static int mha_core_impl(const void* Q, int ldq, const void* Kt, int ldk, const void* V, int ldv, void* O, int ldo,
+                         int batch, int Lq, int Lk, int heads, int head_dim, float scale, int dtype,
+                         const uint8_t* key_mask, float dropout_p, const int64_t* dropout_seed, kinet_stream_t stream) {
     KINET_CHECK_ARG(batch >= 0 && Lq >= 0 && Lk >= 0 && heads > 0, "mha: bad sizes");
     KINET_CHECK_ARG(head_dim == 32 || head_dim == 36 || head_dim == 16 || head_dim == 64,
                     "mha: head_dim %d not instantiated (16/32/36/64)", head_dim);
+    KINET_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || dropout_seed),
+                    "mha: dropout p %g must be in [0, 1) with a seed", (double)dropout_p);
     if (batch == 0 || Lq == 0) return KINET_OK;
     hipStream_t s = (hipStream_t)stream;
-    if (kinet::mha_use_mfma && kinet::launch_mha_mfma(Q, ldq, Kt, ldk, V, ldv, O, ldo, batch, Lq, Lk, heads, head_dim,
-                                                      scale, dtype, key_mask, s)) {
+    const bool drop = dropout_p > 0.f;
+    if (!drop && kinet::mha_use_mfma &&
+        kinet::launch_mha_mfma(Q, ldq, Kt, ldk, V, ldv, O, ldo, batch, Lq, Lk, heads, head_dim, scale, dtype, key_mask,
+                               s)) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;
     }
+    const int64_t* dseed = drop ? dropout_seed : nullptr;
+    const uint32_t dthresh = kinet::dropout_thresh(dropout_p);
+    const float dscale = drop ? 1.f / (1.f - dropout_p) : 1.f;
     dim3 grid((Lq + 15) / 16, heads, batch);
 #define MH(DD) DISPATCH_T(dtype, hipLaunchKernelGGL((mha_kernel<T, DD>), grid, dim3(256), 0, s, (const T*)Q, ldq, \
                                                    (const T*)Kt, ldk, (const T*)V, ldv, (T*)O, ldo, Lq, Lk, heads, \
-                                                   scale, key_mask))
+                                                   scale, key_mask, dseed, dthresh, dscale))
     switch (head_dim) {
         case 16: MH(16); break;
         case 32: MH(32); break;
@@ -734,6 +748,43 @@ extern "C" int kinet_mha_core(const void* Q, int ldq, const void* Kt, int ldk, c
         case 64: MH(64); break;
     }
 #undef MH
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_mha_core(const void* Q, int ldq, const void* Kt, int ldk, const void* V, int ldv, void* O, int ldo,
+                              int batch, int Lq, int Lk, int heads, int head_dim, float scale, int dtype,
+                              const uint8_t* key_mask, kinet_stream_t stream) {
+    return mha_core_impl(Q, ldq, Kt, ldk, V, ldv, O, ldo, batch, Lq, Lk, heads, head_dim, scale, dtype, key_mask, 0.f,
+                         nullptr, stream);
+}
+
+extern "C" int kinet_mha_core_dropout(const void* Q, int ldq, const void* Kt, int ldk, const void* V, int ldv, void* O,
+                                      int ldo, int batch, int Lq, int Lk, int heads, int head_dim, float scale,
+                                      int dtype, const uint8_t* key_mask, float dropout_p, const int64_t* dropout_seed,
+                                      kinet_stream_t stream) {
+    return mha_core_impl(Q, ldq, Kt, ldk, V, ldv, O, ldo, batch, Lq, Lk, heads, head_dim, scale, dtype, key_mask,
+                         dropout_p, dropout_seed, stream);
+}
+
+namespace kinet {
+namespace {
+__global__ void dropout_mask_kernel(const int64_t* __restrict__ dseed, uint8_t* __restrict__ keep, long n,
+                                    uint32_t thresh) {
+    const uint64_t seed = (uint64_t)*dseed;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        keep[i] = dropout_keep(seed, (uint64_t)i, thresh) ? 1 : 0;
+}
+}  // namespace
+}  // namespace kinet
+
+extern "C" int kinet_dropout_mask(const int64_t* dropout_seed, int64_t n, float dropout_p, uint8_t* keep,
+                                  kinet_stream_t stream) {
+    KINET_CHECK_ARG(n >= 0 && dropout_seed && dropout_p >= 0.f && dropout_p < 1.f, "dropout_mask: bad arguments");
+    if (n == 0) return KINET_OK;
+    const long blocks = std::min<long>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(kinet::dropout_mask_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dropout_seed, keep,
+                       (long)n, kinet::dropout_thresh(dropout_p));
     KINET_LAUNCH_CHECK();
     return KINET_OK;
 }
@@ -865,18 +916,26 @@ namespace kinet {
 namespace {
 constexpr int NMS_MAX = 4096;
 
-// one workgroup: rank every box by score (descending, ties by index -- a stable order), then
+// one workgroup: rank every box by score (descending, ties by index -- a stable order; NaN
+// scores rank first), then
 // walk the ranks; each kept box suppresses, in parallel, every later box with IoU > thresh
 __global__ __launch_bounds__(1024) void nms_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
                                                    uint8_t* __restrict__ keep, int n, float thresh) {
     __shared__ int order[NMS_MAX];
     __shared__ uint8_t supp[NMS_MAX];
     __shared__ int cur;
+    // scores compared as monotone integer keys: a strict total order even with NaNs (which
+    // rank first, as torch.sort(descending=True) places them), so every rank is written once
+    auto key = [](float f) -> uint32_t {
+        const uint32_t u = __float_as_uint(f);
+        if ((u & 0x7fffffffu) > 0x7f800000u) return 0xffffffffu;
+        return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    };
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const float si = scores[i];
+        const uint32_t si = key(scores[i]);
         int r = 0;
         for (int j = 0; j < n; ++j) {
-            const float sj = scores[j];
+            const uint32_t sj = key(scores[j]);
             r += (sj > si || (sj == si && j < i)) ? 1 : 0;
         }
         order[r] = i;

@@ -11,15 +11,25 @@ Contract: the callable must be a pure function of its tensor arguments for a fix
 outputs are the graph's own buffers, overwritten by the next replay.  Tensor-keyed caches
 (``kernels.cached``: padding-mask embeddings) are forced to recompute INSIDE the recording,
 so a new mask is re-embedded on every replay instead of reusing the warm-up's value.
+
+Weights: the recording holds the device pointers of the weight casts / packings that
+``kernels.cached`` built during warm-up.  ``GraphedCall`` keeps every cache entry alive for
+its lifetime (so the allocator cannot hand those buffers to anything else) and, given the
+module's parameters and buffers, snapshots their (_version, data_ptr) at record time: a
+replay after ``load_state_dict``, an optimizer step or ``set_compute_dtype`` raises instead
+of silently running the stale weights.
 """
 import torch
+
+from kinet_amd import kernels
 
 __all__ = ['GraphedCall']
 
 
 class GraphedCall:
-    def __init__(self, fn, tensors, warmup=3):
+    def __init__(self, fn, tensors, warmup=3, params=()):
         self.fn = fn
+        self.params = [p for p in params if p is not None]
         self.static = [t.detach().clone() for t in tensors]
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -32,6 +42,18 @@ class GraphedCall:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph), torch.no_grad():
             self.out = fn(*self.static)
+        self._keep = kernels.cache_values()      # the buffers the graph reads stay allocated
+        self._pver = self._param_versions()
+
+    def _param_versions(self):
+        return [(p._version, p.data_ptr(), p.dtype) for p in self.params]
+
+    def check_weights(self):
+        """RuntimeError when a parameter or buffer changed since the recording."""
+        if self._param_versions() != self._pver:
+            raise RuntimeError('GraphedCall: the module parameters changed after the recording '
+                               '(load_state_dict / optimizer step / set_compute_dtype); the graph would replay '
+                               'the old weights -- record a new GraphedCall')
 
     def __call__(self, *tensors):
         if len(tensors) != len(self.static):
@@ -41,5 +63,6 @@ class GraphedCall:
                 raise ValueError(f'GraphedCall: input {tuple(t.shape)} {t.dtype} does not match the recorded '
                                  f'{tuple(s.shape)} {s.dtype}; record another GraphedCall for this signature')
             s.copy_(t)
+        self.check_weights()
         self.graph.replay()
         return self.out

@@ -48,6 +48,11 @@ def clear_cache():
     _cache.clear()
 
 
+def cache_values():
+    """Strong references to every cached value (HIP-graph recordings keep them allocated)."""
+    return [hit[1] for ent in list(_cache.values()) for hit in ent[1].values()]
+
+
 def cached_multi(tensors, tag, make):
     """Cache make(*tensors) on the first tensor, invalidated if ANY of them changes."""
     t0 = tensors[0]
@@ -420,13 +425,28 @@ def nms(boxes, scores, iou_threshold):
         s = scores.float().contiguous()
         N.call('kinet_nms', N.ptr(b), N.ptr(s), N.ptr(keep), n, float(iou_threshold), N.stream(boxes.device))
         idx = keep.nonzero().flatten()
-        return idx[torch.argsort(-s[idx], stable=True)]
+        # descending, ties by index, NaN first: the kernel's own rank order
+        return idx[torch.sort(s[idx], descending=True, stable=True)[1]]
     return keep.nonzero().flatten()
 
 
 # --------------------------------------------------------------------------- attention
-def mha_core(q, k, v, heads, scale, key_mask=None, out=None):
-    """q (B, Lq, E) (row stride may exceed E), k/v (B, Lk, E) -> (B, Lq, E)."""
+def dropout_seed(device):
+    """A device int64 seed for the dropout kernels, drawn from torch's generator of `device`
+    (as F.dropout draws its Philox offset from it), without a host sync."""
+    return torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, device=device)
+
+
+def dropout_mask(seed, n, p):
+    """The keep mask (uint8, n elements) the dropout kernels derive from `seed` at probability p."""
+    keep = torch.empty(n, dtype=torch.uint8, device=seed.device)
+    N.call('kinet_dropout_mask', N.ptr(seed), n, float(p), N.ptr(keep), N.stream(seed.device))
+    return keep
+
+
+def mha_core(q, k, v, heads, scale, key_mask=None, out=None, dropout_p=0.0, seed=None):
+    """q (B, Lq, E) (row stride may exceed E), k/v (B, Lk, E) -> (B, Lq, E).  dropout_p > 0:
+    attention-probability dropout with the keep mask of `seed` (kinet_mha_core_dropout)."""
     B, Lq, E = q.shape
     Lk = k.shape[1]
     D = E // heads
@@ -435,6 +455,12 @@ def mha_core(q, k, v, heads, scale, key_mask=None, out=None):
             raise RuntimeError('mha_core: rows must be unit-stride with packed batches')
     o = out if out is not None else torch.empty((B, Lq, E), dtype=q.dtype, device=q.device)
     km = key_mask.to(torch.uint8).contiguous() if key_mask is not None else None
+    if dropout_p > 0:
+        N.call('kinet_mha_core_dropout', N.ptr(q), q.stride(1), N.ptr(k), k.stride(1), N.ptr(v), v.stride(1),
+               N.ptr(o), o.stride(1), B, Lq, Lk, heads, D, float(scale), N.dtype_code(q.dtype), N.ptr(km),
+               float(dropout_p), N.ptr(seed), N.stream(q.device),
+               work={'family': 'attn', 'flops': 4.0 * B * heads * Lq * Lk * D})
+        return o
     N.call('kinet_mha_core', N.ptr(q), q.stride(1), N.ptr(k), k.stride(1), N.ptr(v), v.stride(1), N.ptr(o),
            o.stride(1), B, Lq, Lk, heads, D, float(scale), N.dtype_code(q.dtype), N.ptr(km), N.stream(q.device),
            work={'family': 'attn', 'flops': 4.0 * B * heads * Lq * Lk * D})
@@ -657,7 +683,7 @@ def groupnorm_backward(dy, x, gamma, groups, eps, need_params=True):
     return dx, dg, db
 
 
-def mha_backward(q, k, v, do, heads, scale, key_mask=None):
+def mha_backward(q, k, v, do, heads, scale, key_mask=None, dropout_p=0.0, seed=None):
     """Backward of mha_core (f32): returns dq, dk, dv with the layouts of q, k, v."""
     B, Lq, E = q.shape
     Lk = k.shape[1]
@@ -674,6 +700,7 @@ def mha_backward(q, k, v, do, heads, scale, key_mask=None):
     if q.stride(1) != E or k.stride(1) != E or v.stride(1) != E:
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
     N.call('kinet_mha_backward', N.ptr(q), E, N.ptr(k), E, N.ptr(v), E, N.ptr(do.contiguous()), E, N.ptr(dq),
-           N.ptr(dk), N.ptr(dv), B, Lq, Lk, heads, E // heads, float(scale), N.ptr(km), N.ptr(ws), N.stream(q.device),
+           N.ptr(dk), N.ptr(dv), B, Lq, Lk, heads, E // heads, float(scale), N.ptr(km), N.ptr(ws), float(dropout_p),
+           N.ptr(seed) if dropout_p > 0 else None, N.stream(q.device),
            work={'family': 'attn', 'flops': 8.0 * B * heads * Lq * Lk * (E // heads)})
     return dq, dk, dv

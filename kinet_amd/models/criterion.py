@@ -140,22 +140,47 @@ class SetCriterion(nn.Module):
         return loss_map[loss](outputs, targets, indices, num_boxes, **kwargs)
 
     def num_boxes(self, outputs, targets):
-        """detr.py:841-846: total target count, summed over ranks, averaged, >= 1."""
+        """detr.py:841-846: total target count, summed over ranks, averaged, >= 1 (a host
+        number on one rank: no device round trip)."""
         n = sum(len(t["labels"]) for t in targets)
+        if _world_size() < 2:
+            return float(max(n, 1))
         n = torch.as_tensor([n], dtype=torch.float, device=next(iter(outputs.values())).device)
-        if _world_size() > 1:
-            dist.all_reduce(n)
+        dist.all_reduce(n)
         return torch.clamp(n / _world_size(), min=1).item()
+
+    def match(self, output_sets, targets):
+        """The matcher's indices for every output set, moved to the predictions' device in ONE
+        non-blocking copy (the losses index device tensors with them; the reference indexes
+        with host tensors, one implicit copy per sample and loss)."""
+        from kinet_amd.models.training import glue_timer, to_device
+        with glue_timer():
+            return self._match(output_sets, targets, to_device)
+
+    def _match(self, output_sets, targets, to_device):
+        if hasattr(self.matcher, 'match_many'):
+            host = self.matcher.match_many(output_sets, targets)
+        else:
+            host = [self.matcher(o, targets) for o in output_sets]
+        device = output_sets[0]['pred_logits'].device
+        flat = [t for per_set in host for pair in per_set for t in pair]
+        if device.type != 'cuda' or not flat:
+            return host
+        dev = to_device(torch.cat([t.long() for t in flat]), device).split([len(t) for t in flat])
+        it = iter(dev)
+        return [[(next(it), next(it)) for _ in per_set] for per_set in host]
 
     def forward(self, outputs, targets):
         outputs_without_aux = {k: v for k, v in outputs.items() if k != 'aux_outputs'}
-        indices = self.matcher(outputs_without_aux, targets)
+        aux = list(outputs.get('aux_outputs', []))
+        all_indices = self.match([outputs_without_aux] + aux, targets)
+        indices = all_indices[0]
         num_boxes = self.num_boxes(outputs, targets)
         losses = {}
         for loss in self.losses:
             losses.update(self.get_loss(loss, outputs, targets, indices, num_boxes))
-        for i, aux_outputs in enumerate(outputs.get('aux_outputs', [])):
-            indices = self.matcher(aux_outputs, targets)
+        for i, aux_outputs in enumerate(aux):
+            indices = all_indices[i + 1]
             for loss in self.losses:
                 kwargs = {'log': False} if loss == 'labels' else {}
                 l_dict = self.get_loss(loss, aux_outputs, targets, indices, num_boxes, **kwargs)

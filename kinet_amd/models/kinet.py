@@ -64,7 +64,8 @@ def _linear(x, mod, fast, relu=False, residual=None, ln=None, x_add=None, drop=N
 def _attention(mod, query, key, value, fast, q_add=None, k_add=None, key_padding_mask=None):
     """nn.MultiheadAttention(query [+ q_add], key [+ k_add], value, key_padding_mask)[0]
     BEFORE its out_proj (the caller fuses out_proj with residual + LayerNorm); batch-first.
-    Attention-probability dropout is not applied (as kinet_amd.autograd.multihead_attention)."""
+    In training the attention probabilities are dropped with the module's `dropout` (as
+    kinet_amd.autograd.multihead_attention)."""
     E = mod.embed_dim
     w, b = mod.in_proj_weight, mod.in_proj_bias
     scale = mod.head_dim ** -0.5
@@ -80,7 +81,8 @@ def _attention(mod, query, key, value, fast, q_add=None, k_add=None, key_padding
     q = A.linear(query if q_add is None else query + q_add, w[:E], b[:E])
     k = A.linear(key if k_add is None else key + k_add, w[E:2 * E], b[E:2 * E])
     v = A.linear(value, w[2 * E:], b[2 * E:])
-    return A.mha_core(q, k, v, mod.num_heads, scale, key_padding_mask)
+    return A.mha_core(q, k, v, mod.num_heads, scale, key_padding_mask,
+                      dropout_p=mod.dropout if mod.training else 0.0)
 
 
 def _layer_norm(x, ln, fast, residual=None):
@@ -501,7 +503,8 @@ def graph_kinet_forward(model, samples, targets=None, warmup=3):
                    for i in range(B)]
         return model(smp, tgs)[0]
 
-    gc = GraphedCall(fn, flat(samples, targets), warmup)
+    gc = GraphedCall(fn, flat(samples, targets), warmup,
+                     params=list(model.parameters()) + list(model.buffers()))
 
     def call(smp, tgs=None):
         if (tgs is not None and len(tgs[0]['track_query_hs_embeds_det']) > 0) != has_trk:

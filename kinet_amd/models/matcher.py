@@ -2,7 +2,8 @@
 build_matcher :685-712).
 
 The cost matrix (focal or softmax class cost, L1 box cost, -GIoU) is built batched on the
-device where the predictions live and crosses to the host in ONE copy; the linear sum
+device where the predictions live and crosses to the host in ONE copy (one for all of the
+criterion's final + auxiliary output sets: `match_many`); the linear sum
 assignment stays on the host (scipy.optimize.linear_sum_assignment, as in the reference,
 matcher.py:198) -- the north_star keeps the matcher host-side.  Track queries are forced
 onto the targets whose track ids they carry and false-positive track queries are made
@@ -56,29 +57,50 @@ class HungarianMatcher(nn.Module):
 
     @torch.no_grad()
     def forward(self, outputs, targets):
-        cost_matrix = self.cost_matrix(outputs, targets).cpu()
+        return self.match_many([outputs], targets)[0]
+
+    @torch.no_grad()
+    def match_many(self, outputs_list, targets):
+        """Indices of several output sets against the same targets -- the criterion's final
+        and auxiliary decoder outputs (detr.py:819-868 calls the matcher once per set) --
+        with ONE device->host synchronisation for all their cost matrices and the track-query
+        masks / match ids (to_host), instead of one per set."""
+        from kinet_amd.models.training import to_host
         sizes = [len(v["boxes"]) for v in targets]
         offsets = np.cumsum([0] + sizes[:-1])
         tq = [i for i, t in enumerate(targets) if 'track_query_match_ids' in t]
+        costs = torch.stack([self.cost_matrix(o, targets) for o in outputs_list])
+        extra = []
         if tq:
-            # matcher.py:177-196 without its per-query Python loop: every sample's masks and
-            # match ids come over in one copy each; a false-positive track query matches
-            # nothing (row = inf); the k-th true track query is forced onto target
-            # match_ids[k] (its row and that column inf, -1 at the pair)
             masks = torch.stack([torch.stack([targets[i]['track_queries_fal_pos_mask'],
-                                              targets[i]['track_queries_mask']]) for i in tq]).cpu()
+                                              targets[i]['track_queries_mask']]).to(costs.device) for i in tq])
             ids = [targets[i]['track_query_match_ids'] for i in tq]
             counts = [len(m) for m in ids]
-            ids = torch.cat(ids).cpu().split(counts) if sum(counts) else [torch.zeros(0, dtype=torch.long)] * len(tq)
+            extra = [masks, torch.cat([m.to(costs.device).long() for m in ids]) if sum(counts)
+                     else torch.zeros(0, dtype=torch.long)]
+        host = to_host(costs, *extra)
+        costs = host[0]
+        forced = []
+        if tq:
+            masks, ids = host[1], host[2].split(counts)
+            # matcher.py:177-196 without its per-query Python loop: a false-positive track
+            # query matches nothing (row = inf); the k-th true track query is forced onto
+            # target match_ids[k] (its row and that column inf, -1 at the pair)
             for n, i in enumerate(tq):
                 fal_pos, tq_mask = masks[n, 0], masks[n, 1]
                 rows = (tq_mask & ~fal_pos).nonzero().flatten()
                 cols = ids[n][:len(rows)].long() + int(offsets[i])
-                cost_matrix[i, fal_pos | tq_mask] = np.inf
+                forced.append((i, fal_pos | tq_mask, rows, cols))
+        result = []
+        for cost_matrix in costs:
+            for i, rowmask, rows, cols in forced:
+                cost_matrix[i, rowmask] = np.inf
                 cost_matrix[i, :, cols] = np.inf
                 cost_matrix[i, rows, cols] = -1
-        indices = [linear_sum_assignment(c[i]) for i, c in enumerate(cost_matrix.split(sizes, -1))]
-        return [(torch.as_tensor(i, dtype=torch.int64), torch.as_tensor(j, dtype=torch.int64)) for i, j in indices]
+            indices = [linear_sum_assignment(c[i]) for i, c in enumerate(cost_matrix.split(sizes, -1))]
+            result.append([(torch.as_tensor(i, dtype=torch.int64), torch.as_tensor(j, dtype=torch.int64))
+                           for i, j in indices])
+        return result
 
 
 def build_matcher(args):

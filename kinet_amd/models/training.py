@@ -14,6 +14,7 @@ tests/golden/train_sampler.npz.  The reference's distance weight uses the x offs
 """
 import contextlib
 import math
+import time
 
 import torch
 from torch import nn
@@ -32,8 +33,67 @@ def empty_track_queries(model, targets):
         target['track_query_match_ids'] = torch.tensor([]).long().to(device)
 
 
+# host-glue accounting of the training step (kinet_amd/train.py benchmark_train reports it):
+# seconds spent in the matcher / sampler, seconds of those spent waiting in to_host for the
+# device, and the number of device->host synchronisations
+GLUE = {'on': False, 'glue_s': 0.0, 'sync_wait_s': 0.0, 'syncs': 0}
+
+
+class glue_timer:
+    def __enter__(self):
+        self.t0 = time.perf_counter()
+
+    def __exit__(self, *exc):
+        if GLUE['on']:
+            GLUE['glue_s'] += time.perf_counter() - self.t0
+
+
+def to_host(*tensors):
+    """Device -> host copies of several tensors with ONE synchronisation: pinned destinations,
+    non-blocking copies queued on the current stream, then a single stream sync.  Host
+    tensors pass through."""
+    dev = next((t.device for t in tensors if t.is_cuda), None)
+    if dev is None:
+        return list(tensors)
+    t0 = time.perf_counter()
+    out = []
+    for t in tensors:
+        if t.is_cuda:
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            out.append(h)
+        else:
+            out.append(t)
+    torch.cuda.current_stream(dev).synchronize()
+    if GLUE['on']:
+        GLUE['sync_wait_s'] += time.perf_counter() - t0
+        GLUE['syncs'] += 1
+    return out
+
+
+def to_device(t, device):
+    """Host -> device without a host-side wait (pinned source, non-blocking copy)."""
+    if device.type != 'cuda':
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def add_track_queries_to_targets(model, targets, prev_indices, prev_out, add_false_pos=True):
-    """detr_tracking.py:39-218."""
+    with glue_timer():
+        _add_track_queries_to_targets(model, targets, prev_indices, prev_out, add_false_pos)
+
+
+def _add_track_queries_to_targets(model, targets, prev_indices, prev_out, add_false_pos=True):
+    """detr_tracking.py:39-218, batched host traffic.
+
+    The reference loops over samples with device tensors, so every `nonzero`, membership
+    test and `multinomial(box_weights.cpu())` synchronises with the GPU (≈4 syncs per sample
+    plus one per false positive).  Here the sampler's inputs cross to the host ONCE per batch
+    (track ids of both frames, the previous frame's boxes when false positives are drawn; one
+    stream sync), the per-sample logic runs on host tensors with the reference's exact
+    sequence of global-RNG calls, and the results go back in one non-blocking copy per dtype:
+    the track-query embeddings / boxes are one gather from the flattened previous-frame
+    outputs, split per sample."""
     device = prev_out['pred_boxes'].device
     fp_prob = model._track_query_false_positive_prob
     fn_prob = model._track_query_false_negative_prob
@@ -45,53 +105,80 @@ def add_track_queries_to_targets(model, targets, prev_indices, prev_out, add_fal
     if num_prev_target_ind:
         num_prev_target_ind_for_fps = torch.randint(int(math.ceil(fp_prob * num_prev_target_ind)) + 1, (1,)).item()
 
-    num_q_all = prev_out['pred_boxes'].shape[1]
-    for i, (target, prev_ind) in enumerate(zip(targets, prev_indices)):
-        prev_out_ind, prev_target_ind = prev_ind
+    B, num_q_all = prev_out['pred_boxes'].shape[:2]
+    # one host copy of everything the sampler reads (matcher indices are host tensors already)
+    prev_ids = [t['prev_target']['track_ids'] for t in targets]
+    cur_ids = [t['track_ids'] for t in targets]
+    n_prev, n_cur = [len(x) for x in prev_ids], [len(x) for x in cur_ids]
+    ids_dev = torch.cat([x.to(device).long().flatten() for x in prev_ids + cur_ids])
+    copies = [ids_dev]
+    if add_false_pos and num_prev_target_ind_for_fps:
+        copies.append(prev_out['pred_boxes'].detach().float())
+    host = to_host(*copies)
+    ids_host = host[0].split(n_prev + n_cur)
+    boxes_all = host[1] if len(host) > 1 else None
+    indices = [(o.cpu(), t.cpu()) for o, t in prev_indices]
+
+    flat_idx, match_ids, tq_masks, fp_masks, counts = [], [], [], [], []
+    for i in range(len(targets)):
+        prev_out_ind, prev_target_ind = indices[i]
         if fn_prob:
             # random subset of the matched detections (:62-79)
             random_subset_mask = torch.randperm(len(prev_target_ind))[:num_prev_target_ind]
-            prev_out_ind = prev_out_ind[random_subset_mask.to(prev_out_ind.device)]
-            prev_target_ind = prev_target_ind[random_subset_mask.to(prev_target_ind.device)]
+            prev_out_ind = prev_out_ind[random_subset_mask]
+            prev_target_ind = prev_target_ind[random_subset_mask]
 
         # match track ids between frames (:82-94)
-        prev_track_ids = target['prev_target']['track_ids'][prev_target_ind.to(target['prev_target']['track_ids'].device)]
-        match = prev_track_ids.unsqueeze(dim=1).eq(target['track_ids'])
+        match = ids_host[i][prev_target_ind].unsqueeze(dim=1).eq(ids_host[len(targets) + i])
         target_ind_matching = match.any(dim=1)
-        target['track_query_match_ids'] = match.nonzero()[:, 1]
+        match_ids.append(match.nonzero()[:, 1])
 
+        out_ind = prev_out_ind.tolist()
         if add_false_pos:
-            # random false positives next to matched detections (:97-158); the candidate boxes
-            # come to the host once per sample (the reference re-gathers them on the device and
-            # copies the distance weights to the host once per false positive)
-            boxes_host = prev_out['pred_boxes'][i].detach().float().cpu()
-            out_ind_host = prev_out_ind.cpu()
-            prev_boxes_matched = boxes_host[out_ind_host[target_ind_matching.cpu()]]
-            taken = set(out_ind_host.tolist())
-            not_prev_out_ind = [ind for ind in range(num_q_all) if ind not in taken]
+            # random false positives next to matched detections (:97-158), on the host copy
             random_false_out_ind = []
+            taken = set(out_ind)
+            not_prev_out_ind = [ind for ind in range(num_q_all) if ind not in taken]
             prev_target_ind_for_fps = torch.randperm(num_prev_target_ind)[:num_prev_target_ind_for_fps]
+            if len(prev_target_ind_for_fps):
+                boxes_host = boxes_all[i]
+                prev_boxes_matched = boxes_host[prev_out_ind[target_ind_matching]]
             for j in prev_target_ind_for_fps:
                 if len(prev_boxes_matched) > j:
                     prev_boxes_unmatched = boxes_host[not_prev_out_ind]
                     box_weights = prev_boxes_matched[j].unsqueeze(dim=0)[:, :2] - prev_boxes_unmatched[:, :2]
-                    box_weights = box_weights[:, 0] ** 2 + box_weights[:, 0] ** 2   # (sic, :128)
+                    box_weights = box_weights[:, 0] ** 2 + box_weights[:, 0] ** 2   # (sic, :132)
                     box_weights = torch.sqrt(box_weights)
                     random_false_out_idx = not_prev_out_ind.pop(torch.multinomial(box_weights, 1).item())
                 else:
                     random_false_out_idx = not_prev_out_ind.pop(torch.randperm(len(not_prev_out_ind))[0])
                 random_false_out_ind.append(random_false_out_idx)
-            prev_out_ind = torch.tensor(out_ind_host.tolist() + random_false_out_ind).long()
+            out_ind = out_ind + random_false_out_ind
             target_ind_matching = torch.cat([target_ind_matching,
-                                             torch.zeros(len(random_false_out_ind), dtype=torch.bool, device=device)])
+                                             torch.zeros(len(random_false_out_ind), dtype=torch.bool)])
+        K = len(out_ind)
+        counts.append(K)
+        flat_idx.append(torch.tensor(out_ind, dtype=torch.long) + i * num_q_all)
+        # track query masks (:164-184); queries are prepended to the object queries
+        tail = torch.zeros(model.num_queries, dtype=torch.bool)
+        tq_masks.append(torch.cat([torch.ones(K, dtype=torch.bool), tail]))
+        fp_masks.append(torch.cat([~target_ind_matching, tail]))
 
-        # track query masks (:174-184); queries are prepended to the object queries
-        tail = torch.zeros(model.num_queries, dtype=torch.bool, device=device)
-        prev_out_ind = prev_out_ind.to(device)
-        target['track_query_hs_embeds'] = prev_out['hs_embed'][i, prev_out_ind]
-        target['track_query_boxes'] = prev_out['pred_boxes'][i, prev_out_ind].detach()
-        target['track_queries_mask'] = torch.cat([torch.ones_like(target_ind_matching, dtype=torch.bool), tail])
-        target['track_queries_fal_pos_mask'] = torch.cat([~target_ind_matching.to(device), tail])
+    # back to the device: one copy per dtype, then views
+    n_match = [len(m) for m in match_ids]
+    longs = to_device(torch.cat(flat_idx + match_ids), device)
+    bools = to_device(torch.cat(tq_masks + fp_masks), device)
+    idx_dev, mid_dev = longs[:sum(counts)], longs[sum(counts):]
+    hs = prev_out['hs_embed'].flatten(0, 1)[idx_dev].split(counts)
+    bx = prev_out['pred_boxes'].detach().flatten(0, 1)[idx_dev].split(counts)
+    mids = mid_dev.split(n_match)
+    masks = bools.split([c + model.num_queries for c in counts] * 2)
+    for i, target in enumerate(targets):
+        target['track_query_match_ids'] = mids[i]
+        target['track_query_hs_embeds'] = hs[i]
+        target['track_query_boxes'] = bx[i]
+        target['track_queries_mask'] = masks[i]
+        target['track_queries_fal_pos_mask'] = masks[len(targets) + i]
 
 
 def _has_dropout(model):
@@ -129,8 +216,9 @@ def prepare_track_queries(model, targets, base_forward, prev_features=None):
                                                             prev_prev_features)
         else:
             prev_out, _, prev_features, _, _ = base_forward([t['prev_image'] for t in targets])
-        prev_indices = model._matcher(_without_aux(prev_out), prev_targets)
-        device = prev_targets[0]['labels'].device
-        prev_indices = [(o.to(device), t.to(device)) for o, t in prev_indices]
+        # the matcher's indices stay on the host: the sampler consumes them there (the
+        # reference moves them to the device, :262-265, and its sampler reads them back)
+        with glue_timer():
+            prev_indices = model._matcher(_without_aux(prev_out), prev_targets)
         add_track_queries_to_targets(model, targets, prev_indices, prev_out)
     return prev_features

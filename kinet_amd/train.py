@@ -176,16 +176,36 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
+    # host glue of the step (matcher + track-query sampler), measured over
+    # two extra steps: wall seconds in those functions, the part of it spent waiting for the
+    # device in the one-sync-per-call host copies, and the number of such syncs
+    from kinet_amd.models import training as TR
+    TR.GLUE.update(on=True, glue_s=0.0, sync_wait_s=0.0, syncs=0)
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    glue = dict(TR.GLUE)
+    TR.GLUE['on'] = False
     frames = batch * steps * world
+    from kinet_amd.models.training import _has_dropout
+    # with dropout > 0 the previous frame runs op-for-op in f32 (train-mode dropout, as the
+    # reference runs it: prepare_track_queries -> reference_path), not the bf16 HIP path
+    prev_desc = ('float32 (op-for-op path: train-mode dropout %g, as the reference)' % args.dropout
+                 if _has_dropout(model) else str(prev_dtype).replace('torch.', ''))
     return {'metric': 'train frames/sec (config 4: mot17 deformable multi_frame tracking, 3x%dx%d pairs)'
                       % (height, width),
             'value': frames / el, 'unit': 'frames/s', 'images_per_s': 2 * frames / el, 'n_gpus': world,
             'steps': steps, 'warmup': warmup, 's_per_step': el / steps, 'loss': float(loss), 'scaling': 'weak',
+            'host_glue': {'ms_per_step': glue['glue_s'] / 2 * 1e3,
+                          'device_wait_ms_per_step': glue['sync_wait_s'] / 2 * 1e3,
+                          'host_only_ms_per_step': (glue['glue_s'] - glue['sync_wait_s']) / 2 * 1e3,
+                          'device_to_host_syncs_per_step': glue['syncs'] / 2,
+                          'what': 'matcher (prev frame + criterion, all output sets) + track-query sampler'},
             'dtype': 'f32', 'data': 'synthetic frame pairs, 10-30 boxes, random-init weights',
             'config': {'workload': 'config4 two-pass tracking training step (prev frame no-grad, current frame '
                                    'fwd+bwd, AdamW)', 'batch_per_gpu': batch, 'hidden_dim': args.hidden_dim,
                        'num_queries': args.num_queries, 'dropout': args.dropout,
-                       'prev_frame_dtype': str(prev_dtype).replace('torch.', ''),
+                       'prev_frame_dtype': prev_desc,
                        'grad_frame_dtype': 'f32', 'f32_matmul_precision': matmul_precision +
                        (' (bf16x3 MFMA products)' if matmul_precision != 'highest' else ' (exact f32 MFMA)'),
                        'parallelism': f'ddp{world} (RCCL all-reduce)'}}

@@ -154,6 +154,79 @@ def test_mha_core_fwd_bwd(E, heads, Lq, mask):
         _close(a, r, rel=2e-4, name=n)
 
 
+@pytest.mark.parametrize('E,heads,Lq,Lk,mask,p', [(288, 8, 520, 520, True, 0.1), (256, 8, 77, 130, False, 0.5)])
+def test_mha_dropout_fixed_mask(E, heads, Lq, Lk, mask, p):
+    """Attention-probability dropout (nn.MultiheadAttention(dropout=p), deformable_transformer.py:345):
+    forward and gradients equal torch fp32 autograd of softmax -> (P * Z) @ V with the SAME keep
+    mask Z, materialised by kinet_dropout_mask from the seed the kernels used."""
+    from kinet_amd import autograd as A
+    from kinet_amd import kernels as K
+    B = 2
+    q = _g(B, Lq, E, seed=31).requires_grad_()
+    k = _g(B, Lk, E, seed=32).requires_grad_()
+    v = _g(B, Lk, E, seed=33).requires_grad_()
+    km = None
+    if mask:
+        km = torch.zeros(B, Lk, dtype=torch.bool, device='cuda')
+        km[1, -40:] = True
+    go = _g(B, Lq, E, seed=34)
+    D = E // heads
+    seed = torch.tensor([123456789], dtype=torch.int64, device='cuda')
+    o = A.mha_core(q, k, v, heads, D ** -0.5, km, dropout_p=p, seed=seed)
+    (o * go).sum().backward()
+    keep = K.dropout_mask(seed, B * heads * Lq * Lk, p).view(B, heads, Lq, Lk).float()
+    q2, k2, v2 = (t.detach().clone().requires_grad_() for t in (q, k, v))
+
+    def split(t):
+        return t.view(B, -1, heads, D).transpose(1, 2)
+    s = split(q2) @ split(k2).transpose(-1, -2) * D ** -0.5
+    if km is not None:
+        s = s.masked_fill(km[:, None, None, :], float('-inf'))
+    prob = s.softmax(-1) * keep / (1 - p)
+    o2 = (prob @ split(v2)).transpose(1, 2).reshape(B, Lq, E)
+    (o2 * go).sum().backward()
+    for n, a, r in zip(['o', 'dq', 'dk', 'dv'], [o.detach(), q.grad, k.grad, v.grad], [o2.detach(), q2.grad, k2.grad,
+                                                                                     v2.grad]):
+        _close(a, r, rel=2e-4, name=n)
+
+
+def test_dropout_mask_statistics():
+    """The keep mask is Bernoulli(1 - p): keep rate within 5 sigma, no correlation between
+    neighbouring elements or between two seeds, and reproducible from its seed."""
+    from kinet_amd import kernels as K
+    n = 1 << 22
+    for p in (0.1, 0.5):
+        s1 = torch.tensor([7], dtype=torch.int64, device='cuda')
+        s2 = torch.tensor([8], dtype=torch.int64, device='cuda')
+        a = K.dropout_mask(s1, n, p).double()
+        b = K.dropout_mask(s2, n, p).double()
+        q = 1 - p
+        sig = (q * p / n) ** 0.5
+        assert abs(a.mean().item() - q) < 5 * sig
+        # P(both kept) = q^2 for independent draws (neighbours, other seed)
+        assert abs((a[1:] * a[:-1]).mean().item() - q * q) < 5 * (q * q * (1 - q * q) / n) ** 0.5
+        assert abs((a * b).mean().item() - q * q) < 5 * (q * q * (1 - q * q) / n) ** 0.5
+        assert torch.equal(a, K.dropout_mask(s1, n, p).double())
+
+
+def test_multihead_attention_train_dropout_reproducible():
+    """Training-mode multihead_attention drops probabilities (the output differs from eval
+    mode) with a seed from torch's CUDA generator: torch.manual_seed reproduces it."""
+    from kinet_amd import autograd as A
+    E, H, B, L = 288, 8, 2, 64
+    mod = torch.nn.MultiheadAttention(E, H, dropout=0.1).cuda().train()
+    x = _g(B, L, E, seed=35)
+    torch.manual_seed(3)
+    y1 = A.multihead_attention(mod, x, x, x)
+    torch.manual_seed(3)
+    y2 = A.multihead_attention(mod, x, x, x)
+    y3 = A.multihead_attention(mod, x, x, x)
+    mod.eval()
+    y0 = A.multihead_attention(mod, x, x, x)
+    assert torch.equal(y1, y2)
+    assert not torch.equal(y1, y3) and not torch.equal(y1, y0)
+
+
 def test_multihead_attention_matches_module():
     """in_proj split + core + out_proj == nn.MultiheadAttention (batch-first by transposes)."""
     from kinet_amd import autograd as A

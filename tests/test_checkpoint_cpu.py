@@ -80,3 +80,42 @@ def test_resume_round_trip_through_a_file(tmp_path):
     assert ck['epoch'] == 7 and ck['args'].lr == 2e-4
     for k, v in src.state_dict().items():
         assert torch.equal(dst.state_dict()[k], v), k
+
+
+def test_load_full_train_py_checkpoint(tmp_path):
+    """train.py:322-330 saves model, optimizer, lr_scheduler (MultiStepLR: a Counter of
+    milestones), epoch, args, vis_win_names and best_val_stats -- with tracking_eval on
+    (cfgs/train.yaml:68) the latter holds numpy.float64 MOTA / IDF1 values (engine.py:343).
+    weights_only loading must accept all of it without unpickling code."""
+    import numpy as np
+    from kinet_amd.checkpoint import load_checkpoint
+    m = torch.nn.Linear(3, 2)
+    opt = torch.optim.AdamW(m.parameters(), lr=2e-4)
+    sched = torch.optim.lr_scheduler.MultiStepLR(opt, [40, 50])
+    ck = {'model': {'detr.' + k: v for k, v in m.state_dict().items()}, 'optimizer': opt.state_dict(),
+          'lr_scheduler': sched.state_dict(), 'epoch': 7, 'args': argparse.Namespace(lr=2e-4, hidden_dim=288),
+          'vis_win_names': {'train_loss': 'w1', 'val_mota': 'w2'},
+          'best_val_stats': [np.float64(0.61), np.float64(0.70), np.float32(0.5), np.int64(12)]}
+    p = tmp_path / 'checkpoint.pth'
+    torch.save(ck, p)
+    got = load_checkpoint(str(p))
+    assert got['epoch'] == 7 and got['args'].hidden_dim == 288
+    assert got['best_val_stats'][0] == np.float64(0.61) and isinstance(got['best_val_stats'][3], np.int64)
+    assert dict(got['lr_scheduler']['milestones']) == {40: 1, 50: 1}
+    assert torch.equal(got['model']['detr.weight'], m.weight)
+    # the allow-list is scoped to the call, not registered process-wide
+    with pytest.raises(Exception):
+        torch.load(p, weights_only=True)
+
+
+def test_load_checkpoint_refuses_code(tmp_path):
+    import os
+    from kinet_amd.checkpoint import load_checkpoint
+
+    class Evil:
+        def __reduce__(self):
+            return (os.getcwd, ())
+    p = tmp_path / 'evil.pth'
+    torch.save({'model': {}, 'x': Evil()}, p)
+    with pytest.raises(Exception):
+        load_checkpoint(str(p))

@@ -167,3 +167,13 @@ def test_kinet_graph_replay_equals_eager(golden_dir, dtype):
             assert torch.equal(got['pred_boxes'], ref['pred_boxes'])
         with pytest.raises(ValueError):
             call(s0, None)
+        # new weights after the recording: the replay refuses instead of reading stale packs
+        with torch.no_grad():
+            next(model.parameters()).mul_(0.5)
+        with pytest.raises(RuntimeError, match='parameters changed'):
+            call(s0, tg(1.0))
+        call = graph_kinet_forward(model, s0, tg(1.0))   # re-recorded: equal to eager again
+        ref, *_ = model(s0, tg(1.0))
+        got = call(s0, tg(1.0))
+        torch.cuda.synchronize()
+        assert torch.equal(got['pred_boxes'], ref['pred_boxes'])

@@ -59,3 +59,33 @@ def test_nms_kernel_matches_restatement():
                 supp |= iou[i] > thr
         got = K.nms(boxes.cuda(), scores.cuda(), thr).cpu().tolist()
         assert got == keep, (n, thr)
+
+
+@pytest.mark.gpu
+def test_nms_nan_scores_total_order():
+    """NaN scores: ranks stay a permutation -- NaNs first, as torch.sort(descending)
+    orders them -- so the kernel never reads an unwritten rank slot."""
+    from kinet_amd import kernels as K
+    g = torch.Generator().manual_seed(5)
+    n = 200
+    c = torch.rand(n, 2, generator=g) * 300
+    boxes = torch.cat([c, c + torch.rand(n, 2, generator=g) * 60 + 1], 1)
+    scores = torch.rand(n, generator=g)
+    scores[::7] = float('nan')
+    scores[3] = float('inf')
+    scores[5] = -float('inf')
+    order = torch.sort(scores, descending=True, stable=True)[1]
+    a = (boxes[:, 2] - boxes[:, 0]) * (boxes[:, 3] - boxes[:, 1])
+    lt = torch.max(boxes[:, None, :2], boxes[:, :2])
+    rb = torch.min(boxes[:, None, 2:], boxes[:, 2:])
+    wh2 = (rb - lt).clamp(min=0)
+    inter = wh2[..., 0] * wh2[..., 1]
+    iou = inter / (a[:, None] + a - inter)
+    supp = torch.zeros(n, dtype=torch.bool)
+    keep = []
+    for i in order.tolist():
+        if not supp[i]:
+            keep.append(i)
+            supp |= iou[i] > 0.5
+    got = K.nms(boxes.cuda(), scores.cuda(), 0.5).cpu().tolist()
+    assert got == keep
