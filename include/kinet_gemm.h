@@ -73,6 +73,15 @@ int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, in
                          int in_dtype, int out_dtype, const float* bias, const uint8_t* row_mask,
                          int rows_per_batch, int head_dim, kinet_stream_t stream);
 
+/* kinet_gemm_headmajor with A + A2 as the left operand (the position embedding added at load
+ * time, `with_pos_embed` of deformable_transformer.py:278); the MSDA offsets / logits
+ * projection of the encoder writes (M, N, Lq, L*P*3) head-major this way
+ * (kinet_msda_encoder_forward). */
+int kinet_gemm_headmajor_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K,
+                            int lda, int ldb, int in_dtype, int out_dtype, const float* bias,
+                            const uint8_t* row_mask, int rows_per_batch, int head_dim,
+                            kinet_stream_t stream);
+
 /* Split-K forms for small-M / long-K problems (few output tiles): K is cut into `ksplit`
  * slices (rounded to whole 64-element K-steps) whose f32 partial tiles go to `workspace`
  * (ksplit * M * N floats, caller-allocated), then one finalize pass sums the slices and

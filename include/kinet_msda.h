@@ -95,6 +95,29 @@ int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_
                              int value_dtype, int output_dtype, int offlog_dtype,
                              const int32_t* query_tile_order, kinet_stream_t stream);
 
+/* Encoder-sized fused sampling (the encoder's MSDeformAttn.forward, ms_deform_attn.py:69-87)
+ * with the offsets / logits projection in HEAD-MAJOR layout:
+ *   offsets_logits_hm  (M, N, Lq, L*P*3) f16: per (head, frame, query) [L*P*2 offsets in
+ *                      (l, p, xy) order | L*P logits in (l, p) order] -- the sampling_offsets /
+ *                      attention_weights rows of one head interleaved (kinet_amd.msda packs the
+ *                      weight rows so kinet_gemm_headmajor_ex writes it directly)
+ *   spatial_shapes_host (L, 2) int64 (H, W) in HOST memory (the launch geometry -- which
+ *                      levels fit the LDS map -- is chosen from it; KINET_ERR_ARG when not even
+ *                      the coarsest level fits: use kinet_msda_fused_forward)
+ *   value              f16 head-major: (b, s, m, c) at value[b*value_sb + m*value_sm + s*32 + c]
+ *   ref_points, query_attn_mask, output, query_tile_order as kinet_msda_fused_forward
+ *   (output (N, Lq, M*32) bf16 or f16).
+ * Same semantics as kinet_msda_fused_forward (softmax over L*P, the reference's 2-d offset
+ * normaliser quirk, 4-d refs, query mask); head_dim 32, L = 4, P = 4.  Each level's 16 taps
+ * are summed as f16 pairs before the f32 sum.  One workgroup per CU owns one (frame, head)
+ * map with its coarse levels staged in LDS (msda_enc.hip). */
+int kinet_msda_encoder_forward(const void* value, int64_t value_sb, int64_t value_sm,
+                               const int64_t* spatial_shapes_host, const void* offsets_logits_hm,
+                               const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
+                               void* output, int batch, int spatial_size, int num_heads, int channels,
+                               int num_levels, int num_query, int num_point, int output_dtype,
+                               const int32_t* query_tile_order, kinet_stream_t stream);
+
 /* Diagnostic kernel-selection knob (no reference counterpart, A/B timing only): bit 0 = never
  * use the specialised 16-bit / head_dim-32 fused kernels; bit 5 = no LDS-staged encoder
  * kernel; bit 6 = that kernel with every tap product summed in f32; bit 7 = two rounds of its

@@ -712,6 +712,10 @@ using namespace kinet;
 extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                                     int in_dtype, int out_dtype, const float* bias, const uint8_t* row_mask,
                                     int rows_per_batch, int head_dim, kinet_stream_t stream);
+extern "C" int kinet_gemm_headmajor_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K,
+                                       int lda, int ldb, int in_dtype, int out_dtype, const float* bias,
+                                       const uint8_t* row_mask, int rows_per_batch, int head_dim,
+                                       kinet_stream_t stream);
 
 extern "C" int kinet_gemm_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K, int lda,
                              int ldb, int ldc, int in_dtype, const float* scale, const float* bias, const void* R,
@@ -745,15 +749,24 @@ extern "C" int kinet_gemm_ex(const void* A, const void* A2, const void* B, void*
 extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                                     int in_dtype, int out_dtype, const float* bias, const uint8_t* row_mask,
                                     int rows_per_batch, int head_dim, kinet_stream_t stream) {
+    return kinet_gemm_headmajor_ex(A, nullptr, B, C, M, N, K, lda, ldb, in_dtype, out_dtype, bias, row_mask,
+                                   rows_per_batch, head_dim, stream);
+}
+
+extern "C" int kinet_gemm_headmajor_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K,
+                                       int lda, int ldb, int in_dtype, int out_dtype, const float* bias,
+                                       const uint8_t* row_mask, int rows_per_batch, int head_dim,
+                                       kinet_stream_t stream) {
     KINET_CHECK_ARG(out_dtype == in_dtype || (in_dtype == KINET_BF16 && out_dtype == KINET_F16),
                     "gemm_headmajor: out_dtype must equal in_dtype (or f16 from bf16)");
     KINET_CHECK_ARG(M >= 0 && N > 0 && K > 0, "gemm_headmajor: invalid sizes");
     KINET_CHECK_ARG(rows_per_batch > 0 && M % rows_per_batch == 0, "gemm_headmajor: M must be batch*rows_per_batch");
     KINET_CHECK_ARG(head_dim > 0 && head_dim % 4 == 0 && N % head_dim == 0, "gemm_headmajor: N must be a multiple of head_dim (%% 4)");
     KINET_CHECK_ARG(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K, "gemm_headmajor: bad K/lda/ldb");
-    KINET_CHECK_ARG(aligned16(A) && aligned16(B), "gemm_headmajor: A and B must be 16-byte aligned");
+    KINET_CHECK_ARG(aligned16(A) && aligned16(B) && (A2 == nullptr || aligned16(A2)),
+                    "gemm_headmajor: A, A2 and B must be 16-byte aligned");
     GemmArgs a{};
-    a.A = A; a.B = B; a.C = C; a.bias = bias; a.row_mask = row_mask;
+    a.A = A; a.A2 = A2; a.B = B; a.C = C; a.bias = bias; a.row_mask = row_mask;
     a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = N;
     a.hm_rows = rows_per_batch; a.hm_d = head_dim; a.hm_batch = M / rows_per_batch;
     const long long es = (long long)dtype_size(in_dtype);

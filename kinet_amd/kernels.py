@@ -513,6 +513,77 @@ def encoder_tile_order(shapes, device, qt=16):
     return o
 
 
+_host_shapes = {}
+ENC_MAP_ROWS = 2400      # msda_enc.hip EMAP_ROWS: LDS map rows (64 B) incl. the zero margins
+
+
+def msda_encoder_supported(value, shapes, Lq, n_heads, n_levels, n_points, batch):
+    """True when kinet_msda_encoder_forward takes the call: f16 head-major values of head_dim
+    32, 4 levels x 4 points, an encoder-sized query set (>= 2048 per frame) and at least the
+    coarsest level fitting the LDS map (with max W + 1 zero rows on each side)."""
+    if value.dim() != 4 or value.dtype != torch.float16 or value.shape[-1] != 32 or value.stride(2) != 32:
+        return False
+    if n_levels != 4 or n_points != 4 or Lq < 2048 or shapes is None or len(shapes) != 4:
+        return False
+    h, w = shapes[-1]
+    if h * w + 2 * (w + 1) > ENC_MAP_ROWS or batch * Lq >= (1 << 24):
+        return False
+    return value.data_ptr() % 16 == 0 and value.stride(1) % 8 == 0 and value.stride(0) % 8 == 0
+
+
+def offsets_proj_headmajor(x, weight, bias, heads, x_add=None, out_dtype=torch.float16):
+    """The MSDA offsets + logits projection (x [+ x_add]) @ W^T + b stored head-major
+    (heads, B, Lq, Nout/heads): W's rows must already be grouped per head
+    (MSDeformAttn.packed_offsets_weights_headmajor)."""
+    N.require_gpu(x)
+    B, Lq, K = x.shape
+    x2 = x.reshape(B * Lq, K)
+    a2 = x_add.reshape(B * Lq, K) if x_add is not None else None
+    if x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16 or \
+            (a2 is not None and (a2.stride() != x2.stride() or a2.data_ptr() % 16)):
+        x2 = x2.contiguous()
+        a2 = a2.contiguous() if a2 is not None else None
+    w = weight_as(weight, x.dtype)
+    Nout = w.shape[0]
+    rec = Nout // heads
+    out = torch.empty((heads, B, Lq, rec), dtype=out_dtype, device=x.device)
+    e = x.element_size()
+    N.call('kinet_gemm_headmajor_ex', N.ptr(x2), N.ptr(a2), N.ptr(w), N.ptr(out), B * Lq, Nout, K, x2.stride(0), K,
+           N.dtype_code(x.dtype), N.dtype_code(out_dtype), N.ptr(f32(bias)), None, Lq, rec, N.stream(x.device),
+           work={'family': 'gemm', 'flops': 2.0 * B * Lq * Nout * K, 'shape': (B * Lq, Nout, K),
+                 'bytes': (B * Lq * K * (2 if a2 is not None else 1) + Nout * K) * e + B * Lq * Nout * 2})
+    return out
+
+
+def msda_encoder(value, shapes, offlog_hm, reference_points, n_heads, query_attn_mask=None, out_dtype=None,
+                 query_tile_order=None):
+    """Encoder-sized MSDeformAttn sampling (kinet_msda_encoder_forward): value (M, B, S, 32)
+    f16 head-major, shapes = host list of (H, W), offlog_hm (M, B, Lq, 48) f16 from
+    offsets_proj_headmajor, reference_points (B, Lq, 4, 2|4) f32 -> (B, Lq, M*32)."""
+    M_, B, S, D = value.shape
+    Lq = offlog_hm.shape[2]
+    key = tuple(tuple(int(v) for v in s) for s in shapes)
+    hs = _host_shapes.get(key)
+    if hs is None:
+        hs = _host_shapes[key] = torch.tensor(key, dtype=torch.int64)
+    ref = reference_points.float().contiguous()
+    od = out_dtype or torch.bfloat16
+    out = torch.empty((B, Lq, M_ * D), dtype=od, device=value.device)
+    qm = query_attn_mask.to(torch.uint8).contiguous() if query_attn_mask is not None else None
+    if query_tile_order is not None and (query_tile_order.dtype != torch.int32 or
+                                         query_tile_order.numel() != (Lq + 15) // 16):
+        raise RuntimeError('msda_encoder: query_tile_order must be int32 with ceil(Lq/16) entries')
+    offlog_hm = offlog_hm.contiguous()
+    nsamp = B * Lq * M_ * 16
+    N.call('kinet_msda_encoder_forward', N.ptr(value), value.stride(1), value.stride(0), N.ptr(hs), N.ptr(offlog_hm),
+           N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), B, S, M_, D, 4, Lq, 4, N.dtype_code(od),
+           N.ptr(query_tile_order), N.stream(value.device),
+           work={'family': 'msda', 'flops': 10.0 * nsamp * D, 'Lq': Lq, 'S': S,
+                 # compulsory bytes: value once, f16 offsets + logits, refs, output once
+                 'bytes': B * S * M_ * D * 2 + offlog_hm.numel() * 2 + ref.numel() * 4 + out.numel() * out.element_size()})
+    return out
+
+
 def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_levels, n_points,
                query_attn_mask=None, want_loc_attw=False, head_major=False, out_dtype=None,
                query_tile_order=None):

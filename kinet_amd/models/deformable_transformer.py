@@ -96,19 +96,22 @@ class DeformableTransformerEncoderLayer(nn.Module):
         src2 = A.linear_module(self.dropout2(self.activation(A.linear_module(src, self.linear1))), self.linear2)
         return A.layer_norm(src + self.dropout3(src2), self.norm2)
 
-    def forward(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None):
+    def forward(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None,
+                shapes_host=None):
         if fast_path(self):
-            return self.forward_fast(src, pos, reference_points, spatial_shapes, padding_mask, query_order)
+            return self.forward_fast(src, pos, reference_points, spatial_shapes, padding_mask, query_order,
+                                     shapes_host)
         src2 = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, spatial_shapes, padding_mask)
         src = A.layer_norm(src + self.dropout1(src2), self.norm1)
         return self.forward_ffn(src)
 
-    def forward_fast(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None):
+    def forward_fast(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None,
+                     shapes_host=None):
         # deformable_transformer.py:290-299, one kernel per step
         a = self.self_attn
         value = a.project_value(src, padding_mask)                                     # head-major
         samp = a.sample(src, reference_points, value, spatial_shapes, query_add=pos,   # (src+pos) @ W
-                        query_order=query_order)
+                        query_order=query_order, shapes_host=shapes_host)
         n1, n2 = self.norm1, self.norm2
         src = K.linear(samp, a.output_proj.weight, a.output_proj.bias, residual=src, ln=(n1.weight, n1.bias, n1.eps))
         if K.ffn_supported(src, self.linear1, self.linear2):
@@ -139,15 +142,17 @@ class DeformableTransformerEncoder(nn.Module):
         return reference_points[:, :, None] * valid_ratios[:, None]
 
     def forward(self, src, spatial_shapes, valid_ratios, pos=None, padding_mask=None, reference_points=None,
-                query_order=None):
+                query_order=None, shapes_host=None):
         output = src
         if reference_points is None:
             shapes = spatial_shapes.tolist() if torch.is_tensor(spatial_shapes) else spatial_shapes
+            shapes_host = shapes_host or [tuple(int(v) for v in s) for s in shapes]
             reference_points = self.get_reference_points(shapes, valid_ratios, device=src.device)
         if not torch.is_tensor(spatial_shapes):
             spatial_shapes = torch.as_tensor(spatial_shapes, dtype=torch.long, device=src.device)
         for layer in self.layers:
-            output = layer(output, pos, reference_points, spatial_shapes, padding_mask, query_order=query_order)
+            output = layer(output, pos, reference_points, spatial_shapes, padding_mask, query_order=query_order,
+                           shapes_host=shapes_host)
         return output
 
 
@@ -436,7 +441,7 @@ class DeformableTransformer(nn.Module):
                 src, pos = src.contiguous(), pos.contiguous()
                 pm = pm.contiguous() if pm is not None else None
             encs.append(self.encoder(src, e['spatial_shapes'], e['valid_ratios'], pos, pm, reference_points=e['ref'],
-                                     query_order=e.get('order')))
+                                     query_order=e.get('order'), shapes_host=e['shapes']))
         if len(encs) == 2:
             prev_memory, memory = encs
             memory = torch.cat([memory, prev_memory], 1)   # [current, prev] -- reference order (:173)

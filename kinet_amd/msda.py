@@ -115,12 +115,34 @@ class MSDeformAttn(nn.Module):
                            lambda a, b: torch.cat([a.detach(), b.detach()], 0).float().contiguous())
         return w, b
 
+    def packed_offsets_weights_headmajor(self):
+        """The same projection with its rows grouped per head -- head m's L*P*2 offset rows,
+        then its L*P logit rows -- so a head-major store of the GEMM output is the
+        (M, N, Lq, L*P*3) layout kinet_msda_encoder_forward reads."""
+        so, aw = self.sampling_offsets, self.attention_weights
+        M, LP = self.n_heads, self.n_levels * self.n_points
+
+        def interleave(a, b):
+            return torch.cat([a.detach().view(M, 2 * LP, *a.shape[1:]), b.detach().view(M, LP, *b.shape[1:])],
+                             1).reshape(M * 3 * LP, *a.shape[1:])
+        w = K.cached_multi([so.weight, aw.weight], 'packed_w_hm', lambda a, b: interleave(a, b).contiguous())
+        b = K.cached_multi([so.bias, aw.bias], 'packed_b_hm', lambda a, b: interleave(a, b).float().contiguous())
+        return w, b
+
     def sample(self, query, reference_points, value, input_spatial_shapes, query_attn_mask=None, query_add=None,
-               query_order=None):
+               query_order=None, shapes_host=None):
         """value already projected: head-major (M, N, S, D) from project_value (or a
         row-major (N, S, d) tensor); the offsets/weights projection input is query
         (+ query_add, e.g. the position embedding, added at GEMM load time); returns the
-        pre-output_proj (N, Lq, d)."""
+        pre-output_proj (N, Lq, d).  shapes_host: the level shapes as a host list (lets an
+        encoder-sized call take kinet_msda_encoder_forward)."""
+        N_, Lq = query.shape[:2]
+        if (query.dtype in (torch.bfloat16, torch.float16) and
+                K.msda_encoder_supported(value, shapes_host, Lq, self.n_heads, self.n_levels, self.n_points, N_)):
+            w, b = self.packed_offsets_weights_headmajor()
+            offlog = K.offsets_proj_headmajor(query, w, b, self.n_heads, x_add=query_add)
+            return K.msda_encoder(value, shapes_host, offlog, reference_points, self.n_heads, query_attn_mask,
+                                  out_dtype=query.dtype, query_tile_order=query_order)
         w, b = self.packed_offsets_weights()
         # bf16 compute: offsets/logits in f16 (half the bytes of f32 through HBM twice; f16
         # keeps 11 mantissa bits for the pixel offsets); parity mode stays f32

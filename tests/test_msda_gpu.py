@@ -349,3 +349,140 @@ def test_encoder_lds_kernel_order_and_batch_invariant():
     torch.cuda.synchronize()
     assert torch.equal(o_nat, o_ord) and torch.equal(o_ord, o_again)
     assert torch.equal(o_one[0], o_ord[1])
+
+
+# ---- encoder kernel, head-major offsets / logits (msda_enc.hip, kinet_msda_encoder_forward) ----
+
+def _hm(offlog, M, L=4, P=4):
+    """(B, Lq, M*L*P*3) [offsets | logits] -> (M, B, Lq, L*P*3) per-head [offsets | logits], f16."""
+    B, Lq, _ = offlog.shape
+    off = offlog[..., :M * L * P * 2].reshape(B, Lq, M, L * P * 2)
+    lg = offlog[..., M * L * P * 2:].reshape(B, Lq, M, L * P)
+    return torch.cat([off, lg], -1).permute(2, 0, 1, 3).contiguous().half()
+
+
+@pytest.mark.parametrize('shapes,ref_dim,noise', [
+    (((64, 84), (32, 42), (16, 21), (8, 11)), 2, 3.0),       # levels 2-3 staged (as at 800x1333)
+    (((64, 84), (32, 42), (16, 21), (8, 11)), 4, 6.0),       # box references, far-out samples
+    (((60, 70), (40, 50), (45, 50), (10, 13)), 2, 2.0),      # level 3 only fits
+    (((50, 60), (20, 30), (10, 13), (5, 7)), 2, 1.0),        # levels 1-3 staged
+    (((25, 40), (15, 20), (8, 10), (4, 5)), 2, 4.0),         # every level staged (Lq > S)
+    (((100, 167), (50, 84), (25, 42), (13, 21)), 2, 2.0),    # the config-2 geometry (800x1333)
+])
+@pytest.mark.parametrize('out_dtype,masked', [(torch.bfloat16, False), (torch.float16, True)])
+def test_encoder_kernel_matches_fast_kernel(shapes, ref_dim, noise, out_dtype, masked):
+    """kinet_msda_encoder_forward against msda_fused_fast_kernel (flag 32) on the same f16
+    offsets / logits (row-major for the fast kernel, head-major for the encoder kernel).
+    Bound as test_encoder_lds_kernel_matches_fast_kernel (acc16): the tap weights are
+    quantised to f16 after f32 location arithmetic that the compiler may contract
+    differently (2^-11 max|value|), each level's 16 taps are summed as f16 pairs
+    (2^-7 max|value|), plus one rounding of either output."""
+    from kinet_amd import _native
+    from kinet_amd import kernels as K
+    B, M, P = 2, 8, 4
+    Lq = max(sum(h * w for h, w in shapes), 2304)
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, Lq + 7 * ref_dim,
+                                                  dtype=torch.float16)
+    offlog = offlog.half()
+    qm = qmask if masked else None
+    o_enc = K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, qm, out_dtype=out_dtype)
+    lib = _native.lib()
+    try:
+        lib.kinet_msda_set_flags(32)
+        o_fast = K.msda_fused(value, ss, offlog, ref, M, 4, P, qm, head_major=True, out_dtype=out_dtype)
+    finally:
+        lib.kinet_msda_set_flags(0)
+    torch.cuda.synchronize()
+    ulp = 2.0 ** -7 if out_dtype == torch.bfloat16 else 2.0 ** -10
+    d = (o_enc.float() - o_fast.float()).abs()
+    vmax = value.float().abs().max().item()
+    big = torch.maximum(o_fast.float().abs(), o_enc.float().abs())
+    assert (d <= big * ulp + (2.0 ** -7 + 2.0 ** -11) * vmax).all(), d.max().item()
+    assert d.mean().item() <= 2e-3, d.mean().item()
+    if masked:
+        assert (o_enc.float()[qmask] == 0).all()
+    assert torch.isfinite(o_enc.float()).all()
+
+
+def test_encoder_kernel_vs_oracle():
+    """The encoder kernel against the C oracle (cuh:165-237 restated), fed the locations /
+    attention weights the fast kernel reports for the same inputs."""
+    from kinet_amd import kernels as K
+    from oracle import msda_oracle as O
+    shapes = ((64, 84), (32, 42), (16, 21), (8, 11))
+    B, M, P = 2, 8, 4
+    Lq = sum(h * w for h, w in shapes)
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 78, dtype=torch.float16)
+    offlog = offlog.half()
+    out = K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, qmask, out_dtype=torch.float16)
+    _, loc, aw = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, want_loc_attw=True, head_major=True,
+                              out_dtype=torch.float16)
+    torch.cuda.synchronize()
+    v = value.float().permute(1, 2, 0, 3).contiguous().cpu().numpy()
+    ref_out = torch.from_numpy(O.fwd(v, ss.cpu().numpy(), loc.cpu().numpy(), aw.cpu().numpy())).reshape(out.shape)
+    d = (out.float().cpu() - ref_out).abs()
+    bound = 4e-3 * ref_out.abs() + 4e-3 + 2.0 ** -7 * value.float().abs().max().item()
+    assert (d <= bound).all(), d.max().item()
+    assert d.mean().item() <= 2e-3, d.mean().item()
+
+
+def test_encoder_kernel_order_and_batch_invariant():
+    """Each query's result depends only on its own inputs: tile order, batch size (query
+    chunks per head map) and a rerun leave it bit-identical."""
+    from kinet_amd import kernels as K
+    shapes = ((64, 84), (32, 42), (16, 21), (8, 11))
+    M, P = 8, 4
+    Lq = sum(h * w for h, w in shapes)
+    value, ss, offlog, ref, qmask = _fused_inputs(3, shapes, Lq, M, P, 2, 3.0, 6, dtype=torch.float16)
+    hm = _hm(offlog, M)
+    order = K.encoder_tile_order(shapes, value.device)
+    o_nat = K.msda_encoder(value, shapes, hm, ref, M, out_dtype=torch.bfloat16)
+    o_ord = K.msda_encoder(value, shapes, hm, ref, M, out_dtype=torch.bfloat16, query_tile_order=order)
+    o_again = K.msda_encoder(value, shapes, hm, ref, M, out_dtype=torch.bfloat16, query_tile_order=order)
+    o_one = K.msda_encoder(value[:, 1:2], shapes, hm[:, 1:2], ref[1:2], M, out_dtype=torch.bfloat16,
+                           query_tile_order=order)
+    torch.cuda.synchronize()
+    assert torch.equal(o_nat, o_ord) and torch.equal(o_ord, o_again)
+    assert torch.equal(o_one[0], o_ord[1])
+
+
+def test_encoder_kernel_large_magnitudes():
+    """f16 range on the bf16 path (values and offsets are stored f16): values up to 2^14 and
+    offsets of thousands of pixels (samples far outside every level) stay finite, match the
+    f32-accumulating fast kernel within the stated f16 bounds, and out-of-image samples add 0."""
+    from kinet_amd import _native
+    from kinet_amd import kernels as K
+    shapes = ((64, 84), (32, 42), (16, 21), (8, 11))
+    B, M, P = 1, 8, 4
+    Lq = sum(h * w for h, w in shapes)
+    value, ss, offlog, ref, _ = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 99, dtype=torch.float16)
+    value = (value.float() * 4096.0).clamp(-16384, 16384).half()
+    offlog = offlog.clone()
+    offlog[:, : Lq // 2, : M * 32] *= 1000.0          # half the queries sample far outside
+    offlog = offlog.half()
+    o_enc = K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, out_dtype=torch.bfloat16)
+    lib = _native.lib()
+    try:
+        lib.kinet_msda_set_flags(32)
+        o_fast = K.msda_fused(value, ss, offlog, ref, M, 4, P, None, head_major=True, out_dtype=torch.bfloat16)
+    finally:
+        lib.kinet_msda_set_flags(0)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o_enc.float()).all()
+    vmax = value.float().abs().max().item()
+    d = (o_enc.float() - o_fast.float()).abs()
+    big = torch.maximum(o_fast.float().abs(), o_enc.float().abs())
+    assert (d <= big * 2.0 ** -7 + (2.0 ** -7 + 2.0 ** -11) * vmax).all(), d.max().item()
+
+
+def test_encoder_kernel_rejects_unstaged_geometry():
+    """Shapes whose coarsest level does not fit the LDS map are refused (the module falls back
+    to kinet_msda_fused_forward: msda_encoder_supported is False for them)."""
+    from kinet_amd import kernels as K
+    shapes = ((70, 80), (56, 60), (45, 50), (40, 40))
+    B, M, P = 1, 8, 4
+    Lq = sum(h * w for h, w in shapes)
+    value, ss, offlog, ref, _ = _fused_inputs(B, shapes, Lq, M, P, 2, 1.0, 3, dtype=torch.float16)
+    assert not K.msda_encoder_supported(value, shapes, Lq, M, 4, 4, B)
+    with pytest.raises(RuntimeError, match='coarsest level'):
+        K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, out_dtype=torch.bfloat16)

@@ -71,6 +71,8 @@ def main():
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--order', action='store_true', help='encoder tile order (kernels.encoder_tile_order)')
     ap.add_argument('--flags', type=int, default=0, help='kinet_msda_set_flags value (kernel variants)')
+    ap.add_argument('--hm', action='store_true',
+                    help='encoder kernel on head-major offsets/logits (kinet_msda_encoder_forward)')
     a = ap.parse_args()
     if a.flags:
         from kinet_amd import _native
@@ -81,14 +83,23 @@ def main():
     order = K.encoder_tile_order(ss.tolist(), value.device) if a.order and not a.decoder else None
     fn = lambda: K.msda_fused(value, ss, offlog, ref, M, L, P, head_major=True, out_dtype=torch.bfloat16,   # noqa: E731
                               query_tile_order=order)
+    kind = 'fused'
+    if a.hm and not a.decoder:
+        B_, Lq_ = offlog.shape[:2]
+        hm = torch.cat([offlog[..., :M * L * P * 2].reshape(B_, Lq_, M, -1),
+                        offlog[..., M * L * P * 2:].reshape(B_, Lq_, M, -1)], -1).permute(2, 0, 1, 3).contiguous()
+        shapes = [tuple(s) for s in ss.tolist()]
+        fn = lambda: K.msda_encoder(value, shapes, hm, ref, M, out_dtype=torch.bfloat16,   # noqa: E731
+                                    query_tile_order=order)
+        kind = 'encoder-hm'
     ms = time_call(fn, a.iters)
     B, Lq = offlog.shape[:2]
     S = value.shape[2]
     nsamp = B * Lq * M * L * P
     gathered = nsamp * 4 * value.shape[-1] * value.element_size()
-    compulsory = value.numel() * value.element_size() + offlog.numel() * 4 + ref.numel() * 4 + \
+    compulsory = value.numel() * value.element_size() + offlog.numel() * offlog.element_size() + ref.numel() * 4 + \
         B * Lq * M * value.shape[-1] * value.element_size()
-    print(f'[flags {a.flags}] msda {"decoder" if a.decoder else "encoder"} B={B} Lq={Lq} S={S} noise={a.noise}: {ms * 1e3:.1f} us/call  '
+    print(f'[{kind} flags {a.flags}] msda {"decoder" if a.decoder else "encoder"} B={B} Lq={Lq} S={S} noise={a.noise}: {ms * 1e3:.1f} us/call  '
           f'compulsory {compulsory / ms / 1e6:.0f} GB/s  gathered {gathered / ms / 1e6:.0f} GB/s')
 
 
