@@ -41,7 +41,7 @@ MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'f16': 2500.0, 'f32': 157.3}   # dense
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command
 # (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950 per MI355X_MICROARCH.md "HBM")
 PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
-MSDA_ENC_KERNEL = 'msda_enc_lds_kernel'     # config-2 encoder calls (coarse levels in LDS)
+MSDA_ENC_KERNEL = 'msda_enc_kernel'         # config-2 encoder calls (msda_enc.hip: coarse levels + a level-1 band in LDS)
 MSDA_KERNEL = 'msda_fused_fast_kernel'      # decoder calls
 
 WORKLOADS = {
@@ -246,6 +246,59 @@ def summarize_trace(trace, steps_traced=1):
     return fam, msda
 
 
+def decoder_touched_bytes(model, samples, extra):
+    """Bytes the decoder's sampling kernel must move per call: the value rows (pixel, head)
+    its bilinear corners actually touch -- counted from the sampling locations of one more
+    forward -- plus its offsets / logits, references and output.  The decoder's 300 queries x
+    8 heads x 16 samples touch a small part of each value map, so the whole map is not the
+    compulsory traffic of that kernel."""
+    from kinet_amd import kernels as K
+    calls = []
+    orig = K.msda_fused
+
+    def spy(value, spatial_shapes, offlog, reference_points, n_heads, n_levels, n_points, query_attn_mask=None,
+            want_loc_attw=False, head_major=False, out_dtype=None, query_tile_order=None):
+        out = orig(value, spatial_shapes, offlog, reference_points, n_heads, n_levels, n_points, query_attn_mask,
+                   want_loc_attw, head_major, out_dtype, query_tile_order)
+        S = value.shape[2] if head_major else value.shape[1]
+        if not want_loc_attw and offlog.shape[1] != S:
+            calls.append((value, spatial_shapes, offlog, reference_points, n_heads, n_levels, n_points,
+                          query_attn_mask, head_major, out_dtype))
+        return out
+    K.msda_fused = spy
+    try:
+        with torch.no_grad():
+            model(samples, *extra)
+    finally:
+        K.msda_fused = orig
+    res = []
+    for value, ss, offlog, ref, M, L, P, qm, hm, od in calls:
+        o, loc, _ = orig(value, ss, offlog, ref, M, L, P, qm, True, hm, od)
+        B, Lq = loc.shape[:2]
+        D = value.shape[-1]
+        S = value.shape[2] if hm else value.shape[1]
+        keys = []
+        start = 0
+        bm = (torch.arange(B, device=loc.device)[:, None, None, None] * M +
+              torch.arange(M, device=loc.device)[None, None, :, None])          # (B, 1, M, 1)
+        for l, (H, W) in enumerate(ss.tolist()):
+            x, y = loc[:, :, :, l, :, 0], loc[:, :, :, l, :, 1]                   # (B, Lq, M, P)
+            h, w = y * H - 0.5, x * W - 0.5
+            inside = (h > -1) & (w > -1) & (h < H) & (w < W)
+            hl, wl = torch.floor(h).long(), torch.floor(w).long()
+            for dy in (0, 1):
+                for dx in (0, 1):
+                    r, c = hl + dy, wl + dx
+                    ok = inside & (r >= 0) & (r < H) & (c >= 0) & (c < W)
+                    k = (bm * S + start + r * W + c)[ok]
+                    keys.append(k)
+            start += H * W
+        rows = torch.unique(torch.cat(keys)).numel()
+        res.append(rows * D * value.element_size() + offlog.numel() * offlog.element_size() + ref.numel() * 4
+                   + o.numel() * o.element_size())
+    return statistics.mean(res) if res else None
+
+
 def pmc_traffic(kernel):
     """(bytes per launch, provenance) of `kernel` from the committed PMC summary, or (None, None)."""
     try:
@@ -404,6 +457,7 @@ def main():
     trace = _native.trace_end()
     torch.cuda.synchronize()
     fam, msda = summarize_trace(trace, 3)
+    dec_touched = decoder_touched_bytes(model, samples, extra[0]) if a.workload == 'config2' else None
     split = roofline_split(trace, 3, MFMA_PEAK_TFLOPS[a.dtype])
 
     # config-4 training step (BASELINE configs[3]): every rank runs the DDP step, gradients
@@ -444,10 +498,19 @@ def main():
                         'algorithmic_bytes_per_launch': t_b / len(launches),
                         'avg_launch_ms': t_ms / len(launches), 'launches_per_step': len(launches) / 3}
             if a.workload == 'config2' and enc and dec:
-                msda_roof = roof(enc, MSDA_ENC_KERNEL + '<f16_t, bf16_t, f16_t> (encoder launches, Lq = S = %d)'
+                msda_roof = roof(enc, MSDA_ENC_KERNEL + '<bf16_t, 2, 2, false, true> (encoder launches, Lq = S = %d)'
                                  % enc[0][0], MSDA_ENC_KERNEL)
                 msda_roof['decoder_kernel'] = roof(dec, MSDA_KERNEL + '<f16_t, bf16_t, f16_t, 4, 4> (decoder launches)',
                                                    MSDA_KERNEL)
+                # the decoder held against the bytes it must touch (value rows its corners
+                # reach), not the whole value map
+                if dec_touched:
+                    dk = msda_roof['decoder_kernel']
+                    t_ms = dk['avg_launch_ms']
+                    ach = dec_touched / (t_ms * 1e-3) / 1e9
+                    dk.update(algorithmic_bytes_per_launch=dec_touched, achieved=ach, frac=ach / HBM_PEAK_GBS,
+                              bytes_basis='value rows touched by the bilinear corners (counted from one forward) + '
+                                          'offsets/logits + references + output')
                 msda_roof['all_msda_launches'] = roof(msda, 'encoder + decoder launches', None)
             else:
                 msda_roof = roof(msda, 'msda_fused_kernel<f16_t, 4> (D=36, encoder + decoder launches)', None)

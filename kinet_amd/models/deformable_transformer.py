@@ -12,8 +12,11 @@ Two execution paths with identical arithmetic:
     FFN as two GEMMs (ReLU / residual fused), decoder self-attention as in_proj GEMMs +
     the MHA kernel, and box refinement as one small kernel.  Activations stay in the
     compute dtype (bf16 perf mode, f32 parity mode) in (batch, tokens, channels) layout.
-  * training (autograd enabled) -- the reference's op sequence in torch with
-    MSDeformAttnFunction (HIP forward/backward kernels) at the operator boundary.
+  * training (autograd enabled) -- the reference's op sequence, op for op, on kinet_amd
+    autograd Functions (kinet_amd/autograd.py: Linear, LayerNorm, attention core with its
+    probability dropout, ...; forward and backward HIP kernels) with MSDeformAttnFunction
+    (HIP forward / backward) at the operator boundary; torch supplies only glue (dropout
+    masks outside attention, adds, reshapes).
 Reference quirks kept on purpose: 2-d sampling offsets divided by
 (H, W) applied to (x, y); multi-frame memory concatenated [current, prev] while shapes,
 masks and valid ratios stay [prev, current].

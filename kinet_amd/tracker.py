@@ -73,8 +73,15 @@ class Track:
         self.last_pos.append(self.last_pos[-1])
         self.last_pos_relative.append(self.last_pos_relative[-1])
 
-    def reset_last_pos(self):
+    def reset_last_pos(self, clear_relative=False):
+        """tracker.py:1120-1124.  The reference also clears last_pos_relative, after which its
+        repeat_last_pos raises IndexError on the next frame the track is not re-detected
+        (tracker.py:1110-1114); this build keeps that list by default.  clear_relative=True
+        (tracker cfg `reference_clear_last_pos_relative`) reproduces the reference exactly,
+        defect included."""
         self.last_pos.clear()
+        if clear_relative:
+            self.last_pos_relative.clear()
         self.last_pos.append(self.pos.clone())
 
 
@@ -100,6 +107,10 @@ class Tracker:
         self.reid_greedy_matching = tracker_cfg['reid_greedy_matching']
         self.prev_frame_dist = tracker_cfg['prev_frame_dist']
         self.steps_termination = tracker_cfg['steps_termination']
+        # compatibility switch for a reference defect (Track.reset_last_pos): False = keep the
+        # relative-position history on re-identification (default), True = clear it as the
+        # reference does (its next repeat_last_pos then raises IndexError)
+        self.reference_clear_last_pos_relative = bool(tracker_cfg.get('reference_clear_last_pos_relative', False))
         self._logger = logger if logger is not None else (lambda *a: None)
         self._verbose = verbose
 
@@ -219,7 +230,7 @@ class Tracker:
                 track.pos = new_det_boxes[c]
                 track.score = new_det_scores[c]
                 track.hs_embed.append(new_det_hs_embeds[c])
-                track.reset_last_pos()
+                track.reset_last_pos(self.reference_clear_last_pos_relative)
                 assigned.append(int(c))
                 remove_inactive.append(track)
                 self.tracks.append(track)

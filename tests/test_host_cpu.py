@@ -119,3 +119,18 @@ def test_nested_tensor_padding_and_sizes():
     assert nt.mask[0, :, 12:].all() and not nt.mask[0, :, :12].any()
     assert nt.mask[1, 8:].all() and not nt.mask[1, :8, :14].any()
     assert torch.equal(nt.tensors[1, :, :8, :14], b)
+
+
+def test_track_reset_last_pos_compat_switch():
+    """Track.reset_last_pos: by default the relative-position history survives a
+    re-identification; with the reference-compatibility switch it is cleared as in the
+    reference (tracker.py:1120-1124), whose next repeat_last_pos then raises IndexError."""
+    from kinet_amd.tracker import Track
+    t = Track(torch.tensor([0., 0., 2., 2.]), 0.9, 1, torch.zeros(4), 0, pos_rel=torch.tensor([0., 0., .1, .1]))
+    t.reset_last_pos()
+    t.repeat_last_pos()
+    assert len(t.last_pos_relative) == 2
+    t.reset_last_pos(clear_relative=True)
+    assert len(t.last_pos_relative) == 0
+    with pytest.raises(IndexError):
+        t.repeat_last_pos()

@@ -369,8 +369,9 @@ def _hm(offlog, M, L=4, P=4):
     (((25, 40), (15, 20), (8, 10), (4, 5)), 2, 4.0),         # every level staged (Lq > S)
     (((100, 167), (50, 84), (25, 42), (13, 21)), 2, 2.0),    # the config-2 geometry (800x1333)
 ])
-@pytest.mark.parametrize('out_dtype,masked', [(torch.bfloat16, False), (torch.float16, True)])
-def test_encoder_kernel_matches_fast_kernel(shapes, ref_dim, noise, out_dtype, masked):
+@pytest.mark.parametrize('out_dtype,masked,ordered', [(torch.bfloat16, False, True), (torch.float16, True, False),
+                                                      (torch.float16, True, True)])
+def test_encoder_kernel_matches_fast_kernel(shapes, ref_dim, noise, out_dtype, masked, ordered):
     """kinet_msda_encoder_forward against msda_fused_fast_kernel (flag 32) on the same f16
     offsets / logits (row-major for the fast kernel, head-major for the encoder kernel).
     Bound as test_encoder_lds_kernel_matches_fast_kernel (acc16): the tap weights are
@@ -385,7 +386,10 @@ def test_encoder_kernel_matches_fast_kernel(shapes, ref_dim, noise, out_dtype, m
                                                   dtype=torch.float16)
     offlog = offlog.half()
     qm = qmask if masked else None
-    o_enc = K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, qm, out_dtype=out_dtype)
+    # ordered: the encoder's row-sorted tile order (queries = the pixels of the levels)
+    S = sum(h * w for h, w in shapes)
+    order = K.encoder_tile_order(shapes, value.device) if ordered and Lq == S else None
+    o_enc = K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, qm, out_dtype=out_dtype, query_tile_order=order)
     lib = _native.lib()
     try:
         lib.kinet_msda_set_flags(32)
@@ -479,7 +483,7 @@ def test_encoder_kernel_rejects_unstaged_geometry():
     """Shapes whose coarsest level does not fit the LDS map are refused (the module falls back
     to kinet_msda_fused_forward: msda_encoder_supported is False for them)."""
     from kinet_amd import kernels as K
-    shapes = ((70, 80), (56, 60), (45, 50), (40, 40))
+    shapes = ((100, 110), (70, 80), (56, 60), (48, 50))
     B, M, P = 1, 8, 4
     Lq = sum(h * w for h, w in shapes)
     value, ss, offlog, ref, _ = _fused_inputs(B, shapes, Lq, M, P, 2, 1.0, 3, dtype=torch.float16)
