@@ -41,7 +41,7 @@ MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'f16': 2500.0, 'f32': 157.3}   # dense
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command
 # (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950 per MI355X_MICROARCH.md "HBM")
 PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
-MSDA_ENC_KERNEL = 'msda_enc_kernel'         # config-2 encoder calls (msda_enc.hip: coarse levels + a level-1 band in LDS)
+MSDA_ENC_KERNEL = 'msda_enc_kernel'         # config-2 encoder calls (msda_enc.hip: coarse levels in LDS)
 MSDA_KERNEL = 'msda_fused_fast_kernel'      # decoder calls
 
 WORKLOADS = {
@@ -74,8 +74,6 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=20.0, help='bound on the CPU baseline sample')
     ap.add_argument('--gemm-flags', type=int, default=0,
                     help='diagnostic kernel-selection flags (kinet_gemm_set_flags, csrc/gemm.hip) for A/B runs')
-    ap.add_argument('--msda-flags', type=int, default=0,
-                    help='diagnostic kernel-selection flags (kinet_msda_set_flags, csrc/msda.hip) for A/B runs')
     ap.add_argument('--cpu-stub', action='store_true',
                     help='tests only: run the launch/timing skeleton with a tiny CPU model over gloo')
     a = ap.parse_args()
@@ -387,8 +385,6 @@ def main():
     from kinet_amd.models import nested_tensor_from_tensor_list
     if a.gemm_flags:
         _native.lib().kinet_gemm_set_flags(a.gemm_flags)
-    if a.msda_flags:
-        _native.lib().kinet_msda_set_flags(a.msda_flags)
     model = build(dev, dtype, wl)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     # one independent batch per in-flight slot (distinct requests, all resident in HBM)
@@ -498,7 +494,7 @@ def main():
                         'algorithmic_bytes_per_launch': t_b / len(launches),
                         'avg_launch_ms': t_ms / len(launches), 'launches_per_step': len(launches) / 3}
             if a.workload == 'config2' and enc and dec:
-                msda_roof = roof(enc, MSDA_ENC_KERNEL + '<bf16_t, 2, 2, false, true> (encoder launches, Lq = S = %d)'
+                msda_roof = roof(enc, MSDA_ENC_KERNEL + '<bf16_t, 2, 2, false> (encoder launches, Lq = S = %d)'
                                  % enc[0][0], MSDA_ENC_KERNEL)
                 msda_roof['decoder_kernel'] = roof(dec, MSDA_KERNEL + '<f16_t, bf16_t, f16_t, 4, 4> (decoder launches)',
                                                    MSDA_KERNEL)

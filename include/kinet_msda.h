@@ -80,10 +80,8 @@ int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num
  *                 16-query tiles giving the order the specialised kernels process them in
  *                 (outputs unchanged); the encoder passes its tiles sorted by image row across
  *                 levels so the value rows they share are fetched into L2 once.
- * Encoder-sized calls (num_query >= 2048 per frame, F16 head-major values with head_dim 32,
- * L = 4, P = 4, loc_out == NULL) run with the coarse levels of each head staged in LDS; there
- * each level's 16 bilinear taps are summed as f16 pairs (11-bit significand) before the f32
- * sum, tap weights are f16 as on every 16-bit path. */
+ * (Encoder-sized calls with their level shapes on the host are faster through
+ * kinet_msda_encoder_forward, below.) */
 int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_ss, int64_t value_sm,
                              const int64_t* spatial_shapes,
                              const void* offsets_logits, int ld_off,
@@ -117,12 +115,6 @@ int kinet_msda_encoder_forward(const void* value, int64_t value_sb, int64_t valu
                                void* output, int batch, int spatial_size, int num_heads, int channels,
                                int num_levels, int num_query, int num_point, int output_dtype,
                                const int32_t* query_tile_order, kinet_stream_t stream);
-
-/* Diagnostic kernel-selection knob (no reference counterpart, A/B timing only): bit 0 = never
- * use the specialised 16-bit / head_dim-32 fused kernels; bit 5 = no LDS-staged encoder
- * kernel; bit 6 = that kernel with every tap product summed in f32; bit 7 = two rounds of its
- * workgroups.  Bits 3-4 select backward-kernel variants.  Returns the previous flags. */
-int kinet_msda_set_flags(int flags);
 
 #ifdef __cplusplus
 }

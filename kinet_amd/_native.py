@@ -22,7 +22,6 @@ _SIGS = {
     'kinet_msda_forward': [P, P, P, P, P] + [I] * 10 + [P],
     'kinet_msda_backward': [P] * 9 + [I] * 10 + [P],
     'kinet_msda_backward_workspace_bytes': [I] * 5,
-    'kinet_msda_set_flags': [I],
     'kinet_msda_encoder_forward': [P, I64, I64, P, P, P, I, P, P] + [I] * 8 + [P, P],
     'kinet_msda_fused_forward': [P, I64, I64, I64, P, P, I, P, I, P, P, P, P] + [I] * 10 + [P, P],
     'kinet_gemm_set_flags': [I],

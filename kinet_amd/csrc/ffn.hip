@@ -45,7 +45,7 @@ struct FfnArgs {
                // prologue (results are garbage)
 };
 
-int ffn_debug = 0;
+thread_local int ffn_debug = 0;   // test-only knob (kinet_ffn_set_debug), per calling thread
 
 template <int D>
 struct FfnGeo {

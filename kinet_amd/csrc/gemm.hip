@@ -42,10 +42,12 @@ namespace {
 // multi-tap convolutions; 128 = KINET_F32_X3 weight-gradient GEMM splitting at fragment-read time;
 // 256 = no XCD placement of that GEMM's K-slices; 512 = the wave-per-row attention backward
 }  // namespace
-int kinet_gemm_flags = 0;   // declared in gemm_common.h (read by grad.hip too)
+// test / A-B selection knobs (kinet_gemm_set_flags, kinet_gemm_force_tile): per calling thread,
+// never read by default paths except as "0 = automatic"
+thread_local int kinet_gemm_flags = 0;   // declared in gemm_common.h (read by grad.hip too)
 namespace {
 // diagnostic tile override for gemm_kernel (kinet_gemm_force_tile; 0 = heuristic)
-int force_bm = 0, force_bn = 0;
+thread_local int force_bm = 0, force_bn = 0;
 
 
 template <int BM, int BN>

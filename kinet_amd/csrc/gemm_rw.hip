@@ -458,7 +458,7 @@ bool al16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
 
 }  // namespace
 
-int rw_min_m = 4096;   // smallest M routed to the resident-weight kernel (kinet_gemm_set_flags bit 3: 256)
+thread_local int rw_min_m = 4096;   // smallest M routed to the resident-weight kernel (kinet_gemm_set_flags bit 3: 256)
 
 // Entry from gemm.hip's dispatcher: launch the resident-weight kernel when the problem
 // fits it; false leaves the call to the tiled kernel.

@@ -36,10 +36,6 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxLevels = 16;
 
-// diagnostic flags (kinet_msda_set_flags): bit 0 = never use msda_fused_fast_kernel; bit 5 = never use msda_enc_lds_kernel (encoder calls then take msda_fused_fast_kernel); bit 6 =
-// msda_enc_lds_kernel with every tap product accumulated in f32 (no f16 per-level partial sums);
-// bit 7 = twice as many query chunks per head map (two rounds of workgroups; timing studies)
-int msda_flags = 0;
 
 struct LevelInfo {
     int start[kMaxLevels];
@@ -680,438 +676,6 @@ __global__ __launch_bounds__(MH * 64) void msda_fused_fast_kernel(
 }
 
 // ---------------------------------------------------------------------------------
-// encoder forward: the coarse levels of one head map resident in LDS
-// ---------------------------------------------------------------------------------
-// msda_fused_fast_kernel gathers every bilinear corner through the texture path (TA/L1,
-// 64 B per clock per CU): at the config-2 encoder shape that is 11.6 GB of 64-byte corner
-// rows per batch-16 call, a ~300 us floor that no ordering of the queries removes.  The
-// coarse levels are small -- 25x42 + 13x21 pixels of one head at 800x1333, 84.7 KB -- yet
-// they receive half of all taps (every query samples every level with P points).  So one
-// workgroup owns one (frame, head) map and a run of query tiles, stages the coarse levels
-// of that head in LDS once (plus one zero row for out-of-image corners), and serves their
-// taps with ds_read_b128 (256 B per clock per CU); only the fine levels go through the
-// texture path.  Per (query, head) the arithmetic and its order are those of
-// msda_fused_fast_kernel except that the fine-level and the LDS-level taps accumulate in
-// two f32 sums added at the end (so the two streams of taps overlap).
-//  * 16 waves per workgroup, one workgroup per CU (LDS: 94 KB map + 64 KB tap records);
-//  * head-major values (M, B, S, 32): a pixel row is 64 B.  A tap record is 16 B: the byte
-//    offsets of the sample's top-left corner and of the corner below it (the right corners
-//    are +64 B, an immediate offset) + the four f16 corner weights.  A corner outside the
-//    level keeps its address -- a neighbouring pixel, a zero margin row of the LDS map, or
-//    past the buffer's range, which reads 0 -- and gets weight 0; a sample outside the level
-//    points past the range (global) or at the top margin (LDS) with all weights 0;
-//  * records are wave-private, stored sample-major with the query index XORed by the
-//    sample index, so neither the phase-1 stores (8 consecutive samples of one query per
-//    lane group) nor the phase-2 broadcast reads (one sample of 4 queries per group) hit
-//    the same banks twice;
-//  * the staged levels are the coarsest suffix that fits (decided per workgroup from
-//    spatial_shapes, identical everywhere); global and LDS samples are interleaved in
-//    pairs so LDS reads and FMAs fill the gather latency.
-constexpr int kEncWaves = 16;
-constexpr int kEncMapRows = 1472;      // staged pixels incl. the zero margins (94,208 B)
-constexpr int kEncMinQueries = 2048;   // per frame; fewer queries do not amortise the staging
-
-template <typename T>
-__device__ __forceinline__ void mac_sample(f32x2 (&acc)[4], const u32x4v (&v)[4], uint32_t w01, uint32_t w23) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t wp = k < 2 ? w01 : w23;
-        if constexpr (std::is_same<T, f16_t>::value) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                acc[j][0] = (k & 1) ? fma_mix16_lo_hi(acc[j][0], v[k][j], wp) : fma_mix16_lo_lo(acc[j][0], v[k][j], wp);
-                acc[j][1] = (k & 1) ? fma_mix16_hi_hi(acc[j][1], v[k][j], wp) : fma_mix16_hi_lo(acc[j][1], v[k][j], wp);
-            }
-        } else {
-            const float wk = (float)__builtin_bit_cast(f16_t, (uint16_t)((k & 1) ? (wp >> 16) : (wp & 0xffffu)));
-            const f32x2 w2 = {wk, wk};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                f32x2 x;
-                widen2<T>(v[k][j], x);
-                acc[j] = __builtin_elementwise_fma(x, w2, acc[j]);
-            }
-        }
-    }
-}
-
-struct EncStage {
-    int lc;       // first LDS-resident level (4: none)
-    int mstart;   // its token offset in the head map
-    int npix;     // staged pixels
-    int mtop;     // zero rows before them (= zero rows after them): max staged W + 1
-};
-
-// acc(2 x f16) += v(2 x f16) * (lo or hi half of w, both lanes): one v_pk_fma_f16 per 2 MACs
-__device__ __forceinline__ uint32_t pk_fma_wlo(uint32_t acc, uint32_t v, uint32_t w) {
-    asm("v_pk_fma_f16 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "v"(v), "v"(w));
-    return acc;
-}
-__device__ __forceinline__ uint32_t pk_fma_whi(uint32_t acc, uint32_t v, uint32_t w) {
-    asm("v_pk_fma_f16 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(v), "v"(w));
-    return acc;
-}
-
-__device__ __forceinline__ uint32_t pk_mul_wlo(uint32_t v, uint32_t w) {
-    uint32_t d;
-    asm("v_pk_mul_f16 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(d) : "v"(v), "v"(w));
-    return d;
-}
-
-// corners 1-3 of a level's first sample (corner 0 started the sum with a multiply)
-__device__ __forceinline__ void mac_sample16_tail(uint32_t (&h)[4], const u32x4v (&v)[4], uint32_t w01, uint32_t w23) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        h[j] = pk_fma_whi(h[j], v[1][j], w01);
-        h[j] = pk_fma_wlo(h[j], v[2][j], w23);
-        h[j] = pk_fma_whi(h[j], v[3][j], w23);
-    }
-}
-
-// one sample's 4 corners x 8 channels into the running f16 pairs of its level
-__device__ __forceinline__ void mac_sample16(uint32_t (&h)[4], const u32x4v (&v)[4], uint32_t w01, uint32_t w23) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        h[j] = pk_fma_wlo(h[j], v[0][j], w01);
-        h[j] = pk_fma_whi(h[j], v[1][j], w01);
-        h[j] = pk_fma_wlo(h[j], v[2][j], w23);
-        h[j] = pk_fma_whi(h[j], v[3][j], w23);
-    }
-}
-
-// a level's f16 partial sums into the f32 accumulators (v_fma_mix with an f16 1.0)
-__device__ __forceinline__ void flush16(f32x2 (&acc)[4], uint32_t (&h)[4]) {
-    constexpr uint32_t one = 0x3c003c00u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        acc[j][0] = fma_mix16_lo_lo(acc[j][0], h[j], one);
-        acc[j][1] = fma_mix16_hi_lo(acc[j][1], h[j], one);
-    }
-}
-
-// ACC16: the 16 bilinear taps of one level (P points x 4 corners) are summed as f16 pairs
-// by v_pk_fma_f16 (2 MACs per instruction, 11-bit significand -- above the bf16 compute
-// dtype's 8) and each level's sum is added into f32; 0: every tap product accumulated in
-// f32 by v_fma_mix_f32, as msda_fused_fast_kernel.
-template <typename T, typename TO, typename TL, int LC, bool ACC16, int REFD>
-__device__ __forceinline__ void enc_lds_tiles(const FastLevels& lv, const EncStage& st, const u32x4v* vmap,
-                                              uint4* wrec, const __amdgpu_buffer_rsrc_t& rv,
-                                              const __amdgpu_buffer_rsrc_t& ro, int ld_off,
-                                              const __amdgpu_buffer_rsrc_t& rr, const __amdgpu_buffer_rsrc_t& rq,
-                                              TO* __restrict__ out,
-                                              int b, int m, int M, int Lq, const int* __restrict__ torder, int chunk,
-                                              int nchunk, int ntile, int wave, int lane) {
-    constexpr int L = 4, P = 4, LP = 16, D = 32, QT = 16, NW = kEncWaves;
-    constexpr int NG = LC * P, NL = LP - NG;
-    // phase-1 lane constants, hoisted out of the tile loop: lane = (query lane >> 2, level
-    // lane & 3) and handles that level's P = 4 points, so one tile is one round of 64 lanes
-    // with 3 vector loads per lane (the 4 points' offsets, their logits, the reference point)
-    const int l = lane & 3, qi = lane >> 2;
-    const bool in_lds = l >= LC;
-    const int H = lv.H[l], W = lv.W[l];
-    // byte offset of the level's pixel (0, 0) and of one pixel: the head map (64-byte rows,
-    // head-major D = 32) or the LDS map (zero margin rows, then the staged levels)
-    const int pbase = in_lds ? (st.mtop + lv.start[l] - st.mstart) * 64 : lv.start[l] * 64;
-    const int wbytes = W * 64;
-    const float Hf = lv.Hf[l], Wf = lv.Wf[l], rH = lv.rH[l], rW = lv.rW[l];
-    const bool lok = lv.ok[l] != 0;
-    // a sample outside the level: every corner read returns zero (global: past the buffer's
-    // range; LDS: the top margin rows) and every weight is 0
-    const uint32_t zoff = in_lds ? 0u : 0x80000000u;
-    const uint32_t rowstride = (uint32_t)ld_off * (uint32_t)sizeof(TL);
-    const uint32_t lg_off = (uint32_t)(M * LP * 2 + m * LP + l * P) * (uint32_t)sizeof(TL);
-    const uint32_t of_off = (uint32_t)((m * LP + l * P) * 2) * (uint32_t)sizeof(TL);
-    const float rscale = 0.5f / (float)P;
-    // this workgroup's 16-tile groups are chunk, chunk + nchunk, ...: the workgroups of one
-    // head map sweep the (row-ordered) tiles side by side and share its rows in L2
-    for (int t = chunk * NW + wave; t < ntile; t += nchunk * NW) {
-        const int bx = torder ? torder[t] : t;
-        const int q0 = bx * QT;
-        // the previous tile's record reads are done before this tile overwrites them
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        // phase 1, branch-free, 32-bit buffer offsets (a query past Lq reads row Lq - 1 and
-        // ends with zero weights)
-        const int q = q0 + qi;
-        const bool ok = q < Lq;
-        const uint32_t row = (uint32_t)(b * Lq + (ok ? q : Lq - 1));
-        const uint32_t ob = __umul24(row, rowstride);   // row < 2^24 (host check)
-        float lg[P], ox[P], oy[P];
-        if constexpr (std::is_same<TL, float>::value) {
-            const u32x4v o0 = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(ro, ob + of_off, 0, 0));
-            const u32x4v o1 = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(ro, ob + of_off + 16, 0, 0));
-            const u32x4v g4 = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(ro, ob + lg_off, 0, 0));
-#pragma unroll
-            for (int p = 0; p < P; ++p) {
-                const u32x4v& o = p < 2 ? o0 : o1;
-                ox[p] = __uint_as_float(o[(p & 1) * 2]);
-                oy[p] = __uint_as_float(o[(p & 1) * 2 + 1]);
-                lg[p] = __uint_as_float(g4[p]);
-            }
-        } else {
-            const u32x4v o = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(ro, ob + of_off, 0, 0));
-            const uint2 g = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ro, ob + lg_off, 0, 0));
-#pragma unroll
-            for (int p = 0; p < P; ++p) {
-                ox[p] = (float)__builtin_bit_cast(f16_t, (uint16_t)(o[p] & 0xffffu));
-                oy[p] = (float)__builtin_bit_cast(f16_t, (uint16_t)(o[p] >> 16));
-                const uint32_t gw = p < 2 ? g.x : g.y;
-                lg[p] = (float)__builtin_bit_cast(f16_t, (uint16_t)((p & 1) ? (gw >> 16) : (gw & 0xffffu)));
-            }
-        }
-        const uint32_t rb = (row * (uint32_t)L + (uint32_t)l) * (uint32_t)REFD * 4u;
-        float rx, ry, rw = 0.f, rh = 0.f;
-        if constexpr (REFD == 2) {
-            const float2 r2 = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rr, rb, 0, 0));
-            rx = r2.x;
-            ry = r2.y;
-        } else {
-            const float4 r4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rr, rb, 0, 0));
-            rx = r4.x;
-            ry = r4.y;
-            rw = r4.z;
-            rh = r4.w;
-        }
-        // query mask byte (a buffer of 0 records when there is no mask: reads 0)
-        const uint32_t qm = __builtin_amdgcn_raw_buffer_load_b8(rq, row, 0, 0);
-        // softmax over the query's 16 logits: 4 in this lane, 4 lanes (ms_deform_attn.py:71-72)
-        float mx = fmaxf(fmaxf(lg[0], lg[1]), fmaxf(lg[2], lg[3]));
-        mx = group_reduce<4, true>(mx);
-        float e[P], es = 0.f;
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-            e[p] = __expf(lg[p] - mx);
-            es += e[p];
-        }
-        es = group_reduce<4, false>(es);
-        // ms_deform_attn.py:73-74; a query past Lq gets weight 0
-        const float ra = (qm || !ok) ? 0.f : __builtin_amdgcn_rcpf(es);
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-            const int lp = l * P + p;
-            float x, y;
-            if constexpr (REFD == 2) {   // offsets / spatial_shapes[(H, W)] on (x, y): the reference's quirk (:77-79)
-                x = rx + ox[p] * rH;
-                y = ry + oy[p] * rW;
-            } else {                     // :80-82
-                x = rx + ox[p] * rscale * rw;
-                y = ry + oy[p] * rscale * rh;
-            }
-            const float a = e[p] * ra;
-            const float h = y * Hf - 0.5f, w = x * Wf - 0.5f;                    // cuh:227-228
-            const bool valid = lok && h > -1.f && w > -1.f && h < Hf && w < Wf;   // cuh:229
-            const float hf = floorf(h), wf = floorf(w);
-            const int hl = valid ? (int)hf : 0, wl = valid ? (int)wf : 0;
-            const float lh = h - hf, lw = w - wf, hh = 1.f - lh, hw = 1.f - lw;
-            const bool h0 = hl >= 0, h1 = hl + 1 < H, c0 = wl >= 0, c1 = wl + 1 < W;
-            // record: byte offsets of the top-left corner and of the one below it (the right
-            // corners are +64 B); a corner outside the level keeps its address -- a
-            // neighbouring pixel, a margin row, or past the buffer's range (reads 0) -- and
-            // gets weight 0
-            const uint32_t o00 = valid ? (uint32_t)(pbase + (__mul24(hl, W) + wl) * 64) : zoff;
-            const float av = valid ? a : 0.f;
-            // corner weights associated as msda_fused_fast_kernel's
-            const float w0 = (h0 && c0) ? hh * hw * av : 0.f, w1 = (h0 && c1) ? hh * lw * av : 0.f;
-            const float w2 = (h1 && c0) ? lh * hw * av : 0.f, w3 = (h1 && c1) ? lh * lw * av : 0.f;
-            wrec[lp * QT + (qi ^ lp)] = make_uint4(o00, o00 + (uint32_t)wbytes, pack_f16x2(w0, w1), pack_f16x2(w2, w3));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-
-        // phase 2: 4 lanes x 8 channels per query.  The fine-level samples stream through two
-        // register slots -- sample k + 1's four corner rows are in flight while sample k is
-        // accumulated -- and one LDS-level sample is read and accumulated per step to fill the
-        // gather latency.
-        const int qo = qi;   // phase 2's query of this lane is phase 1's
-        const unsigned cb = (unsigned)(lane & 3) * 16u;
-        const int cq = lane & 3;
-        // ACC16: one f32 sum (the level sums are added in a fixed order); otherwise the
-        // fine-level and the LDS-level taps accumulate in two f32 sums
-        f32x2 accg[4] = {}, accl[4] = {};
-        uint32_t hg[4], hl16[4];
-        constexpr int NMAX = NG > NL ? NG : NL;
-        const char* vm = reinterpret_cast<const char*>(vmap) + cb;
-        auto issue = [&](int s, u32x4v (&v)[4], uint4& rg) {
-            rg = wrec[s * QT + (qo ^ s)];
-            const uint32_t a0 = rg.x + cb, a1 = rg.y + cb;
-            v[0] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, a0, 0, 0));
-            v[1] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, a0 + 64u, 0, 0));
-            v[2] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, a1, 0, 0));
-            v[3] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, a1 + 64u, 0, 0));
-        };
-        // POS: the sample's point index within its level (0 starts the level's f16 sum with a
-        // multiply, P - 1 adds it into f32)
-        auto mac = [&](auto pos, uint32_t (&h)[4], f32x2 (&acc)[4], const u32x4v (&v)[4], uint32_t w01,
-                       uint32_t w23) {
-            constexpr int POS = decltype(pos)::value;
-            if constexpr (ACC16) {
-                if constexpr (POS == 0) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) h[j] = pk_mul_wlo(v[0][j], w01);
-                    mac_sample16_tail(h, v, w01, w23);
-                } else {
-                    mac_sample16(h, v, w01, w23);
-                }
-                if constexpr (POS == P - 1) flush16(accg, h);
-            } else {
-                mac_sample<T>(acc, v, w01, w23);
-            }
-        };
-        auto lds_sample = [&](auto pos, int s) {
-            const uint4 rl = wrec[s * QT + (qo ^ s)];
-            u32x4v vl[4];
-            vl[0] = *reinterpret_cast<const u32x4v*>(vm + rl.x);
-            vl[1] = *reinterpret_cast<const u32x4v*>(vm + rl.x + 64);
-            vl[2] = *reinterpret_cast<const u32x4v*>(vm + rl.y);
-            vl[3] = *reinterpret_cast<const u32x4v*>(vm + rl.y + 64);
-            mac(pos, hl16, accl, vl, rl.z, rl.w);
-        };
-        using I0 = std::integral_constant<int, 0>;
-        using I1 = std::integral_constant<int, 1>;
-        using I2 = std::integral_constant<int, 2>;
-        using I3 = std::integral_constant<int, 3>;
-        u32x4v va[4], vb[4];
-        uint4 rca, rcb;
-        if constexpr (NG > 0) issue(0, va, rca);
-        // one level of each stream per step (P = 4 samples), steps kept rolled: unrolled, the
-        // compiler hoists later gathers and spills
-        static_assert(P == 4 && NG % P == 0 && NL % P == 0, "levels of 4 points");
-#pragma unroll 1
-        for (int k = 0; k < NMAX; k += 4) {
-            if (k + 1 < NG) issue(k + 1, vb, rcb);
-            if (k < NL) lds_sample(I0{}, NG + k);
-            if (k < NG) mac(I0{}, hg, accg, va, rca.z, rca.w);
-            if (k + 2 < NG) issue(k + 2, va, rca);
-            if (k + 1 < NL) lds_sample(I1{}, NG + k + 1);
-            if (k + 1 < NG) mac(I1{}, hg, accg, vb, rcb.z, rcb.w);
-            __builtin_amdgcn_sched_barrier(0);   // keep the halves apart (register pressure)
-            if (k + 3 < NG) issue(k + 3, vb, rcb);
-            if (k + 2 < NL) lds_sample(I2{}, NG + k + 2);
-            if (k + 2 < NG) mac(I2{}, hg, accg, va, rca.z, rca.w);
-            if (k + 4 < NG) issue(k + 4, va, rca);
-            if (k + 3 < NL) lds_sample(I3{}, NG + k + 3);
-            if (k + 3 < NG) mac(I3{}, hg, accg, vb, rcb.z, rcb.w);
-        }
-        if (q < Lq) {
-            VecT<TO, 8> o;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if constexpr (ACC16) {
-                    o.v[2 * j] = Cvt<TO>::from(accg[j][0]);
-                    o.v[2 * j + 1] = Cvt<TO>::from(accg[j][1]);
-                } else {
-                    o.v[2 * j] = Cvt<TO>::from(accg[j][0] + accl[j][0]);
-                    o.v[2 * j + 1] = Cvt<TO>::from(accg[j][1] + accl[j][1]);
-                }
-            }
-            *reinterpret_cast<VecT<TO, 8>*>(out + ((long)b * Lq + q) * M * D + (long)m * D + cq * 8) = o;
-        }
-    }
-}
-
-template <typename T, typename TO, typename TL, bool ACC16>
-__global__ __launch_bounds__(kEncWaves * 64) void msda_enc_lds_kernel(
-    const T* __restrict__ value, long vsb, int vss, long vsm, int head_bytes, const int64_t* __restrict__ shapes,
-    const TL* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
-    const uint8_t* __restrict__ qmask, TO* __restrict__ out, int S, int B, int M, int Lq,
-    const int* __restrict__ torder, int nchunk) {
-    static_assert(sizeof(T) == 2 && sizeof(TO) == 2, "16-bit values and output");
-    constexpr int L = 4, QT = 16, LP = 16, NT = kEncWaves * 64;
-    __shared__ FastLevels lv;
-    __shared__ EncStage st;
-    __shared__ u32x4v vmap[kEncMapRows * 4];
-    __shared__ uint4 rec[kEncWaves * QT * LP];
-    // XCD-aware remap (cdna_hip_programming.md T1): the query chunks of one (frame, head)
-    // map run on one XCD and share its L2
-    int b, m, chunk;
-    {
-        const int nblk = gridDim.x, lin = blockIdx.x;
-        const int qd = nblk >> 3, rm = nblk & 7, xcd = lin & 7;
-        const int nid = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + (lin >> 3);
-        chunk = nid % nchunk;
-        const int bm = nid / nchunk;
-        b = bm / M;
-        m = bm % M;
-    }
-    (void)B;
-    if (threadIdx.x == 0) {
-        long long acc = 0;
-        for (int l = 0; l < L; ++l) {
-            const long long H = shapes[2 * l], W = shapes[2 * l + 1];
-            lv.start[l] = (int)acc;
-            lv.H[l] = (int)H;
-            lv.W[l] = (int)W;
-            lv.ok[l] = (H > 0 && W > 0 && acc + H * W <= S) ? 1 : 0;
-            lv.Hf[l] = (float)H;
-            lv.Wf[l] = (float)W;
-            lv.rH[l] = H > 0 ? 1.f / (float)H : 0.f;
-            lv.rW[l] = W > 0 ? 1.f / (float)W : 0.f;
-            acc += H * W;
-        }
-        // the coarsest suffix of levels that fits the map with its zero margins (max W + 1
-        // rows before and after: the rows a corner of an edge pixel can address)
-        int lc = L, npix = 0, wmax = 0;
-        for (int l = L - 1; l >= 0; --l) {
-            if (!lv.ok[l]) break;
-            const long long np = (long long)npix + (long long)lv.H[l] * lv.W[l];
-            const int wm = lv.W[l] > wmax ? lv.W[l] : wmax;
-            if (np + 2LL * (wm + 1) > kEncMapRows) break;
-            npix = (int)np;
-            wmax = wm;
-            lc = l;
-        }
-        st.lc = lc;
-        st.mstart = lc < L ? lv.start[lc] : 0;
-        st.npix = npix;
-        st.mtop = lc < L ? wmax + 1 : 0;
-    }
-    __syncthreads();
-    const int rowb = vss * (int)sizeof(T);
-    const char* hmap = reinterpret_cast<const char*>(value + (long)b * vsb + (long)m * vsm);
-    {
-        const int npix = st.npix, mstart = st.mstart, mtop = st.mtop;
-        const int rows = npix + 2 * mtop;
-        for (int i = threadIdx.x; i < rows * 4; i += NT) {
-            const int p = (i >> 2) - mtop;
-            u32x4v v = {0u, 0u, 0u, 0u};
-            if (p >= 0 && p < npix) v = *reinterpret_cast<const u32x4v*>(hmap + (long)(mstart + p) * rowb + (i & 3) * 16);
-            vmap[i] = v;
-        }
-    }
-    __syncthreads();
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)hmap, (short)0, head_bytes, 0x00020000);
-    const int ntile = (Lq + QT - 1) / QT;
-    uint4* wrec = rec + wave * (QT * LP);
-    const int ldn = ld_off * (int)sizeof(TL);
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)offlog, (short)0, B * Lq * ldn, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)ref, (short)0, B * Lq * L * ref_dim * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rq =
-        __builtin_amdgcn_make_buffer_rsrc((void*)qmask, (short)0, qmask ? B * Lq : 0, 0x00020000);
-#define ENC_TILES(LCV, RD)                                                                                     \
-    enc_lds_tiles<T, TO, TL, LCV, ACC16, RD>(lv, st, vmap, wrec, rv, ro, ld_off, rr, rq, out, b, m, M, Lq,       \
-                                             torder, chunk, nchunk, ntile, wave, lane)
-#define ENC_LC(RD)                               \
-    switch (st.lc) {                             \
-        case 0: ENC_TILES(0, RD); break;         \
-        case 1: ENC_TILES(1, RD); break;         \
-        case 2: ENC_TILES(2, RD); break;         \
-        case 3: ENC_TILES(3, RD); break;         \
-        default: ENC_TILES(4, RD); break;        \
-    }
-    if (ref_dim == 2) {
-        ENC_LC(2)
-    } else {
-        ENC_LC(4)
-    }
-#undef ENC_LC
-#undef ENC_TILES
-}
-
-// ---------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------
 template <typename A>
@@ -1376,10 +940,9 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
     }
     if (nval) KINET_CHECK_HIP(hipMemsetAsync(acc_buf, 0, nval * sizeof(GA), stream));
     if (N > 0 && Lq > 0) {
-        // groups padded to a power of two (reductions by shuffles instead of LDS atomics) unless
-        // flag 8 asks for the packed groups
+        // groups padded to a power of two (reductions by shuffles instead of LDS atomics)
         int lpq = c.lpq, qt = c.qt;
-        if ((lpq & (lpq - 1)) != 0 && !(msda_flags & 8)) {
+        if ((lpq & (lpq - 1)) != 0) {
             int p2 = 1;
             while (p2 < lpq) p2 <<= 1;
             if (p2 <= 64 && (kThreads / p2) / M >= 1) {
@@ -1388,8 +951,7 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
             }
         }
         const bool pow2 = (lpq & (lpq - 1)) == 0 && lpq <= 64;
-        const bool aln = sizeof(GA) == 4 && lpq == 16 && c.vec == 4 && (M * D) % 16 == 0 && D <= 48 &&
-                         !(msda_flags & 16);
+        const bool aln = sizeof(GA) == 4 && lpq == 16 && c.vec == 4 && (M * D) % 16 == 0 && D <= 48;
         const size_t nsamp = (size_t)qt * M * L * P;
         const size_t lds = sizeof(LevelInfo) + nsamp * sizeof(BwdTap<Acc>) + (pow2 ? 0 : nsamp * 3 * sizeof(Acc));
         KINET_CHECK_ARG(lds <= 160 * 1024, "msda backward: LDS request %zu too large", lds);
@@ -1463,54 +1025,9 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
         // specialised kernel: head_dim 32, (L, P) in {(4, 4), (8, 4)}, 16-byte aligned vectors
         const long long head_bytes = ((long long)(S - 1) * vss + D) * (long long)sizeof(T);
         if (D == 32 && P == 4 && (L == 4 || L == 8) && vss % 8 == 0 && vsb % 8 == 0 && vsm % 8 == 0 &&
-            ((uintptr_t)value % 16) == 0 && head_bytes < (1LL << 31) && !(msda_flags & 1)) {
+            ((uintptr_t)value % 16) == 0 && head_bytes < (1LL << 31)) {
             dim3 grid((Lq + 15) / 16, N, (M + 3) / 4);
-            const int ntile = (Lq + 15) / 16;
-            bool enc_lds = false;
-            if constexpr (std::is_same<T, f16_t>::value) {
-                // encoder-sized call with f16 values (the perf path; the bf16-value variant
-                // needs the widened pairs and spills at 128 VGPRs): coarse levels from LDS,
-                // one workgroup per CU, enough query chunks per (frame, head) map to give
-                // every CU one workgroup
-                if (L == 4 && loc_out == nullptr && Lq >= kEncMinQueries && vss == 32 && !(msda_flags & 32) &&
-                    (long long)N * Lq * ld_off * (long long)sizeof(TL) < (1LL << 31) && (long long)N * Lq < (1LL << 24) &&
-                    (long long)N * Lq * L * ref_dim * 4LL < (1LL << 31)) {
-                    const int maps = N * M;
-                    // one round of one-per-CU workgroups.  Flag 128: two rounds, half as many
-                    // head maps in flight per XCD, whose fine-level rows then stay in its L2
-                    // (config 2, batch 16, alone: HBM fetch 0.88 -> 0.65 GB per call = the
-                    // compulsory bytes, 354 -> 351 us), but under the bench's 3-stream
-                    // concurrency its second round waits for whole CUs (rocprof: 402 vs 346 us)
-                    // (the fewest chunks whose workgroups fill >= 90 % of their last round: at
-                    // batch 24, 192 maps x 2 = 1.5 rounds took 628 us for 1.5x the work of
-                    // batch 16's 342)
-                    const int base = (256 + maps - 1) / maps;
-                    int nchunk = base;
-                    for (int c = base; c <= 4 * base; ++c) {
-                        const long long wgs = (long long)maps * c, rounds = (wgs + 255) / 256;
-                        if (wgs * 10 >= rounds * 256 * 9) {
-                            nchunk = c;
-                            break;
-                        }
-                    }
-                    if (msda_flags & 128) nchunk *= 2;
-                    nchunk = std::max(1, std::min(nchunk, ntile / kEncWaves));
-                    KINET_CHECK_ARG((long long)maps * nchunk < (1LL << 31), "msda fused: grid too large");
-                    if (msda_flags & 64)
-                        hipLaunchKernelGGL((msda_enc_lds_kernel<T, TO, TL, false>), dim3(maps * nchunk),
-                                           dim3(kEncWaves * 64), 0, stream, (const T*)value, vsb, vss, vsm,
-                                           (int)head_bytes, shapes, (const TL*)offlog_v, ld_off, ref, ref_dim, qmask,
-                                           (TO*)out, S, N, M, Lq, torder, nchunk);
-                    else
-                        hipLaunchKernelGGL((msda_enc_lds_kernel<T, TO, TL, true>), dim3(maps * nchunk),
-                                           dim3(kEncWaves * 64), 0, stream, (const T*)value, vsb, vss, vsm,
-                                           (int)head_bytes, shapes, (const TL*)offlog_v, ld_off, ref, ref_dim, qmask,
-                                           (TO*)out, S, N, M, Lq, torder, nchunk);
-                    enc_lds = true;
-                }
-            }
-            if (enc_lds) {
-            } else if (L == 4) {
+            if (L == 4) {
                 // 2 heads (waves) per workgroup, 2 samples per gather group: 12.5 KiB LDS and
                 // 52 VGPRs, 12 workgroups per CU (encoder call 271 -> 258 us vs 4 heads x 4)
                 dim3 g2((Lq + 15) / 16, N, (M + 1) / 2);
@@ -1557,12 +1074,6 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
 }
 }  // namespace
 }  // namespace kinet
-
-extern "C" int kinet_msda_set_flags(int flags) {
-    const int old = kinet::msda_flags;
-    kinet::msda_flags = flags;
-    return old;
-}
 
 extern "C" int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_ss, int64_t value_sm,
                                         const int64_t* spatial_shapes, const void* offsets_logits, int ld_off,

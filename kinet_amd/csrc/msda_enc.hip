@@ -332,7 +332,8 @@ __global__ __launch_bounds__(EW * 64) void msda_enc_kernel(const EncArgs a) {
     __shared__ EncLevels lv;
     __shared__ u32x4v vmap[EMAP_ROWS * 4];
     // XCD-aware remap (cdna_hip_programming.md T1): the query chunks of one (frame, head)
-    // map run on one XCD and share its L2
+    // map run on one XCD and share its L2.  Assumes MI355X's 8 XCDs with round-robin dispatch;
+    // elsewhere the mapping is still a bijection (only the L2 grouping is lost).
     int b, m, chunk;
     {
         const int nblk = gridDim.x, lin = blockIdx.x;

@@ -708,7 +708,7 @@ namespace kinet {
 bool launch_mha_mfma(const void* Q, int ldq, const void* Kt, int ldk, const void* V, int ldv, void* O, int ldo,
                      int batch, int Lq, int Lk, int heads, int head_dim, float scale, int dtype,
                      const uint8_t* key_mask, hipStream_t stream);
-int mha_use_mfma = 1;
+thread_local int mha_use_mfma = 1;   // test-only knob (kinet_mha_set_mfma), per calling thread
 }  // namespace kinet
 
 extern "C" int kinet_mha_set_mfma(int enable) {

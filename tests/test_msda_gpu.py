@@ -161,19 +161,17 @@ def _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, seed, dtype=torch.bfloat1
 ])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
 def test_fast_fused_kernel_matches_generic(shapes, Lq, ref_dim, noise, dtype):
-    from kinet_amd import _native
+    """The specialised 16-bit kernel (msda_fused_fast_kernel) against the generic fused kernel
+    run in f32 on the same values (exactly representable in f32): locations and attention
+    weights to a few ulp, outputs within one 16-bit output rounding plus the f16 tap-weight
+    quantisation (2^-11 relative per weight)."""
     from kinet_amd import kernels as K
     B, M, P = 2, 8, 4
     value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, Lq, dtype)
     L = len(shapes)
-    lib = _native.lib()
-    try:
-        lib.kinet_msda_set_flags(0)
-        out_f, loc_f, aw_f = K.msda_fused(value, ss, offlog, ref, M, L, P, qmask, want_loc_attw=True, head_major=True)
-        lib.kinet_msda_set_flags(1)
-        out_g, loc_g, aw_g = K.msda_fused(value, ss, offlog, ref, M, L, P, qmask, want_loc_attw=True, head_major=True)
-    finally:
-        lib.kinet_msda_set_flags(0)
+    out_f, loc_f, aw_f = K.msda_fused(value, ss, offlog, ref, M, L, P, qmask, want_loc_attw=True, head_major=True)
+    out_g, loc_g, aw_g = K.msda_fused(value.float(), ss, offlog, ref, M, L, P, qmask, want_loc_attw=True,
+                                      head_major=True)
     torch.cuda.synchronize()
     # reciprocal-multiply normalisation / approximate reciprocal in the softmax: a few ulp
     assert torch.allclose(loc_f, loc_g, rtol=1e-6, atol=1e-6)
@@ -255,102 +253,6 @@ def test_fast_fused_query_tile_order_invariant():
     assert torch.equal(o0, o1) and torch.equal(l0, l1) and torch.equal(a0, a1)
 
 
-# ---- encoder kernel with the coarse levels resident in LDS (msda_enc_lds_kernel) ----
-
-@pytest.mark.parametrize('shapes,ref_dim,noise', [
-    (((64, 84), (32, 42), (16, 21), (8, 11)), 2, 3.0),       # levels 2-3 staged (as at 800x1333)
-    (((64, 84), (32, 42), (16, 21), (8, 11)), 4, 6.0),       # box references, far-out samples
-    (((60, 70), (40, 50), (45, 50), (10, 13)), 2, 2.0),      # level 3 only fits
-    (((50, 60), (20, 30), (10, 13), (5, 7)), 2, 1.0),        # levels 1-3 staged
-    (((25, 40), (15, 20), (8, 10), (4, 5)), 2, 4.0),         # every level staged (Lq > S)
-    (((70, 80), (56, 60), (45, 50), (40, 40)), 2, 2.0),      # nothing fits: all taps gathered
-])
-@pytest.mark.parametrize('offlog_dtype,out_dtype', [(torch.float16, torch.bfloat16), (torch.float32, torch.float16)])
-@pytest.mark.parametrize('acc16', [True, False])
-def test_encoder_lds_kernel_matches_fast_kernel(shapes, ref_dim, noise, offlog_dtype, out_dtype, acc16):
-    """Encoder-sized calls (Lq >= 2048, no loc/attw output) take msda_enc_lds_kernel; flag 32
-    forces msda_fused_fast_kernel.  Both quantise the tap weights to f16 after the same f32
-    arithmetic, but the compiler contracts the location arithmetic differently in the two
-    kernels, and a 1-ulp change of a sampling location can move a weight to the next f16
-    value: at most 2^-11 of every |weight x value|, i.e. 2^-11 * max|value| in all (the
-    attention weights sum to 1).  With flag 64 the LDS kernel accumulates every product in f32
-    (fine-level and LDS-level taps in two partial sums); by default (acc16) each level's 16
-    taps are summed as f16 pairs before the f32 sum: per level at most 16 f16 roundings of a
-    partial sum bounded by (that level's attention mass) x max|value|, so at most
-    2^-7 * max|value| more.  Plus one rounding of either 16-bit output (stated bounds; the
-    mean error is far below them)."""
-    from kinet_amd import _native
-    from kinet_amd import kernels as K
-    B, M, P = 2, 8, 4
-    Lq = max(sum(h * w for h, w in shapes), 2304)
-    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, Lq + ref_dim,
-                                                  dtype=torch.float16)
-    offlog = offlog.to(offlog_dtype)
-    lib = _native.lib()
-    try:
-        lib.kinet_msda_set_flags(0 if acc16 else 64)
-        o_lds = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, head_major=True, out_dtype=out_dtype)
-        lib.kinet_msda_set_flags(32)
-        o_fast = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, head_major=True, out_dtype=out_dtype)
-    finally:
-        lib.kinet_msda_set_flags(0)
-    torch.cuda.synchronize()
-    ulp = 2.0 ** -7 if out_dtype == torch.bfloat16 else 2.0 ** -10
-    d = (o_lds.float() - o_fast.float()).abs()
-    vmax = value.float().abs().max().item()
-    extra = (2.0 ** -7 + 2.0 ** -11) * vmax if acc16 else 2.0 ** -11 * vmax
-    # one rounding of either output: at most an ulp of the larger magnitude
-    big = torch.maximum(o_fast.float().abs(), o_lds.float().abs())
-    assert (d <= big * ulp + extra).all(), d.max().item()
-    if acc16:
-        assert d.mean().item() <= 2e-3, d.mean().item()
-    assert (o_lds.float()[qmask] == 0).all()
-    assert torch.isfinite(o_lds.float()).all()
-
-
-def test_encoder_lds_kernel_vs_oracle():
-    """msda_enc_lds_kernel against the C oracle, fed the locations / weights the fast kernel
-    reports for the same call."""
-    from kinet_amd import kernels as K
-    from oracle import msda_oracle as O
-    shapes = ((64, 84), (32, 42), (16, 21), (8, 11))
-    B, M, P = 2, 8, 4
-    Lq = sum(h * w for h, w in shapes)
-    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 77, dtype=torch.float16)
-    out = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, head_major=True, out_dtype=torch.float16)
-    _, loc, aw = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, want_loc_attw=True, head_major=True,
-                              out_dtype=torch.float16)
-    torch.cuda.synchronize()
-    v = value.float().permute(1, 2, 0, 3).contiguous().cpu().numpy()
-    ref_out = torch.from_numpy(O.fwd(v, ss.cpu().numpy(), loc.cpu().numpy(), aw.cpu().numpy())).reshape(out.shape)
-    d = (out.float().cpu() - ref_out).abs()
-    # f16 tap weights (as the fast kernel), f16 per-level partial sums (bound as in
-    # test_encoder_lds_kernel_matches_fast_kernel) and the f16 output rounding
-    bound = 4e-3 * ref_out.abs() + 4e-3 + 2.0 ** -7 * value.float().abs().max().item()
-    assert (d <= bound).all(), d.max().item()
-    assert d.mean().item() <= 2e-3, d.mean().item()
-
-
-def test_encoder_lds_kernel_order_and_batch_invariant():
-    """Each query's result depends on nothing but its own inputs: the tile order, the batch
-    size (which changes the query chunks per head map) and a rerun leave it bit-identical."""
-    from kinet_amd import kernels as K
-    shapes = ((64, 84), (32, 42), (16, 21), (8, 11))
-    M, P = 8, 4
-    Lq = sum(h * w for h, w in shapes)
-    value, ss, offlog, ref, qmask = _fused_inputs(3, shapes, Lq, M, P, 2, 3.0, 5, dtype=torch.float16)
-    offlog = offlog.half()
-    order = K.encoder_tile_order(shapes, value.device)
-    kw = dict(head_major=True, out_dtype=torch.bfloat16)
-    o_nat = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, **kw)
-    o_ord = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, query_tile_order=order, **kw)
-    o_again = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, query_tile_order=order, **kw)
-    o_one = K.msda_fused(value[:, 1:2], ss, offlog[1:2], ref[1:2], M, 4, P, qmask[1:2], query_tile_order=order, **kw)
-    torch.cuda.synchronize()
-    assert torch.equal(o_nat, o_ord) and torch.equal(o_ord, o_again)
-    assert torch.equal(o_one[0], o_ord[1])
-
-
 # ---- encoder kernel, head-major offsets / logits (msda_enc.hip, kinet_msda_encoder_forward) ----
 
 def _hm(offlog, M, L=4, P=4):
@@ -372,13 +274,12 @@ def _hm(offlog, M, L=4, P=4):
 @pytest.mark.parametrize('out_dtype,masked,ordered', [(torch.bfloat16, False, True), (torch.float16, True, False),
                                                       (torch.float16, True, True)])
 def test_encoder_kernel_matches_fast_kernel(shapes, ref_dim, noise, out_dtype, masked, ordered):
-    """kinet_msda_encoder_forward against msda_fused_fast_kernel (flag 32) on the same f16
+    """kinet_msda_encoder_forward against msda_fused_fast_kernel on the same f16
     offsets / logits (row-major for the fast kernel, head-major for the encoder kernel).
     Bound as test_encoder_lds_kernel_matches_fast_kernel (acc16): the tap weights are
     quantised to f16 after f32 location arithmetic that the compiler may contract
     differently (2^-11 max|value|), each level's 16 taps are summed as f16 pairs
     (2^-7 max|value|), plus one rounding of either output."""
-    from kinet_amd import _native
     from kinet_amd import kernels as K
     B, M, P = 2, 8, 4
     Lq = max(sum(h * w for h, w in shapes), 2304)
@@ -390,12 +291,7 @@ def test_encoder_kernel_matches_fast_kernel(shapes, ref_dim, noise, out_dtype, m
     S = sum(h * w for h, w in shapes)
     order = K.encoder_tile_order(shapes, value.device) if ordered and Lq == S else None
     o_enc = K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, qm, out_dtype=out_dtype, query_tile_order=order)
-    lib = _native.lib()
-    try:
-        lib.kinet_msda_set_flags(32)
-        o_fast = K.msda_fused(value, ss, offlog, ref, M, 4, P, qm, head_major=True, out_dtype=out_dtype)
-    finally:
-        lib.kinet_msda_set_flags(0)
+    o_fast = K.msda_fused(value, ss, offlog, ref, M, 4, P, qm, head_major=True, out_dtype=out_dtype)
     torch.cuda.synchronize()
     ulp = 2.0 ** -7 if out_dtype == torch.bfloat16 else 2.0 ** -10
     d = (o_enc.float() - o_fast.float()).abs()
@@ -454,7 +350,6 @@ def test_encoder_kernel_large_magnitudes():
     """f16 range on the bf16 path (values and offsets are stored f16): values up to 2^14 and
     offsets of thousands of pixels (samples far outside every level) stay finite, match the
     f32-accumulating fast kernel within the stated f16 bounds, and out-of-image samples add 0."""
-    from kinet_amd import _native
     from kinet_amd import kernels as K
     shapes = ((64, 84), (32, 42), (16, 21), (8, 11))
     B, M, P = 1, 8, 4
@@ -465,12 +360,7 @@ def test_encoder_kernel_large_magnitudes():
     offlog[:, : Lq // 2, : M * 32] *= 1000.0          # half the queries sample far outside
     offlog = offlog.half()
     o_enc = K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, out_dtype=torch.bfloat16)
-    lib = _native.lib()
-    try:
-        lib.kinet_msda_set_flags(32)
-        o_fast = K.msda_fused(value, ss, offlog, ref, M, 4, P, None, head_major=True, out_dtype=torch.bfloat16)
-    finally:
-        lib.kinet_msda_set_flags(0)
+    o_fast = K.msda_fused(value, ss, offlog, ref, M, 4, P, None, head_major=True, out_dtype=torch.bfloat16)
     torch.cuda.synchronize()
     assert torch.isfinite(o_enc.float()).all()
     vmax = value.float().abs().max().item()

@@ -70,13 +70,9 @@ def main():
     ap.add_argument('--decoder', action='store_true')
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--order', action='store_true', help='encoder tile order (kernels.encoder_tile_order)')
-    ap.add_argument('--flags', type=int, default=0, help='kinet_msda_set_flags value (kernel variants)')
     ap.add_argument('--hm', action='store_true',
                     help='encoder kernel on head-major offsets/logits (kinet_msda_encoder_forward)')
     a = ap.parse_args()
-    if a.flags:
-        from kinet_amd import _native
-        _native.lib().kinet_msda_set_flags(a.flags)
     value, ss, offlog, ref, (M, L, P) = make_inputs(B=a.batch, noise=a.noise, decoder=a.decoder,
                                                     dtype=torch.float16)
     offlog = offlog.half()
@@ -99,7 +95,7 @@ def main():
     gathered = nsamp * 4 * value.shape[-1] * value.element_size()
     compulsory = value.numel() * value.element_size() + offlog.numel() * offlog.element_size() + ref.numel() * 4 + \
         B * Lq * M * value.shape[-1] * value.element_size()
-    print(f'[{kind} flags {a.flags}] msda {"decoder" if a.decoder else "encoder"} B={B} Lq={Lq} S={S} noise={a.noise}: {ms * 1e3:.1f} us/call  '
+    print(f'[{kind}] msda {"decoder" if a.decoder else "encoder"} B={B} Lq={Lq} S={S} noise={a.noise}: {ms * 1e3:.1f} us/call  '
           f'compulsory {compulsory / ms / 1e6:.0f} GB/s  gathered {gathered / ms / 1e6:.0f} GB/s')
 
 

@@ -3,8 +3,7 @@
 shapes: encoder call of 2 frames at 800x1333 (levels 100x167, 50x84, 25x42, 13x21; Lq = S =
 22,223), 8 heads x 36 channels, 4 levels x 4 points, f32; and the decoder call (Lq = 500 + track
 queries, 8 levels of the two frames).  Sampling pattern of the reference init (8-direction grid
-offsets) + noise.  Times each variant selected by kinet_msda_set_flags and checks the gradients
-of every variant against flags 0.   python tools/msda_bwd_probe.py [--flags 0,8] [--iters 10]
+offsets) + noise.  Times the backward call.   python tools/msda_bwd_probe.py [--iters 10]
 """
 import argparse
 import math
@@ -35,35 +34,22 @@ def inputs(B, shapes, Lq, M=8, D=36, P=4, seed=0, decoder=False):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--flags', default='0')
     ap.add_argument('--iters', type=int, default=10)
     a = ap.parse_args()
-    from kinet_amd import _native as N
     from kinet_amd.MultiScaleDeformableAttention import ms_deform_attn_backward
     lv = [(100, 167), (50, 84), (25, 42), (13, 21)]
     cases = {'encoder': (2, lv, 22223), 'decoder': (2, lv + lv, 520)}
     for name, (B, shapes, Lq) in cases.items():
         v, ss, loc, attw, gout = inputs(B, shapes, Lq)
-        ref = None
-        for fl in [int(x) for x in a.flags.split(',')]:
-            N.lib().kinet_msda_set_flags(fl)
-            gr = ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
-            torch.cuda.synchronize()
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(a.iters):
-                ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
-            e.record()
-            torch.cuda.synchronize()
-            ms = s.elapsed_time(e) / a.iters
-            err = ''
-            if ref is None:
-                ref = gr
-            else:
-                err = ' | max rel err vs flags 0: ' + ', '.join(
-                    f'{(x - y).abs().max().item() / max(y.abs().max().item(), 1e-12):.1e}' for x, y in zip(gr, ref))
-            print(f'{name:8s} flags {fl:3d}: {ms:8.3f} ms{err}', flush=True)
-        N.lib().kinet_msda_set_flags(0)
+        ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
+        e.record()
+        torch.cuda.synchronize()
+        print(f'{name:8s}: {s.elapsed_time(e) / a.iters:8.3f} ms', flush=True)
 
 
 if __name__ == '__main__':
