@@ -57,6 +57,15 @@ int kinet_msda_backward(const void* value, const int64_t* spatial_shapes,
 int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num_heads,
                                             int channels, int value_dtype);
 
+/* Tuning hook for kinet_msda_backward on the CALLING thread (no reference counterpart).
+ * Encoder calls (num_query == spatial_size) sum grad_value on chip: one workgroup per
+ * (image, head) walks passes of consecutive queries and adds each value row the pass touches
+ * to global memory once.  0 = automatic for every field; mode -1 always selects the
+ * one-atomic-per-corner kernel, mode 1 the on-chip-sum kernel for any call (A/B and tests);
+ * log2_rows = pixel hash size, queries_per_pass (0 = threads / 16). */
+void kinet_msda_backward_tune(int mode, int log2_rows, int queries_per_block, int threads,
+                              int queries_per_pass);
+
 /* Fused module path (MSDeformAttn.forward, ms_deform_attn.py:49-88): computes
  *   attw = softmax over L*P of logits            (ms_deform_attn.py:70-71)
  *   attw = 0 where query_attn_mask               (:73-74, optional, uint8 (N,Lq))

@@ -22,6 +22,7 @@ _SIGS = {
     'kinet_msda_forward': [P, P, P, P, P] + [I] * 10 + [P],
     'kinet_msda_backward': [P] * 9 + [I] * 10 + [P],
     'kinet_msda_backward_workspace_bytes': [I] * 5,
+    'kinet_msda_backward_tune': [I] * 5,
     'kinet_msda_encoder_forward': [P, I64, I64, P, P, P, I, P, P] + [I] * 8 + [P, P],
     'kinet_msda_fused_forward': [P, I64, I64, I64, P, P, I, P, I, P, P, P, P] + [I] * 10 + [P, P],
     'kinet_gemm_set_flags': [I],
@@ -68,7 +69,7 @@ _SIGS = {
     'kinet_version': [],
 }
 _RESTYPES = {'kinet_last_error': ctypes.c_char_p, 'kinet_version': ctypes.c_char_p,
-             'kinet_msda_backward_workspace_bytes': ctypes.c_int64,
+             'kinet_msda_backward_workspace_bytes': ctypes.c_int64, 'kinet_msda_backward_tune': None,
              'kinet_groupnorm_workspace': ctypes.c_long,
              'kinet_gemm_tn_workspace': ctypes.c_int64, 'kinet_colsum_workspace': ctypes.c_int64,
              'kinet_layernorm_backward_workspace': ctypes.c_int64,

@@ -83,6 +83,20 @@ template <> struct Acc<double> { typedef double type; };
 __device__ __forceinline__ double to_acc(double v, double*) { return v; }
 template <typename T> __device__ __forceinline__ float to_acc(T v, float*) { return to_f32(v); }
 
+// compute units of the current device (read once; 256 on MI355X) -- launchers size their
+// grids in rounds of one workgroup per CU
+inline int cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        n = c;
+    }
+    return n;
+}
+
 inline size_t dtype_size(int dt) {
     switch (dt) {
         case KINET_F32: return 4;

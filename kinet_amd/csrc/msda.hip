@@ -852,6 +852,240 @@ __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------
+// backward, grad_value summed on chip (encoder calls of the training path)
+// ---------------------------------------------------------------------------------
+// Global f32 atomics run at the memory side at one chip-wide byte rate (~1.3 TB/s,
+// MI355X_MICROARCH.md "Global float atomics"), so the scatter above is bound by its
+// 4 corners x D x 4 bytes per sample.  In an encoder call the queries are the pixels
+// themselves in raster order and neighbouring queries sample overlapping value rows.  Here
+// one workgroup owns ONE (image, head) and a chunk of consecutive queries, walked in passes
+// of QP queries; per pass:
+//  1. one thread per sample: bilinear setup; each in-image corner looks its pixel up in an
+//     LDS hash (pixel -> slot) and pushes its contribution (corner weight x attention
+//     weight, query row) onto the slot's LDS linked list; the pass's grad_output rows are
+//     staged in LDS;
+//  2. 16 lanes per query: value corners -> grad wrt location / attention weight (as above);
+//     corners whose hash probe failed are added to global memory directly;
+//  3. lane = (slot, channel): walk the slot's list summing weight x grad_output in a
+//     register, then ONE global atomic per row element -- a row touched by c corners of the
+//     pass costs one add instead of c.  Exclusive ownership: no LDS float atomics (measured
+//     at ~86 cycles per wave-instruction, slower than the global atomics they would save).
+// Any sampling pattern is correct; only the saving depends on locality.
+//
+// LDS: LevelInfo | keys[NS] | head[NS] | plist[NS] | npass | cinfo[QP*L*P*4] (weight,
+//      grad_output row) | next[QP*L*P*4] | G[QP][D] f32 | taps[QP*L*P]
+constexpr int kProbe = 8;
+
+struct HTap {
+    int off[4];    // element offset of each corner's head row in the image, -1 = outside
+    float lh, lw, a;
+    int flags;     // bit 0: sample inside the image; bit 1+k: corner k added directly
+};
+
+// slot of `key` in the open-addressed table, inserting it (and appending the slot to plist)
+// when new; -1 after kProbe occupied probes
+__device__ __forceinline__ int hash_slot(int* keys, int* plist, int* npass, int key, int log2ns) {
+    const unsigned mask = (1u << log2ns) - 1u;
+    unsigned h = ((unsigned)key * 2654435761u) >> (32 - log2ns);
+    for (int i = 0; i < kProbe; ++i, h = (h + 1u) & mask) {
+        const int cur = __hip_atomic_load(keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == key) return (int)h;
+        if (cur != -1) continue;
+        const int old = atomicCAS(keys + h, -1, key);
+        if (old == -1) {
+            plist[atomicAdd(npass, 1)] = (int)h;
+            return (int)h;
+        }
+        if (old == key) return (int)h;
+    }
+    return -1;
+}
+
+template <typename T, typename TL, int VEC, int NJ>
+__global__ __launch_bounds__(512) void msda_bwd_list_kernel(
+    const T* __restrict__ value, const int64_t* __restrict__ shapes, const TL* __restrict__ loc,
+    const TL* __restrict__ attw, const T* __restrict__ gout, float* __restrict__ gvalue,
+    TL* __restrict__ gloc, TL* __restrict__ gattw, int S, int M, int D, int L, int Lq, int P, int QC,
+    int QP, int NA, int log2ns) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int NS = 1 << log2ns;
+    const int nt = blockDim.x, LP = L * P, MD = M * D;
+    const int NSMP = QP * LP;
+    LevelInfo& li = *reinterpret_cast<LevelInfo*>(smem);
+    int* keys = reinterpret_cast<int*>(smem + sizeof(LevelInfo));
+    int* head = keys + NS;
+    int* plist = head + NS;
+    int* npass = plist + NS;
+    int2* cinfo = reinterpret_cast<int2*>(npass + 4);
+    int* next = reinterpret_cast<int*>(cinfo + 4 * NSMP);
+    float* G = reinterpret_cast<float*>(next + 4 * NSMP);
+    HTap* taps = reinterpret_cast<HTap*>(G + QP * D);
+    const int b = blockIdx.y, m = blockIdx.z;
+    const int qbeg = blockIdx.x * QC, qend = min(Lq, qbeg + QC);
+    load_levels(li, shapes, L, S);
+    for (int i = threadIdx.x; i < NS; i += nt) { keys[i] = -1; head[i] = -1; }
+    if (threadIdx.x == 0) *npass = 0;
+    __syncthreads();
+
+    const int lane = threadIdx.x & 15;
+    const T* vimg = value + (long)b * S * MD;
+    float* gimg = gvalue + (long)b * S * MD + m * D;
+    for (int qp = qbeg; qp < qend; qp += QP) {
+        // phase 1: grad_output rows of the pass; one thread per sample
+        for (int i = threadIdx.x; i < QP * D; i += nt) {
+            const int qi = i / D, q = qp + qi;
+            G[i] = q < qend ? to_acc(gout[((long)b * Lq + q) * MD + (long)m * D + (i - qi * D)], (float*)nullptr) : 0.f;
+        }
+        for (int s = threadIdx.x; s < NSMP; s += nt) {
+            const int qi = s / LP, lp = s - qi * LP, l = lp / P, q = qp + qi;
+            HTap t;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) t.off[k] = -1;
+            t.lh = t.lw = t.a = 0.f;
+            t.flags = 0;
+            if (q < qend) {
+                const long gi = ((long)b * Lq + q) * M * LP + (long)m * LP + lp;
+                const float x = (float)loc[2 * gi], y = (float)loc[2 * gi + 1];
+                t.a = (float)attw[gi];
+                const int H = li.H[l], W = li.W[l];
+                const float h = y * (float)H - 0.5f, w = x * (float)W - 0.5f;   // cuh:352-353
+                if (li.ok[l] && h > -1.f && w > -1.f && h < (float)H && w < (float)W) {   // cuh:359
+                    const float hf = floorf(h), wf = floorf(w);
+                    const int hl = (int)hf, wl = (int)wf;
+                    t.lh = h - hf;
+                    t.lw = w - wf;
+                    t.flags = 1;
+                    const float hh = 1.f - t.lh, hw = 1.f - t.lw;
+                    const int p00 = li.start[l] + hl * W + wl;
+                    const bool h0 = hl >= 0, h1 = hl + 1 <= H - 1, c0 = wl >= 0, c1 = wl + 1 <= W - 1;
+                    const int pix[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
+                    const bool in[4] = {h0 && c0, h0 && c1, h1 && c0, h1 && c1};
+                    const float wt[4] = {hh * hw, hh * t.lw, t.lh * hw, t.lh * t.lw};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (in[k]) {
+                            t.off[k] = pix[k] * MD;
+                            const int slot = hash_slot(keys, plist, npass, pix[k], log2ns);
+                            if (slot < 0) {
+                                t.flags |= 2 << k;
+                            } else {
+                                const int cid = 4 * s + k;
+                                cinfo[cid] = make_int2(__float_as_int(wt[k] * t.a), qi * D);
+                                next[cid] = atomicExch(head + slot, cid);
+                            }
+                        }
+                }
+            }
+            taps[s] = t;
+        }
+        __syncthreads();
+
+        // phase 2: 16 lanes per query -- value corners for the location / weight gradients
+        // (lanes < NA hold VEC contiguous channels); overflowed corners added directly
+        for (int qi = threadIdx.x >> 4; qi < QP; qi += nt >> 4) {
+            const int q = qp + qi;
+            if (q >= qend) break;
+            const bool cl = lane < NA;
+            const int c0 = (cl ? lane : 0) * VEC;
+            float gc[VEC];
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) gc[j] = cl ? G[qi * D + c0 + j] : 0.f;
+            const HTap* tq = taps + qi * LP;
+            // two samples per step: their 8 corner loads are in flight together
+            auto load = [&](const HTap& t, float (&v)[4][VEC]) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (cl && (t.flags & 1) && t.off[k] >= 0) {
+                        const VecT<T, VEC> vv = *reinterpret_cast<const VecT<T, VEC>*>(vimg + t.off[k] + m * D + c0);
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) v[k][j] = to_acc(vv.v[j], (float*)nullptr);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) v[k][j] = 0.f;
+                    }
+                }
+            };
+            auto consume = [&](const HTap& t, const float (&v)[4][VEC], int s) {
+                float pa = 0.f, px = 0.f, py = 0.f;
+                const float lh = t.lh, lw = t.lw, hh = 1.f - lh, hw = 1.f - lw;
+                const float wt[4] = {hh * hw, hh * lw, lh * hw, lh * lw};
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) {
+                    const float val = wt[0] * v[0][j] + wt[1] * v[1][j] + wt[2] * v[2][j] + wt[3] * v[3][j];
+                    const float dw = hh * (v[1][j] - v[0][j]) + lh * (v[3][j] - v[2][j]);   // cuh:150-160
+                    const float dh = hw * (v[2][j] - v[0][j]) + lw * (v[3][j] - v[1][j]);   // cuh:139-149
+                    pa += gc[j] * val;
+                    px += gc[j] * dw;
+                    py += gc[j] * dh;
+                }
+                if (t.flags & 30) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (!(t.flags & (2 << k))) continue;
+                        const float wk = wt[k] * t.a;
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) {
+                            const int ch = lane + 16 * j;
+                            if (ch < D) atomicAdd(gimg + t.off[k] + ch, G[qi * D + ch] * wk);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int o = 8; o > 0; o >>= 1) {
+                    pa += __shfl_xor(pa, o, 16);
+                    px += __shfl_xor(px, o, 16);
+                    py += __shfl_xor(py, o, 16);
+                }
+                if (lane == 0) {   // samples outside the image: all three sums are 0
+                    const long gi = ((long)b * Lq + q) * M * LP + (long)m * LP + s;
+                    const int l = s / P;
+                    gattw[gi] = (TL)pa;
+                    gloc[2 * gi] = (TL)(px * t.a * (float)li.W[l]);        // cuh:373
+                    gloc[2 * gi + 1] = (TL)(py * t.a * (float)li.H[l]);    // cuh:374
+                }
+            };
+            int s = 0;
+            for (; s + 1 < LP; s += 2) {
+                const HTap t0 = tq[s], t1 = tq[s + 1];
+                float v0[4][VEC], v1[4][VEC];
+                load(t0, v0);
+                load(t1, v1);
+                consume(t0, v0, s);
+                consume(t1, v1, s + 1);
+            }
+            if (s < LP) {
+                const HTap t0 = tq[s];
+                float v0[4][VEC];
+                load(t0, v0);
+                consume(t0, v0, s);
+            }
+        }
+
+        // phase 3 (reads only what phase 1 wrote, so no barrier before it): lane = (slot,
+        // channel), consecutive lanes on consecutive channels of the pass's rows
+        const int n = *npass;
+        for (int i = threadIdx.x; i < n * D; i += nt) {
+            const int si = i / D, c = i - si * D;
+            const int slot = plist[si];
+            float acc = 0.f;
+            for (int cid = head[slot]; cid >= 0; cid = next[cid]) {
+                const int2 ci = cinfo[cid];
+                acc += __int_as_float(ci.x) * G[ci.y + c];
+            }
+            atomicAdd(gimg + (long)keys[slot] * MD + c, acc);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += nt) {
+            const int slot = plist[i];
+            keys[slot] = -1;
+            head[slot] = -1;
+        }
+        if (threadIdx.x == 0) *npass = 0;
+        __syncthreads();
+    }
+}
+
 template <typename T>
 __global__ void f32_to_kernel(const float* __restrict__ src, T* __restrict__ dst, long n) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -921,6 +1155,14 @@ int launch_fwd(const void* value, const int64_t* shapes, const void* loc, const 
     return KINET_OK;
 }
 
+// backward kernel choice for the calling thread (kinet_msda_backward_tune; 0 = automatic):
+// mode -1 = the direct-atomic kernel, 1 = the list kernel for any call; log2ns = hash rows,
+// qc = queries per workgroup, threads = workgroup size, flush_at = queries per pass
+struct BwdTune {
+    int mode, log2ns, qc, threads, flush_at;
+};
+thread_local BwdTune bwd_tune = {0, 0, 0, 0, 0};
+
 template <typename T, typename TL>
 int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const void* attw,
                const void* gout, void* gvalue, void* gloc, void* gattw, void* workspace, int N, int S,
@@ -939,7 +1181,49 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
         acc_buf = (GA*)workspace;
     }
     if (nval) KINET_CHECK_HIP(hipMemsetAsync(acc_buf, 0, nval * sizeof(GA), stream));
-    if (N > 0 && Lq > 0) {
+    const int LP = L * P;
+    const int nj = (D + 15) / 16;
+    const BwdTune tn = bwd_tune;
+    bool hashed = false;
+    if constexpr (sizeof(GA) == 4) {
+    // encoder calls (queries = the value pixels, Lq == S): rows summed on chip per pass
+    // (msda_bwd_list_kernel); mode 1 forces it, mode -1 forbids it
+    if (N > 0 && Lq > 0 && tn.mode >= 0 && (Lq == S || tn.mode == 1) && c.lpq <= 16 && nj <= 4) {
+        hashed = true;
+        const int threads = tn.threads ? tn.threads : 512;
+        const int QP = tn.flush_at > 0 ? tn.flush_at : threads / 16;   // queries per pass
+        int log2ns = tn.log2ns ? tn.log2ns : 10;
+        const size_t nsmp = (size_t)QP * LP;
+        const size_t lds = sizeof(LevelInfo) + ((size_t)3 << log2ns) * sizeof(int) + 4 * sizeof(int) +
+                           nsmp * 4 * (sizeof(int2) + sizeof(int)) + (size_t)QP * D * sizeof(float) + nsmp * sizeof(HTap);
+        KINET_CHECK_ARG(threads % 64 == 0 && threads <= 512 && QP >= 1 && lds <= 160 * 1024,
+                        "msda backward: pass of %d queries x %d samples does not fit LDS", QP, LP);
+        // query chunk per workgroup: as long as the grid still fills the chip 4 times over
+        int qc = tn.qc;
+        if (qc <= 0) {
+            qc = QP;   // one pass per workgroup: 1.08 ms at the config-4 encoder call (2 passes 1.11, 4 1.18)
+            while (qc > QP && (long)N * M * ((Lq + qc - 1) / qc) < 4L * cu_count()) qc >>= 1;
+        }
+        qc = std::max(QP, qc / QP * QP);
+        dim3 grid((Lq + qc - 1) / qc, N, M);
+#define KH(VEC, NJ)                                                                                             \
+    hipLaunchKernelGGL((msda_bwd_list_kernel<T, TL, VEC, NJ>), grid, dim3(threads), lds, stream, (const T*)value, \
+                       shapes, (const TL*)loc, (const TL*)attw, (const T*)gout, (float*)acc_buf, (TL*)gloc,     \
+                       (TL*)gattw, S, M, D, L, Lq, P, qc, QP, c.lpq, log2ns)
+#define KHJ(VEC) switch (nj) { case 1: KH(VEC, 1); break; case 2: KH(VEC, 2); break; case 3: KH(VEC, 3); break; default: KH(VEC, 4); }
+        switch (c.vec) {
+            case 1: KHJ(1); break;
+            case 2: KHJ(2); break;
+            case 4: if constexpr (16 / sizeof(T) >= 4) { KHJ(4); } break;
+            case 8: if constexpr (16 / sizeof(T) >= 8) { KHJ(8); } break;
+        }
+#undef KHJ
+#undef KH
+        KINET_LAUNCH_CHECK();
+    }
+    }
+    if (hashed) {
+    } else if (N > 0 && Lq > 0) {
         // groups padded to a power of two (reductions by shuffles instead of LDS atomics)
         int lpq = c.lpq, qt = c.qt;
         if ((lpq & (lpq - 1)) != 0) {
@@ -1138,6 +1422,10 @@ extern "C" int kinet_msda_backward(const void* value, const int64_t* spatial_sha
 #undef ARGS
     set_error("msda backward: unsupported dtype pair value=%d loc=%d", value_dtype, loc_dtype);
     return KINET_ERR_ARG;
+}
+
+extern "C" void kinet_msda_backward_tune(int mode, int log2_rows, int queries_per_block, int threads, int flush_at) {
+    bwd_tune = BwdTune{mode, log2_rows, queries_per_block, threads, flush_at};
 }
 
 extern "C" int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num_heads, int channels,

@@ -383,17 +383,6 @@ __global__ __launch_bounds__(EW * 64) void msda_enc_kernel(const EncArgs a) {
     enc_tiles<TO, LC, REFD, QM>(a, lv, vmap, b, m, chunk, wave, lane);
 }
 
-int cu_count() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-    }
-    return n;
-}
-
 }  // namespace
 }  // namespace kinet
 

@@ -97,6 +97,56 @@ def test_large_encoder_shape_vs_oracle(MSDA):
     np.testing.assert_allclose(out.numpy(), ref, atol=1e-5, rtol=1e-4)
 
 
+@pytest.mark.parametrize('tune,extra', [((0, 0, 0, 0, 0), 0), ((1, 0, 0, 0, 0), 57), ((1, 6, 32, 256, 0), 57),
+                                        ((1, 6, 64, 512, 16), 57), ((1, 10, 512, 512, 64), 0),
+                                        ((0, 0, 0, 0, 0), 57), ((-1, 0, 0, 0, 0), 0)])
+@pytest.mark.parametrize('D', [32, 36])
+def test_backward_list_kernel_vs_oracle(MSDA, tune, extra, D):
+    """Encoder-call backward: grad_value rows summed on chip per pass of queries
+    (msda_bwd_list_kernel; automatic when Lq == S, forced by tune mode 1).  Encoder-like
+    queries (raster-ordered pixel centres + grid offsets, heavy row reuse) plus `extra` random
+    ones; hash sizes from automatic down to 64 rows (most corners overflow to the direct
+    global add), passes of 16-64 queries, and the one-atomic-per-corner kernel (mode -1 and
+    the automatic choice for Lq != S), all against the C oracle."""
+    from oracle import msda_oracle
+    from kinet_amd import _native
+    g = torch.Generator().manual_seed(D)
+    shapes = torch.tensor([[20, 33], [10, 17], [5, 9], [3, 5]], dtype=torch.int64)
+    S = int((shapes[:, 0] * shapes[:, 1]).sum())
+    N, M, L, P = 2, 8, 4, 4
+    refs = []
+    for h, w in shapes.tolist():
+        y, x = torch.meshgrid(torch.arange(h) + 0.5, torch.arange(w) + 0.5, indexing='ij')
+        refs.append(torch.stack([x.reshape(-1) / w, y.reshape(-1) / h], -1))
+    ref = torch.cat([torch.cat(refs), torch.rand(extra, 2, generator=g)])
+    Lq = ref.shape[0]
+    th = torch.arange(M) * (2 * np.pi / M)
+    grid = torch.stack([th.cos(), th.sin()], -1)[:, None, None, :] * (torch.arange(P) + 1.0)[None, None, :, None]
+    wh = shapes.flip(1).float()[None, :, None, :]
+    loc = ref[None, :, None, None, None, :] + (grid + 0.7 * torch.randn(N, Lq, M, L, P, 2, generator=g)) / wh
+    loc = loc.float().contiguous()
+    value = torch.randn(N, S, M, D, generator=g)
+    attw = torch.rand(N, Lq, M, L, P, generator=g)
+    go = torch.randn(N, Lq, M * D, generator=g)
+    lib = _native.lib()
+    lib.kinet_msda_backward_tune(*tune)
+    try:
+        gv, gl, ga = MSDA.ms_deform_attn_backward(value.cuda(), shapes.cuda(), loc.cuda(), attw.cuda(), go.cuda(), 64)
+        gvh, _, _ = MSDA.ms_deform_attn_backward(value.cuda().bfloat16(), shapes.cuda(), loc.cuda(), attw.cuda(),
+                                                 go.cuda().bfloat16(), 64)
+        torch.cuda.synchronize()
+    finally:
+        lib.kinet_msda_backward_tune(0, 0, 0, 0, 0)
+    ogv, ogl, oga = msda_oracle.bwd(value.numpy(), shapes.numpy(), loc.numpy(), attw.numpy(), go.numpy())
+    np.testing.assert_allclose(gv.cpu().numpy(), ogv, atol=2e-4, rtol=1e-4)
+    np.testing.assert_allclose(gl.cpu().numpy(), ogl, atol=2e-3, rtol=1e-3)
+    np.testing.assert_allclose(ga.cpu().numpy(), oga, atol=2e-4, rtol=1e-4)
+    # bf16 values: f32 sums of the bf16 grad_output, rounded once to bf16 (8 significant bits)
+    ogvh, _, _ = msda_oracle.bwd(value.numpy(), shapes.numpy(), loc.numpy(), attw.numpy(),
+                                 go.bfloat16().float().numpy())
+    np.testing.assert_allclose(gvh.float().cpu().numpy(), ogvh, atol=1e-3, rtol=8e-3)
+
+
 def test_errors_like_reference(MSDA, golden_dir):
     d, t = _load(golden_dir, 'msda_kat_f32.npz')
     with pytest.raises(RuntimeError, match='must divide im2col_step'):

@@ -1,9 +1,14 @@
 #!/usr/bin/env python
-"""MSDA backward (kinet_msda_backward, csrc/msda.hip msda_bwd_kernel) at the config-4 training
-shapes: encoder call of 2 frames at 800x1333 (levels 100x167, 50x84, 25x42, 13x21; Lq = S =
-22,223), 8 heads x 36 channels, 4 levels x 4 points, f32; and the decoder call (Lq = 500 + track
-queries, 8 levels of the two frames).  Sampling pattern of the reference init (8-direction grid
-offsets) + noise.  Times the backward call.   python tools/msda_bwd_probe.py [--iters 10]
+"""MSDA backward (kinet_msda_backward, csrc/msda.hip) at the config-4 training shapes: encoder
+call of 2 frames at 800x1333 (levels 100x167, 50x84, 25x42, 13x21; Lq = S = 22,223), 8 heads x
+36 channels, 4 levels x 4 points, f32; and the decoder call (Lq = 500 + track queries, 8 levels
+of the two frames).  Encoder queries are the level pixels in raster order with their pixel
+centres as reference points (deformable_transformer.py get_reference_points); decoder queries
+have random reference points.  Offsets: the reference init (8-direction grid, point i at
+radius i+1 pixels) + N(0, noise) pixels.  Times the direct-atomic kernel (tune mode -1) and the
+LDS-table kernel at the given table shapes, and checks they agree.
+
+    python tools/msda_bwd_probe.py [--iters 10] [--noise 0.5] [--sweep]
 """
 import argparse
 import math
@@ -15,17 +20,24 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def inputs(B, shapes, Lq, M=8, D=36, P=4, seed=0, decoder=False):
+def inputs(B, shapes, Lq, M=8, D=36, P=4, seed=0, encoder=True, noise=0.5):
     g = torch.Generator(device='cuda').manual_seed(seed)
     L = len(shapes)
     S = sum(h * w for h, w in shapes)
     ss = torch.tensor(shapes, dtype=torch.int64, device='cuda')
     value = torch.randn(B, S, M, D, device='cuda', generator=g)
-    ref = torch.rand(B, Lq, 1, 1, 1, 2, device='cuda', generator=g)
+    if encoder:
+        refs = []
+        for h, w in shapes:
+            y, x = torch.meshgrid(torch.arange(h, device='cuda') + 0.5, torch.arange(w, device='cuda') + 0.5, indexing='ij')
+            refs.append(torch.stack([x.reshape(-1) / w, y.reshape(-1) / h], -1))
+        ref = torch.cat(refs)[None, :, None, None, None, :].expand(B, Lq, 1, 1, 1, 2)
+    else:
+        ref = torch.rand(B, Lq, 1, 1, 1, 2, device='cuda', generator=g)
     th = torch.arange(M, device='cuda', dtype=torch.float32) * (2 * math.pi / M)
     grid = torch.stack([th.cos(), th.sin()], -1)[:, None, None, :] * (torch.arange(P, device='cuda') + 1.0)[None, None, :, None]
     wh = torch.tensor([[w, h] for h, w in shapes], device='cuda', dtype=torch.float32)[None, :, None, :]
-    off = (grid + 0.5 * torch.randn(B, Lq, M, L, P, 2, device='cuda', generator=g)) / wh
+    off = (grid + noise * torch.randn(B, Lq, M, L, P, 2, device='cuda', generator=g)) / wh
     loc = (ref + off).contiguous()
     attw = torch.softmax(torch.randn(B, Lq, M, L * P, device='cuda', generator=g), -1).view(B, Lq, M, L, P).contiguous()
     gout = torch.randn(B, Lq, M * D, device='cuda', generator=g)
@@ -35,21 +47,47 @@ def inputs(B, shapes, Lq, M=8, D=36, P=4, seed=0, decoder=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=10)
+    ap.add_argument('--noise', type=float, default=0.5)
+    ap.add_argument('--sweep', action='store_true')
+    ap.add_argument('--case', default='encoder,decoder')
     a = ap.parse_args()
+    from kinet_amd import _native
     from kinet_amd.MultiScaleDeformableAttention import ms_deform_attn_backward
+    tune = _native.lib().kinet_msda_backward_tune
     lv = [(100, 167), (50, 84), (25, 42), (13, 21)]
-    cases = {'encoder': (2, lv, 22223), 'decoder': (2, lv + lv, 520)}
-    for name, (B, shapes, Lq) in cases.items():
-        v, ss, loc, attw, gout = inputs(B, shapes, Lq)
-        ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(a.iters):
-            ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
-        e.record()
-        torch.cuda.synchronize()
-        print(f'{name:8s}: {s.elapsed_time(e) / a.iters:8.3f} ms', flush=True)
+    cases = {'encoder': (2, lv, 22223, True), 'decoder': (2, lv + lv, 520, False)}
+    # (mode, log2 hash rows, queries per block, threads, queries per pass)
+    cfgs = [(-1, 0, 0, 0, 0), (0, 0, 0, 0, 0)]
+    if a.sweep:
+        cfgs += [(1, l2, qc, th, qp) for l2 in (9, 10, 11) for qc in (32, 64, 128) for th in (256, 512)
+                 for qp in (16, 32) if qp >= th // 32 and qc >= qp]
+    for name, (B, shapes, Lq, enc) in cases.items():
+        if name not in a.case.split(','):
+            continue
+        v, ss, loc, attw, gout = inputs(B, shapes, Lq, encoder=enc, noise=a.noise)
+        ref = None
+        for cfg in cfgs:
+            tune(*cfg)
+            try:
+                out = ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
+            except RuntimeError as ex:
+                print(f'{name:8s} cfg {cfg}: {ex}', flush=True)
+                continue
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = [t.clone() for t in out]
+                err = 0.0
+            else:
+                err = max(((o - r).abs().max() / r.abs().max().clamp_min(1e-30)).item() for o, r in zip(out, ref))
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.iters):
+                ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
+            e.record()
+            torch.cuda.synchronize()
+            print(f'{name:8s} noise {a.noise} cfg {cfg}: {s.elapsed_time(e) / a.iters:8.3f} ms  '
+                  f'max rel diff vs direct {err:.2e}', flush=True)
+    tune(0, 0, 0, 0, 0)
 
 
 if __name__ == '__main__':
