@@ -61,7 +61,8 @@ int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num
  * Encoder calls (num_query == spatial_size) sum grad_value on chip: one workgroup per
  * (image, head) walks passes of consecutive queries and adds each value row the pass touches
  * to global memory once.  0 = automatic for every field; mode -1 always selects the
- * one-atomic-per-corner kernel, mode 1 the on-chip-sum kernel for any call (A/B and tests);
+ * one-atomic-per-corner kernel, mode 1 the on-chip-sum kernel for any call, mode 2 the
+ * on-chip-sum kernel with queries in index order instead of 8-pixel-wide blocks (A/B, tests);
  * log2_rows = pixel hash size, queries_per_pass (0 = threads / 16). */
 void kinet_msda_backward_tune(int mode, int log2_rows, int queries_per_block, int threads,
                               int queries_per_pass);

@@ -907,10 +907,11 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
     const T* __restrict__ value, const int64_t* __restrict__ shapes, const TL* __restrict__ loc,
     const TL* __restrict__ attw, const T* __restrict__ gout, float* __restrict__ gvalue,
     TL* __restrict__ gloc, TL* __restrict__ gattw, int S, int M, int D, int L, int Lq, int P, int QC,
-    int QP, int NA, int log2ns) {
+    int QP, int NA, int log2ns, int blocked) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int blk[kMaxLevels + 1];
     const int NS = 1 << log2ns;
-    const int nt = blockDim.x, LP = L * P, MD = M * D;
+    const int nt = blockDim.x, LP = L * P, MD = M * D, BH = QP / 8;
     const int NSMP = QP * LP;
     LevelInfo& li = *reinterpret_cast<LevelInfo*>(smem);
     int* keys = reinterpret_cast<int*>(smem + sizeof(LevelInfo));
@@ -922,29 +923,59 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
     float* G = reinterpret_cast<float*>(next + 4 * NSMP);
     HTap* taps = reinterpret_cast<HTap*>(G + QP * D);
     const int b = blockIdx.y, m = blockIdx.z;
-    const int qbeg = blockIdx.x * QC, qend = min(Lq, qbeg + QC);
     load_levels(li, shapes, L, S);
     for (int i = threadIdx.x; i < NS; i += nt) { keys[i] = -1; head[i] = -1; }
-    if (threadIdx.x == 0) *npass = 0;
+    if (threadIdx.x == 0) {
+        *npass = 0;
+        // blocked (encoder calls, queries = pixels in raster order): chunk = one 8 x BH block
+        // of one level's pixels, blocks numbered level by level
+        int acc = 0;
+        for (int l = 0; l < L; ++l) {
+            blk[l] = acc;
+            if (li.ok[l]) acc += ((li.H[l] + BH - 1) / BH) * ((li.W[l] + 7) / 8);
+        }
+        blk[L] = acc;
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 15;
     const T* vimg = value + (long)b * S * MD;
     float* gimg = gvalue + (long)b * S * MD + m * D;
+    const int nchunk = blocked ? blk[L] : (Lq + QC - 1) / QC;
+    for (int chunk = blockIdx.x; chunk < nchunk; chunk += gridDim.x) {
+    int qbeg = 0, qend = QP, bl = 0, by = 0, bx = 0;
+    if (blocked) {
+        while (bl + 1 < L && chunk >= blk[bl + 1]) ++bl;
+        const int r = chunk - blk[bl], nbx = (li.W[bl] + 7) / 8;
+        by = r / nbx;
+        bx = r - by * nbx;
+    } else {
+        qbeg = chunk * QC;
+        qend = min(Lq, qbeg + QC);
+    }
+    // query of pass slot qi, -1 = none
+    auto qof = [&](int qp, int qi) -> int {
+        if (blocked) {
+            const int y = by * BH + (qi >> 3), x = bx * 8 + (qi & 7);
+            return (y < li.H[bl] && x < li.W[bl]) ? li.start[bl] + y * li.W[bl] + x : -1;
+        }
+        const int q = qp + qi;
+        return q < qend ? q : -1;
+    };
     for (int qp = qbeg; qp < qend; qp += QP) {
         // phase 1: grad_output rows of the pass; one thread per sample
         for (int i = threadIdx.x; i < QP * D; i += nt) {
-            const int qi = i / D, q = qp + qi;
-            G[i] = q < qend ? to_acc(gout[((long)b * Lq + q) * MD + (long)m * D + (i - qi * D)], (float*)nullptr) : 0.f;
+            const int qi = i / D, q = qof(qp, qi);
+            G[i] = q >= 0 ? to_acc(gout[((long)b * Lq + q) * MD + (long)m * D + (i - qi * D)], (float*)nullptr) : 0.f;
         }
         for (int s = threadIdx.x; s < NSMP; s += nt) {
-            const int qi = s / LP, lp = s - qi * LP, l = lp / P, q = qp + qi;
+            const int qi = s / LP, lp = s - qi * LP, l = lp / P, q = qof(qp, qi);
             HTap t;
 #pragma unroll
             for (int k = 0; k < 4; ++k) t.off[k] = -1;
             t.lh = t.lw = t.a = 0.f;
             t.flags = 0;
-            if (q < qend) {
+            if (q >= 0) {
                 const long gi = ((long)b * Lq + q) * M * LP + (long)m * LP + lp;
                 const float x = (float)loc[2 * gi], y = (float)loc[2 * gi + 1];
                 t.a = (float)attw[gi];
@@ -984,8 +1015,8 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
         // phase 2: 16 lanes per query -- value corners for the location / weight gradients
         // (lanes < NA hold VEC contiguous channels); overflowed corners added directly
         for (int qi = threadIdx.x >> 4; qi < QP; qi += nt >> 4) {
-            const int q = qp + qi;
-            if (q >= qend) break;
+            const int q = qof(qp, qi);
+            if (q < 0) continue;
             const bool cl = lane < NA;
             const int c0 = (cl ? lane : 0) * VEC;
             float gc[VEC];
@@ -1083,6 +1114,7 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
         }
         if (threadIdx.x == 0) *npass = 0;
         __syncthreads();
+    }
     }
 }
 
@@ -1190,9 +1222,12 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
     // (msda_bwd_list_kernel); mode 1 forces it, mode -1 forbids it
     if (N > 0 && Lq > 0 && tn.mode >= 0 && (Lq == S || tn.mode == 1) && c.lpq <= 16 && nj <= 4) {
         hashed = true;
-        const int threads = tn.threads ? tn.threads : 512;
+        // 256 threads, passes of 16 queries (8 x 2 pixel blocks), 1024-row hash: 35 KB of LDS,
+        // 4 workgroups per CU -- 1.03 ms at the config-4 encoder call; 512 threads x 32 queries
+        // 1.05, 512 x 16 1.40 (tools/msda_bwd_probe.py --sweep, profiles/r03p_msda_bwd_probe.log)
+        const int threads = tn.threads ? tn.threads : 256;
         const int QP = tn.flush_at > 0 ? tn.flush_at : threads / 16;   // queries per pass
-        int log2ns = tn.log2ns ? tn.log2ns : 10;
+        const int log2ns = tn.log2ns ? tn.log2ns : 10;
         const size_t nsmp = (size_t)QP * LP;
         const size_t lds = sizeof(LevelInfo) + ((size_t)3 << log2ns) * sizeof(int) + 4 * sizeof(int) +
                            nsmp * 4 * (sizeof(int2) + sizeof(int)) + (size_t)QP * D * sizeof(float) + nsmp * sizeof(HTap);
@@ -1205,11 +1240,16 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
             while (qc > QP && (long)N * M * ((Lq + qc - 1) / qc) < 4L * cu_count()) qc >>= 1;
         }
         qc = std::max(QP, qc / QP * QP);
-        dim3 grid((Lq + qc - 1) / qc, N, M);
+        // encoder calls: queries in 8 x QP/8 pixel blocks (fewer distinct rows per pass than a
+        // run of QP pixels); the grid over-covers the block count (edge blocks) and each
+        // workgroup loops over chunks, so any level geometry is covered
+        const int blocked = (Lq == S && QP % 8 == 0 && tn.mode != 2) ? 1 : 0;
+        const int nq = blocked ? (S + QP - 1) / QP : (Lq + qc - 1) / qc;
+        dim3 grid(blocked ? nq + nq / 8 + 2 * L : nq, N, M);
 #define KH(VEC, NJ)                                                                                             \
     hipLaunchKernelGGL((msda_bwd_list_kernel<T, TL, VEC, NJ>), grid, dim3(threads), lds, stream, (const T*)value, \
                        shapes, (const TL*)loc, (const TL*)attw, (const T*)gout, (float*)acc_buf, (TL*)gloc,     \
-                       (TL*)gattw, S, M, D, L, Lq, P, qc, QP, c.lpq, log2ns)
+                       (TL*)gattw, S, M, D, L, Lq, P, qc, QP, c.lpq, log2ns, blocked)
 #define KHJ(VEC) switch (nj) { case 1: KH(VEC, 1); break; case 2: KH(VEC, 2); break; case 3: KH(VEC, 3); break; default: KH(VEC, 4); }
         switch (c.vec) {
             case 1: KHJ(1); break;
