@@ -109,22 +109,32 @@ int kinet_msda_fused_forward(const void* value, int64_t value_sb, int64_t value_
  *                      (l, p, xy) order | L*P logits in (l, p) order] -- the sampling_offsets /
  *                      attention_weights rows of one head interleaved (kinet_amd.msda packs the
  *                      weight rows so kinet_gemm_headmajor_ex writes it directly)
- *   spatial_shapes_host (L, 2) int64 (H, W) in HOST memory (the launch geometry -- which
- *                      levels fit the LDS map -- is chosen from it; KINET_ERR_ARG when not even
- *                      the coarsest level fits: use kinet_msda_fused_forward)
+ *   spatial_shapes_host (L, 2) int64 (H, W) in HOST memory (the launch plan -- which levels are
+ *                      staged in LDS, how many strips -- is chosen from it; KINET_ERR_ARG when no
+ *                      plan fits: use kinet_msda_fused_forward)
  *   value              f16 head-major: (b, s, m, c) at value[b*value_sb + m*value_sm + s*32 + c]
  *   ref_points, query_attn_mask, output, query_tile_order as kinet_msda_fused_forward
  *   (output (N, Lq, M*32) bf16 or f16).
  * Same semantics as kinet_msda_fused_forward (softmax over L*P, the reference's 2-d offset
  * normaliser quirk, 4-d refs, query mask); head_dim 32, L = 4, P = 4.  Each level's 16 taps
- * are summed as f16 pairs before the f32 sum.  One workgroup per CU owns one (frame, head)
- * map with its coarse levels staged in LDS (msda_enc.hip). */
+ * are summed as f16 pairs before the f32 sum.  One workgroup per CU owns one horizontal strip
+ * (a contiguous range of query_tile_order) of one (frame, head) map, with the rows of the
+ * coarser levels that strip samples staged in LDS; samples outside the staged rows are
+ * gathered from the map (msda_enc.hip).  query_tile_order should be the row-sorted order
+ * (any order gives the same output; the sorted one keeps the staged rows hit). */
 int kinet_msda_encoder_forward(const void* value, int64_t value_sb, int64_t value_sm,
                                const int64_t* spatial_shapes_host, const void* offsets_logits_hm,
                                const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
                                void* output, int batch, int spatial_size, int num_heads, int channels,
                                int num_levels, int num_query, int num_point, int output_dtype,
                                const int32_t* query_tile_order, kinet_stream_t stream);
+
+/* The launch plan kinet_msda_encoder_forward would use for these level shapes (host only, no
+ * GPU call): plan_out[0] = levels gathered from HBM (the finest ones), [1] = strips per head
+ * map, [2] = LDS map pixels used, [3] = workgroups.  KINET_ERR_ARG when no plan fits (the
+ * caller then uses kinet_msda_fused_forward). */
+int kinet_msda_encoder_plan(const int64_t* spatial_shapes_host, int batch, int num_heads, int num_query,
+                            int32_t* plan_out);
 
 #ifdef __cplusplus
 }

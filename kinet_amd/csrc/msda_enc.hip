@@ -1,26 +1,30 @@
 // Encoder-sized MSDeformAttn sampling (MSDeformAttn.forward, ms_deform_attn.py:69-87, with the
 // sampling of ms_deform_im2col_cuda.cuh:165-237) for gfx950: one workgroup per CU owns one
-// (frame, head) value map, its coarse levels staged in LDS, and sweeps a share of the map's
-// query tiles.  kinet_msda_encoder_forward (include/kinet_msda.h).
+// horizontal STRIP of one (frame, head) value map -- the queries of a contiguous range of the
+// row-sorted tile order -- with the rows of the coarse levels that strip samples staged in LDS.
+// kinet_msda_encoder_forward / kinet_msda_encoder_plan (include/kinet_msda.h).
 //
 // Why this shape: at the config-2 encoder call (batch 16, Lq = S = 22,223,
 // 8 heads x 32 channels, 4 levels x 4 points) every query gathers 16 samples x 4 corners x
-// 64 B = 11.6 GB of corner rows per call.  Through the texture path (64 B per clock per CU)
-// that is a ~300 us floor; the two coarse levels of one head (25x42 + 13x21 px, 85 KB) take
-// half of those taps and fit in LDS (ds_read_b128, 256 B per clock per CU).  The earlier
-// kernel of this design (msda_enc_lds_kernel) was latency-bound: a wave's tile ran phase 1
-// (an HBM round trip for the offsets) and then eight dependent gather round trips with two
-// samples in flight, so 16 waves per CU kept the texture unit ~60 % busy.  Here:
+// 64 B = 11.6 GB of corner rows per call.  Through the texture path (one 64-B row per 4 lanes
+// of a buffer_load_b128) those gathers are what bounds the kernel (TA ~72 % busy in the
+// round-2/3 kernels, which kept only the two coarsest levels -- 85 KB of a head map -- in LDS
+// and gathered levels 0 and 1 from HBM/L2).  A strip of 1/8 of the image needs only ~17 rows
+// of level 1 (+ a halo for the sampling offsets), ~14 of level 2 and the whole of level 3:
+// ~150 KB, so levels 1-3 are read from LDS (ds_read_b128) and only level 0 goes through the
+// texture path -- half the gather instructions per tile and ONE gather round trip per tile
+// instead of two.  A sample whose 2x2 footprint leaves the staged rows (an offset beyond the
+// halo) is gathered from the head map instead: any sampling pattern is correct, the staged
+// halo only decides the speed.
 //  * offsets / logits arrive HEAD-MAJOR (M, B, Lq, 48) f16 [32 offsets (l, p, xy) | 16 logits
 //    (l, p)] from the projection GEMM's head-major epilogue: a 16-query tile of one head is
-//    1.5 KB contiguous (two vector loads per lane, every fetched line fully used);
-//  * the tile's phase-1 loads for tile t+1 are issued while tile t gathers, so phase 1 never
-//    waits for HBM;
+//    1.5 KB contiguous (two vector loads per lane);
+//  * the tile's phase-1 loads for tile t+1 are issued while tile t gathers;
 //  * tap records stay in registers: phase-1 lane (query, level) holds its level's 4 point
 //    records, phase-2 lane (query, channel group) fetches them with a quad-broadcast DPP move
 //    (same quad = same query in both phases), so no LDS record traffic and no barrier;
-//  * all four points of a fine level are gathered at once (16 loads in flight per lane),
-//    while the other stream (LDS levels) computes: two gather round trips per tile.
+//  * the staged rows are filled by LDS-DMA (buffer_load ... lds; rows outside the image and
+//    padding are the buffer range check's zeros) while the first tile's level-0 gathers fly.
 // Per (query, head), each level's 16 taps are summed as f16 pairs by v_pk_fma_f16 (2 MACs per
 // instruction; 11-bit significand, above the bf16 compute dtype's 8) and added into f32
 // accumulators level by level (fixed order: deterministic).
@@ -40,17 +44,25 @@ namespace {
 
 constexpr int EW = 16;             // waves per workgroup (one workgroup per CU)
 constexpr int EQT = 16;            // queries per wave tile
-constexpr int EMAP_ROWS = 2400;    // LDS map rows of 64 B incl. the zero margins (153,600 B)
+constexpr int EMAP_PIX = 2544;     // LDS map pixels of 64 B (162,816 B; the level table fits beside)
 constexpr int EL = 4, EP = 4;      // levels, points (the configs' values; host-checked)
 constexpr int EREC = EL * EP * 3;  // head-major offsets/logits per query and head (48)
+constexpr int EHALO = 4;           // rows staged beyond a strip's query rows on each side
+constexpr uint32_t TAF = 0x80000000u;   // record flag: an LDS level's sample gathered from HBM
 
 struct EncLevels {
     int start[EL], H[EL], W[EL], ok[EL];
     float Hf[EL], Wf[EL], rH[EL], rW[EL];
-    int lc;       // first LDS-resident level (EL: none)
-    int mstart;   // its token offset in the head map
-    int npix;     // staged pixels
-    int mtop;     // zero rows before (and after) them: max staged W + 1
+    int ra[EL];   // LDS level: first staged row (-1 = the zero row above the image)
+    int rn[EL];   // LDS level: staged rows
+    int lb[EL];   // LDS level: map pixel of (row r, col c) = lb + r*W + c
+};
+
+// launch plan (host): levels [0, fl) are gathered from the head map, levels [fl, EL) staged
+// per strip: region l = 1 margin pixel + cap[l] rows x W + 1 margin pixel at map pixel base[l]
+struct EncPlan {
+    int fl, nstrip, zpix, used;
+    int cap[EL], base[EL];
 };
 
 struct EncArgs {
@@ -58,13 +70,13 @@ struct EncArgs {
     long vsb, vsm;
     int head_bytes;        // bytes addressable from a head map's base (buffer range)
     int H[EL], W[EL];      // level shapes (host copy of spatial_shapes)
-    int lc;                // first LDS-resident level (host-computed)
+    int cap[EL], base[EL]; // the plan's LDS regions
     const f16_t* offlog;   // (M, B, Lq, 48) head-major
     const float* ref;      // (B, Lq, L, ref_dim)
     const uint8_t* qmask;  // (B, Lq) or null
     void* out;             // (B, Lq, M*32) row-major
     const int* torder;     // processing order of the 16-query tiles (or null)
-    int S, B, M, Lq, nchunk, ref_dim;
+    int S, B, M, Lq, nstrip, used, ref_dim;
 };
 
 // quad broadcast: every lane of a quad takes lane `SRC` of its quad
@@ -142,10 +154,14 @@ __device__ __forceinline__ void load_tile(TileIn& in, const __amdgpu_buffer_rsrc
 
 // Phase 1: softmax over the query's 16 logits (4 in this lane, 4 lanes of the quad;
 // ms_deform_attn.py:70-74), sampling locations (:77-82) and the bilinear setup of cuh:227-233
-// for this lane's level: per point, the byte offset of the top-left corner (map-relative;
-// a corner outside the level keeps an address -- a neighbouring pixel, a zero margin row of the
-// LDS map, or past the buffer range, which reads 0 -- and gets weight 0) + 4 f16 weights.
-template <int REFD>
+// for this lane's level: per point, the byte offset of the top-left corner + 4 f16 weights.
+//  * gathered level (l < FL): map-relative offset; a corner outside the level keeps an address
+//    (a neighbouring pixel, or past the buffer range, which reads 0) and gets weight 0;
+//  * LDS level: offset into the LDS map when both rows of the footprint are staged; else
+//    TAF | (map offset of corner (hl+1, wl+1)) -- non-negative for every footprint that touches
+//    the level, its other corners (-64, -W*64, -(W+1)*64) wrap past the range when outside;
+//    a sample outside the level points at the zero margin (offset 0) with zero weights.
+template <int FL, int REFD>
 __device__ __forceinline__ void setup_tile(const TileIn& in, const EncLevels& lv, int l, bool ok, uint32_t (&ro)[4],
                                            uint32_t (&rw01)[4], uint32_t (&rw23)[4]) {
     float lg[EP], ox[EP], oy[EP];
@@ -166,10 +182,11 @@ __device__ __forceinline__ void setup_tile(const TileIn& in, const EncLevels& lv
     }
     es = group_reduce<4, false>(es);
     const float ra = (in.qm || !ok) ? 0.f : __builtin_amdgcn_rcpf(es);
-    const bool in_lds = l >= lv.lc;
+    const bool in_lds = l >= FL;
     const int H = lv.H[l], W = lv.W[l];
-    const int pbase = in_lds ? (lv.mtop + lv.start[l] - lv.mstart) * 64 : lv.start[l] * 64;
-    const uint32_t zoff = in_lds ? 0u : 0x80000000u;
+    const int start = lv.start[l];
+    const int r0 = lv.ra[l], r1 = lv.ra[l] + lv.rn[l] - 1;   // staged rows [r0, r1]
+    const int lbase = lv.lb[l];
     const float Hf = lv.Hf[l], Wf = lv.Wf[l], rH = lv.rH[l], rW = lv.rW[l];
     const bool lok = lv.ok[l] != 0;
 #pragma unroll
@@ -190,7 +207,14 @@ __device__ __forceinline__ void setup_tile(const TileIn& in, const EncLevels& lv
         const float lh = h - hf, lw = w - wf, hh = 1.f - lh, hw = 1.f - lw;
         const bool h0 = hl >= 0, h1 = hl + 1 < H, c0 = wl >= 0, c1 = wl + 1 < W;
         const float av = valid ? a : 0.f;
-        ro[p] = valid ? (uint32_t)(pbase + (__mul24(hl, W) + wl) * 64) : zoff;
+        if (in_lds) {
+            const bool staged = hl >= r0 && hl < r1;
+            const uint32_t lo = (uint32_t)(lbase + __mul24(hl, W) + wl) * 64u;
+            const uint32_t go = TAF | (uint32_t)(start + __mul24(hl + 1, W) + wl + 1) * 64u;
+            ro[p] = !valid ? 0u : (staged ? lo : go);
+        } else {
+            ro[p] = valid ? (uint32_t)(start + __mul24(hl, W) + wl) * 64u : TAF;
+        }
         rw01[p] = pack_f16x2((h0 && c0) ? hh * hw * av : 0.f, (h0 && c1) ? hh * lw * av : 0.f);
         rw23[p] = pack_f16x2((h1 && c0) ? lh * hw * av : 0.f, (h1 && c1) ? lh * lw * av : 0.f);
     }
@@ -204,14 +228,59 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
-template <typename TO, int LC, int REFD, bool QM>
-__device__ __forceinline__ void enc_tiles(const EncArgs& a, const EncLevels& lv, const u32x4v* vmap, int b, int m,
-                                          int chunk, int wave, int lane) {
-    constexpr int NGL = LC;            // levels gathered through the texture path
-    constexpr int NLL = EL - LC;       // levels read from LDS
-    constexpr int NST = NGL > NLL ? NGL : NLL;
+__device__ __forceinline__ float wave_min(float x) {
+    x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xf, 0xf, false)));
+    x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xf, 0xf, false)));
+    x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xf, 0xf, false)));
+    x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xf, 0xf, false)));
+    x = fminf(x, __shfl_xor(x, 16));
+    x = fminf(x, __shfl_xor(x, 32));
+    return x;
+}
+
+// The strip's query rows, in normalised image height, from its level-0 queries (the bulk of
+// them; coarser-level queries sample the same band) -- or from every tile's first query when
+// the strip holds no level-0 query.  Every wave computes it (same result in each).
+__device__ __forceinline__ void strip_rows(const EncArgs& a, const EncLevels& lv, int t0, int t1, int lane,
+                                           float& ylo, float& yhi) {
+    float lo0 = INFINITY, hi0 = INFINITY, loa = INFINITY, hia = INFINITY;   // hi kept negated
+    const int end0 = min(lv.start[1], a.Lq);
+    const int W0 = lv.W[0];
+    for (int t = t0 + lane; t < t1; t += 64) {
+        const int q0 = (a.torder ? a.torder[t] : t) * EQT;
+        if (q0 < end0) {
+            const int qb = min(q0 + EQT, end0) - 1;
+            lo0 = fminf(lo0, ((float)(q0 / W0) + 0.5f) * lv.rH[0]);
+            hi0 = fminf(hi0, -((float)(qb / W0) + 0.5f) * lv.rH[0]);
+        }
+        int l = 0;
+#pragma unroll
+        for (int k = 1; k < EL; ++k) l = q0 >= lv.start[k] ? k : l;
+        const float y = ((float)((q0 - lv.start[l]) / lv.W[l]) + 0.5f) * lv.rH[l];
+        loa = fminf(loa, y);
+        hia = fminf(hia, -y);
+    }
+    lo0 = wave_min(lo0);
+    hi0 = wave_min(hi0);
+    loa = wave_min(loa);
+    hia = wave_min(hia);
+    const bool any0 = lo0 < INFINITY;
+    ylo = any0 ? lo0 : loa;
+    yhi = any0 ? -hi0 : -hia;
+    if (!(ylo <= yhi)) {   // no tile (not planned): the whole height
+        ylo = 0.f;
+        yhi = 1.f;
+    }
+}
+
+template <typename TO, int FL, int REFD, bool QM>
+__device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4v* vmap, int b, int m, int strip,
+                                          int wave, int lane) {
+    constexpr int NGL = FL;            // levels gathered through the texture path
+    constexpr int NLL = EL - FL;       // levels read from LDS
+    constexpr int NST = NGL > 1 ? NGL : 1;
     const int Lq = a.Lq, ntile = (Lq + EQT - 1) / EQT;
-    const int stride = a.nchunk * EW;
+    const int t0 = (int)((long)strip * ntile / a.nstrip), t1 = (int)((long)(strip + 1) * ntile / a.nstrip);
     const int qi = lane >> 2, l1 = lane & 3;
     const uint32_t cb = (uint32_t)l1 * 16u;      // phase 2: this lane's 8 channels, bytes
     const char* hmap = reinterpret_cast<const char*>(a.value + (long)b * a.vsb + (long)m * a.vsm);
@@ -222,39 +291,99 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, const EncLevels& lv,
         __builtin_amdgcn_make_buffer_rsrc((void*)a.ref, (short)0, a.B * Lq * EL * REFD * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rq =
         __builtin_amdgcn_make_buffer_rsrc((void*)a.qmask, (short)0, a.qmask ? a.B * Lq : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, a.B * Lq * a.M * 64, 0x00020000);
+
+    // ---- the strip's staged rows (every wave derives the same values) ----
+    float ylo, yhi;
+    strip_rows(a, lv, t0, t1, lane, ylo, yhi);
+    int ra_[EL], lb_[EL];
+#pragma unroll
+    for (int l = FL; l < EL; ++l) {
+        const int H = a.H[l], W = a.W[l], cap = a.cap[l];
+        const int hmin = (int)floorf(ylo * (float)H - 0.5f), hmax = (int)floorf(yhi * (float)H - 0.5f) + 1;
+        int r = hmin - max(0, (cap - (hmax - hmin + 1)) / 2);
+        r = max(-1, min(r, H + 1 - cap));
+        ra_[l] = __builtin_amdgcn_readfirstlane(r);
+        lb_[l] = a.base[l] + 1 - ra_[l] * W;
+    }
+    if (lane < EL && lane >= FL) {   // identical values from every wave
+        int r = ra_[FL], bb = lb_[FL];
+#pragma unroll
+        for (int l = FL + 1; l < EL; ++l)
+            if (lane == l) { r = ra_[l]; bb = lb_[l]; }
+        lv.ra[lane] = r;
+        lv.lb[lane] = bb;
+    }
+
+    // ---- LDS-DMA fill of the staged regions (pieces of 16 map pixels = 1 KiB per wave-instruction;
+    // map pixels outside every region, rows outside the image: the range check's zeros) ----
+    {
+        const int npiece = (a.used + 15) >> 4;
+        for (int j = wave; j < npiece; j += EW) {
+            const int x = j * 16 + (lane >> 2);
+            uint32_t off = TAF;
+#pragma unroll
+            for (int l = FL; l < EL; ++l) {
+                const int W = a.W[l];
+                const int k = x - a.base[l] - 1;                  // -1 .. cap*W within the region
+                const int rel = ra_[l] * W + k;                   // level pixel it mirrors
+                const bool in = k >= -1 && k <= a.cap[l] * W && rel >= 0 && rel < a.H[l] * W;
+                off = in ? (uint32_t)(lv.start[l] + rel) * 64u + (uint32_t)(lane & 3) * 16u : off;
+            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(vmap + j * 64), 16,
+                                                     off, 0, 0, 0);
+        }
+    }
+
     const char* vm = reinterpret_cast<const char*>(vmap) + cb;
     int wb[EL];
 #pragma unroll
-    for (int l = 0; l < EL; ++l) wb[l] = lv.W[l] * 64;
+    for (int l = 0; l < EL; ++l) wb[l] = a.W[l] * 64;
 
-    int t = chunk * EW + wave;
-    if (t >= ntile) return;
-    auto tile_q0 = [&](int tt) { return (a.torder ? a.torder[tt] : tt) * EQT; };
+    int t = t0 + wave;
+    const bool has = t < t1;
+    // the tile order read by scalar loads (lgkmcnt: never waits behind the gathers in flight)
+    typedef __attribute__((address_space(4))) const int* cint_p;
+    const cint_p tord = (cint_p)a.torder;
+    auto tile_q0 = [&](int tt) {
+        tt = __builtin_amdgcn_readfirstlane(tt);
+        return (tord ? tord[tt] : tt) * EQT;
+    };
     TileIn in;
-    int q0 = tile_q0(t);
-    load_tile<REFD, QM>(in, ro, rr, rq, b, Lq, q0 + qi, l1);
+    int q0 = has ? tile_q0(t) : 0;
     uint32_t rec_o[EP], rec_w01[EP], rec_w23[EP];
-    setup_tile<REFD>(in, lv, l1, q0 + qi < Lq, rec_o, rec_w01, rec_w23);
+    u32x4v g[EP][4];
+    // gathered level LV: its 4 points' records from quad lane LV, 16 corner loads in flight
+    auto issue = [&](auto lvc) {
+        constexpr int LV = decltype(lvc)::value;
+#pragma unroll
+        for (int p = 0; p < EP; ++p) {
+            const uint32_t o = quad_bcast<LV>(rec_o[p]) + cb;
+            const uint32_t o1 = o + (uint32_t)wb[LV];
+            g[p][0] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o, 0, 0));
+            g[p][1] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o + 64u, 0, 0));
+            g[p][2] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o1, 0, 0));
+            g[p][3] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o1 + 64u, 0, 0));
+        }
+    };
+    if (has) {
+        load_tile<REFD, QM>(in, ro, rr, rq, b, Lq, q0 + qi, l1);
+        setup_tile<FL, REFD>(in, lv, l1, q0 + qi < Lq, rec_o, rec_w01, rec_w23);
+        if constexpr (NGL > 0) issue(std::integral_constant<int, 0>{});
+    }
+    // every wave: its DMA pieces (and the first gathers) landed, then everyone's
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (!has) return;
+    const int stride = EW;
 #pragma unroll 1
     for (;;) {
         const int tn = t + stride;
-        const bool more = tn < ntile;
+        const bool more = tn < t1;
         const int qn0 = more ? tile_q0(tn) : 0;
+        // the next tile's phase-1 inputs, behind this tile's gathers
+        if (more) load_tile<REFD, QM>(in, ro, rr, rq, b, Lq, qn0 + qi, l1);
         f32x2 acc[4] = {};
-        u32x4v g[EP][4];
-        // fine level LV: its 4 points' records from quad lane LV, 16 corner loads in flight
-        auto issue = [&](auto lvc) {
-            constexpr int LV = decltype(lvc)::value;
-#pragma unroll
-            for (int p = 0; p < EP; ++p) {
-                const uint32_t o = quad_bcast<LV>(rec_o[p]) + cb;
-                const uint32_t o1 = o + (uint32_t)wb[LV];
-                g[p][0] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o, 0, 0));
-                g[p][1] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o + 64u, 0, 0));
-                g[p][2] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o1, 0, 0));
-                g[p][3] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o1 + 64u, 0, 0));
-            }
-        };
         // the gathered level: weights fetched from the quad again (registers are the limit)
         auto consume = [&](auto lvc) {
             constexpr int LV = decltype(lvc)::value;
@@ -267,28 +396,49 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, const EncLevels& lv,
             level_sum16(h, g, w01, w23);
             flush16(acc, h);
         };
-        // coarse level LV from the LDS map, one point at a time (16 VGPRs beside the gathers)
-        auto lds_level = [&](auto lvc) {
+        // LDS level LV, one point at a time (8 VGPRs of corner data beside the gathers).  A
+        // footprint outside the staged rows (record flag TAF) is gathered from the head map:
+        // when any lane of the wave has one at this level, the level runs the FAR variant
+        // (per corner pair, the far lanes' corners loaded in place and waited for inside the
+        // branch, so the common path keeps its gathers in flight and holds no extra registers)
+        auto lds_level = [&](auto lvc, auto farc) {
             constexpr int LV = decltype(lvc)::value;
+            constexpr bool FAR = decltype(farc)::value;
             uint32_t h[4];
 #pragma unroll
             for (int p = 0; p < EP; ++p) {
                 const uint32_t o = quad_bcast<LV>(rec_o[p]);
                 const uint32_t w01 = quad_bcast<LV>(rec_w01[p]);
                 const uint32_t w23 = quad_bcast<LV>(rec_w23[p]);
-                const char* r0 = vm + o;
+                const bool far = FAR && (o & TAF) != 0u;
+                const uint32_t lo = far ? 0u : o;
+                const char* r0 = vm + lo;
                 const char* r1 = r0 + wb[LV];
-                // a corner pair at a time (8 VGPRs beside the gathers in flight)
-                const u32x4v v0 = *reinterpret_cast<const u32x4v*>(r0);
-                const u32x4v v1 = *reinterpret_cast<const u32x4v*>(r0 + 64);
+                const bool any_far = FAR && __builtin_amdgcn_ballot_w64(far) != 0;
+                auto corner = [&](const char* lp, uint32_t back) -> u32x4v {
+                    u32x4v v = *reinterpret_cast<const u32x4v*>(lp);
+                    if (FAR && any_far) {
+                        if (far) {   // exec-masked: the other lanes keep their LDS data
+                            const uint32_t go = (o & ~TAF) + cb - back;
+                            asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)"
+                                         : "+v"(v)
+                                         : "v"(go), "s"(rv)
+                                         : "memory");
+                        }
+                    }
+                    return v;
+                };
+                const uint32_t wrow = (uint32_t)wb[LV];
+                const u32x4v v0 = corner(r0, wrow + 64u);
+                const u32x4v v1 = corner(r0 + 64, wrow);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     h[j] = p == 0 ? pk_mul_lo(v0[j], w01) : pk_fma_lo(h[j], v0[j], w01);
                     h[j] = pk_fma_hi(h[j], v1[j], w01);
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                const u32x4v v2 = *reinterpret_cast<const u32x4v*>(r1);
-                const u32x4v v3 = *reinterpret_cast<const u32x4v*>(r1 + 64);
+                const u32x4v v2 = corner(r1, 64u);
+                const u32x4v v3 = corner(r1 + 64, 0u);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     h[j] = pk_fma_lo(h[j], v2[j], w23);
@@ -298,15 +448,23 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, const EncLevels& lv,
             }
             flush16(acc, h);
         };
+        auto lds_level_any = [&](auto lvc) {
+            constexpr int LV = decltype(lvc)::value;
+            const uint32_t f = quad_bcast<LV>(rec_o[0] | rec_o[1] | rec_o[2] | rec_o[3]);
+            if (__builtin_amdgcn_ballot_w64((f & TAF) != 0u) != 0)
+                lds_level(lvc, std::true_type{});
+            else
+                lds_level(lvc, std::false_type{});
+        };
+        // LDS levels interleaved between the gathered levels' consumes (slot s: LDS levels
+        // FL + [s*NLL/NST, (s+1)*NLL/NST))
         static_for<0, NST>([&](auto sc) {
             constexpr int s = decltype(sc)::value;
-            if constexpr (s < NGL) issue(std::integral_constant<int, s>{});
-            if constexpr (s == 0) {
-                // the next tile's phase-1 inputs, behind this tile's first gathers
-                if (more) load_tile<REFD, QM>(in, ro, rr, rq, b, Lq, qn0 + qi, l1);
+            static_for<FL + s * NLL / NST, FL + (s + 1) * NLL / NST>([&](auto lc) { lds_level_any(lc); });
+            if constexpr (s < NGL) {
+                consume(std::integral_constant<int, s>{});
+                if constexpr (s + 1 < NGL) issue(std::integral_constant<int, s + 1>{});
             }
-            if constexpr (s < NLL) lds_level(std::integral_constant<int, LC + s>{});
-            if constexpr (s < NGL) consume(std::integral_constant<int, s>{});
         });
         const int q = q0 + qi;
         if (q < Lq) {
@@ -316,36 +474,36 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, const EncLevels& lv,
                 o.v[2 * j] = Cvt<TO>::from(acc[j][0]);
                 o.v[2 * j + 1] = Cvt<TO>::from(acc[j][1]);
             }
-            *reinterpret_cast<VecT<TO, 8>*>(static_cast<TO*>(a.out) + ((long)b * Lq + q) * a.M * 32 + (long)m * 32 +
-                                            l1 * 8) = o;
+            const uint32_t oo = ((uint32_t)(b * Lq + q) * (uint32_t)a.M * 32u + (uint32_t)m * 32u + (uint32_t)l1 * 8u) * 2u;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, o), rw, oo, 0, 0);
         }
         if (!more) break;
         t = tn;
         q0 = qn0;
-        setup_tile<REFD>(in, lv, l1, q0 + qi < Lq, rec_o, rec_w01, rec_w23);
+        setup_tile<FL, REFD>(in, lv, l1, q0 + qi < Lq, rec_o, rec_w01, rec_w23);
+        if constexpr (NGL > 0) issue(std::integral_constant<int, 0>{});
     }
 }
 
-template <typename TO, int LC, int REFD, bool QM>
+template <typename TO, int FL, int REFD, bool QM>
 __global__ __launch_bounds__(EW * 64) void msda_enc_kernel(const EncArgs a) {
-    constexpr int NT = EW * 64;
     __shared__ EncLevels lv;
-    __shared__ u32x4v vmap[EMAP_ROWS * 4];
-    // XCD-aware remap (cdna_hip_programming.md T1): the query chunks of one (frame, head)
-    // map run on one XCD and share its L2.  Assumes MI355X's 8 XCDs with round-robin dispatch;
-    // elsewhere the mapping is still a bijection (only the L2 grouping is lost).
-    int b, m, chunk;
+    __shared__ u32x4v vmap[EMAP_PIX * 4];
+    // XCD-aware remap (cdna_hip_programming.md T1): the strips of one (frame, head) map run
+    // on one XCD.  Assumes MI355X's 8 XCDs with round-robin dispatch; elsewhere the mapping is
+    // still a bijection (only the L2 grouping is lost).
+    int b, m, strip;
     {
         const int nblk = gridDim.x, lin = blockIdx.x;
         const int qd = nblk >> 3, rm = nblk & 7, xcd = lin & 7;
         const int nid = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + (lin >> 3);
-        chunk = nid % a.nchunk;
-        const int bm = nid / a.nchunk;
+        strip = nid % a.nstrip;
+        const int bm = nid / a.nstrip;
         b = bm / a.M;
         m = bm % a.M;
     }
     if (threadIdx.x == 0) {
-        int acc = 0, wmax = 0;
+        int acc = 0;
         for (int l = 0; l < EL; ++l) {
             const int H = a.H[l], W = a.W[l];
             lv.start[l] = acc;
@@ -356,37 +514,91 @@ __global__ __launch_bounds__(EW * 64) void msda_enc_kernel(const EncArgs a) {
             lv.Wf[l] = (float)W;
             lv.rH[l] = 1.f / (float)H;
             lv.rW[l] = 1.f / (float)W;
-            if (l >= LC) wmax = W > wmax ? W : wmax;
+            lv.ra[l] = 0;
+            lv.rn[l] = a.cap[l];
+            lv.lb[l] = 0;
             acc += H * W;
-        }
-        // levels LC.. staged with max W + 1 zero rows before and after them (the rows a
-        // corner of an edge pixel can address); the host checked that they fit
-        lv.lc = LC;
-        lv.mstart = LC < EL ? lv.start[LC] : 0;
-        lv.npix = LC < EL ? acc - lv.start[LC] : 0;
-        lv.mtop = LC < EL ? wmax + 1 : 0;
-    }
-    __syncthreads();
-    {
-        const char* hmap = reinterpret_cast<const char*>(a.value + (long)b * a.vsb + (long)m * a.vsm);
-        const int npix = lv.npix, mstart = lv.mstart, mtop = lv.mtop;
-        const int rows = npix + 2 * mtop;
-        for (int i = threadIdx.x; i < rows * 4; i += NT) {
-            const int p = (i >> 2) - mtop;
-            u32x4v v = {0u, 0u, 0u, 0u};
-            if (p >= 0 && p < npix) v = *reinterpret_cast<const u32x4v*>(hmap + (long)(mstart + p) * 64 + (i & 3) * 16);
-            vmap[i] = v;
         }
     }
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    enc_tiles<TO, LC, REFD, QM>(a, lv, vmap, b, m, chunk, wave, lane);
+    enc_tiles<TO, FL, REFD, QM>(a, lv, vmap, b, m, strip, wave, lane);
+}
+
+// LDS regions for strips of 1/n of the image: rows ceil(H/n) + 3 (pixel centres, the +1 corner
+// row, a tile spilling into the next row) + 2*EHALO, at most the whole level + the two zero rows
+bool plan_layout(const int64_t* shapes, int fl, int n, EncPlan& pl) {
+    int wmax = 0;
+    for (int l = fl; l < EL; ++l) wmax = std::max<int>(wmax, (int)shapes[2 * l + 1]);
+    long long pos = ((long long)wmax + 2 + 15) / 16 * 16;   // zero margin: a whole 2x2 footprint of any level
+    pl.zpix = (int)pos;
+    for (int l = 0; l < EL; ++l) pl.cap[l] = pl.base[l] = 0;
+    for (int l = fl; l < EL; ++l) {
+        const long long H = shapes[2 * l], W = shapes[2 * l + 1];
+        const long long cap = std::min<long long>(H + 2, (H + n - 1) / n + 3 + 2 * EHALO);
+        pl.cap[l] = (int)cap;
+        pl.base[l] = (int)pos;
+        pos += (cap * W + 2 + 15) / 16 * 16;
+        if (pos > EMAP_PIX) return false;
+    }
+    pl.used = (int)pos;
+    pl.fl = fl;
+    pl.nstrip = n;
+    return true;
+}
+
+// the fewest gathered levels whose staged levels fit with strips of at least 16 tiles, then the
+// fewest strips (>= what fits) whose workgroups fill >= 90 % of their last round of one per CU
+bool enc_plan(const int64_t* shapes, int batch, int heads, int num_query, EncPlan& pl) {
+    const int cus = cu_count();
+    const int maps = batch * heads;
+    const int ntile = (num_query + EQT - 1) / EQT;
+    const int nmax = std::max(1, ntile / EQT);
+    for (int fl = 0; fl < EL; ++fl) {
+        int nmin = 0;
+        for (int n = 1; n <= nmax && n <= 64; ++n)
+            if (plan_layout(shapes, fl, n, pl)) {
+                nmin = n;
+                break;
+            }
+        if (!nmin) continue;
+        int n = nmin;
+        for (int c = nmin; c <= std::min(nmax, 2 * nmin + cus / std::max(1, maps)); ++c) {
+            const long long wgs = (long long)maps * c, rounds = (wgs + cus - 1) / cus;
+            if (wgs * 10 >= rounds * cus * 9) {
+                n = c;
+                break;
+            }
+        }
+        return plan_layout(shapes, fl, n, pl);
+    }
+    return false;
 }
 
 }  // namespace
 }  // namespace kinet
 
 using namespace kinet;
+
+extern "C" int kinet_msda_encoder_plan(const int64_t* spatial_shapes_host, int batch, int num_heads, int num_query,
+                                       int32_t* plan_out) {
+    KINET_CHECK_ARG(spatial_shapes_host != nullptr && batch > 0 && num_heads > 0 && num_query > 0,
+                    "msda encoder plan: bad arguments");
+    for (int l = 0; l < EL; ++l)
+        KINET_CHECK_ARG(spatial_shapes_host[2 * l] > 0 && spatial_shapes_host[2 * l + 1] > 0 &&
+                            spatial_shapes_host[2 * l] * spatial_shapes_host[2 * l + 1] < (1LL << 30),
+                        "msda encoder plan: bad level shape");
+    EncPlan pl{};
+    KINET_CHECK_ARG(enc_plan(spatial_shapes_host, batch, num_heads, num_query, pl),
+                    "msda encoder: no strip plan fits the LDS map (use kinet_msda_fused_forward)");
+    if (plan_out) {
+        plan_out[0] = pl.fl;
+        plan_out[1] = pl.nstrip;
+        plan_out[2] = pl.used;
+        plan_out[3] = batch * num_heads * pl.nstrip;
+    }
+    return KINET_OK;
+}
 
 extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, int64_t value_sm,
                                           const int64_t* spatial_shapes_host, const void* offsets_logits_hm,
@@ -412,26 +624,18 @@ extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, i
     }
     KINET_CHECK_ARG(npix == spatial_size, "msda encoder: spatial_shapes cover %lld tokens, value has %d", npix,
                     spatial_size);
-    // the coarsest suffix of levels that fits the LDS map with its zero margins
-    int lc = EL;
-    {
-        long long np = 0;
-        int wmax = 0;
-        for (int l = EL - 1; l >= 0; --l) {
-            const long long n = np + spatial_shapes_host[2 * l] * spatial_shapes_host[2 * l + 1];
-            const int wm = std::max<int>(wmax, (int)spatial_shapes_host[2 * l + 1]);
-            if (n + 2LL * (wm + 1) > EMAP_ROWS) break;
-            np = n;
-            wmax = wm;
-            lc = l;
-        }
-    }
-    KINET_CHECK_ARG(lc < EL, "msda encoder: the coarsest level does not fit the LDS map (use kinet_msda_fused_forward)");
     if (batch == 0 || num_query == 0) return KINET_OK;
+    EncPlan pl{};
+    KINET_CHECK_ARG(enc_plan(spatial_shapes_host, batch, num_heads, num_query, pl),
+                    "msda encoder: no strip plan fits the LDS map (use kinet_msda_fused_forward)");
     const long long head_bytes = (long long)spatial_size * 64;
-    KINET_CHECK_ARG(head_bytes < (1LL << 31) && (long long)num_query * EREC * 2 < (1LL << 31) &&
+    long long wmax = 0;
+    for (int l = 0; l < EL; ++l) wmax = std::max<long long>(wmax, spatial_shapes_host[2 * l + 1]);
+    // far-sample records carry a map offset up to (S + W + 1) * 64 below the TAF flag bit
+    KINET_CHECK_ARG((spatial_size + wmax + 2) * 64 < (1LL << 31) && (long long)num_query * EREC * 2 < (1LL << 31) &&
                         (long long)batch * num_query < (1LL << 24) &&
-                        (long long)batch * num_query * EL * ref_dim * 4 < (1LL << 31),
+                        (long long)batch * num_query * EL * ref_dim * 4 < (1LL << 31) &&
+                        (long long)batch * num_query * num_heads * 64 < (1LL << 31),
                     "msda encoder: problem too large for 32-bit buffer offsets");
     EncArgs a{};
     a.value = (const f16_t*)value;
@@ -441,8 +645,9 @@ extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, i
     for (int l = 0; l < EL; ++l) {
         a.H[l] = (int)spatial_shapes_host[2 * l];
         a.W[l] = (int)spatial_shapes_host[2 * l + 1];
+        a.cap[l] = pl.cap[l];
+        a.base[l] = pl.base[l];
     }
-    a.lc = lc;
     a.offlog = (const f16_t*)offsets_logits_hm;
     a.ref = ref_points;
     a.qmask = query_attn_mask;
@@ -453,41 +658,28 @@ extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, i
     a.M = num_heads;
     a.Lq = num_query;
     a.ref_dim = ref_dim;
-    // one round of one-per-CU workgroups: the fewest query chunks per head map whose
-    // workgroups fill >= 90 % of their last round (config 2, batch 16: 128 maps x 2 = one round)
-    const int cus = cu_count();
-    const int maps = batch * num_heads;
-    const int ntile = (num_query + EQT - 1) / EQT;
-    const int base = (cus + maps - 1) / maps;
-    int nchunk = base;
-    for (int c = base; c <= 4 * base; ++c) {
-        const long long wgs = (long long)maps * c, rounds = (wgs + cus - 1) / cus;
-        if (wgs * 10 >= rounds * cus * 9) {
-            nchunk = c;
-            break;
-        }
-    }
-    nchunk = std::max(1, std::min(nchunk, (ntile + EW - 1) / EW));
-    KINET_CHECK_ARG((long long)maps * nchunk < (1LL << 31), "msda encoder: grid too large");
-    a.nchunk = nchunk;
+    a.nstrip = pl.nstrip;
+    a.used = pl.used;
+    const long long maps = (long long)batch * num_heads;
+    KINET_CHECK_ARG(maps * pl.nstrip < (1LL << 31), "msda encoder: grid too large");
     hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(maps * nchunk), block(EW * 64);
-#define EK(TO_, LC_, RD_, QM_) hipLaunchKernelGGL((msda_enc_kernel<TO_, LC_, RD_, QM_>), grid, block, 0, s, a)
-#define EK_QM(TO_, LC_, RD_) if (query_attn_mask) EK(TO_, LC_, RD_, true); else EK(TO_, LC_, RD_, false)
-#define EK_RD(TO_, LC_) if (ref_dim == 2) { EK_QM(TO_, LC_, 2); } else { EK_QM(TO_, LC_, 4); }
-#define EK_LC(TO_)                        \
-    switch (lc) {                         \
+    const dim3 grid((unsigned)(maps * pl.nstrip)), block(EW * 64);
+#define EK(TO_, FL_, RD_, QM_) hipLaunchKernelGGL((msda_enc_kernel<TO_, FL_, RD_, QM_>), grid, block, 0, s, a)
+#define EK_QM(TO_, FL_, RD_) if (query_attn_mask) EK(TO_, FL_, RD_, true); else EK(TO_, FL_, RD_, false)
+#define EK_RD(TO_, FL_) if (ref_dim == 2) { EK_QM(TO_, FL_, 2); } else { EK_QM(TO_, FL_, 4); }
+#define EK_FL(TO_)                        \
+    switch (pl.fl) {                      \
         case 0: EK_RD(TO_, 0) break;      \
         case 1: EK_RD(TO_, 1) break;      \
         case 2: EK_RD(TO_, 2) break;      \
         default: EK_RD(TO_, 3) break;     \
     }
     if (output_dtype == KINET_BF16) {
-        EK_LC(bf16_t)
+        EK_FL(bf16_t)
     } else {
-        EK_LC(f16_t)
+        EK_FL(f16_t)
     }
-#undef EK_LC
+#undef EK_FL
 #undef EK_RD
 #undef EK_QM
 #undef EK

@@ -514,19 +514,32 @@ def encoder_tile_order(shapes, device, qt=16):
 
 
 _host_shapes = {}
-ENC_MAP_ROWS = 2400      # msda_enc.hip EMAP_ROWS: LDS map rows (64 B) incl. the zero margins
+_enc_plans = {}
+
+
+def msda_encoder_plan(shapes, batch, n_heads, Lq):
+    """kinet_msda_encoder_plan for host level shapes: (levels gathered from HBM, strips per head
+    map, LDS map pixels used, workgroups), or None when no strip plan fits the LDS map.  Cached."""
+    key = (tuple(tuple(int(v) for v in s) for s in shapes), int(batch), int(n_heads), int(Lq))
+    if key not in _enc_plans:
+        import ctypes
+        hs = (ctypes.c_int64 * 8)(*[v for s in key[0] for v in s])
+        out = (ctypes.c_int32 * 4)()
+        rc = N.lib().kinet_msda_encoder_plan(ctypes.cast(hs, ctypes.c_void_p), key[1], key[2], key[3],
+                                             ctypes.cast(out, ctypes.c_void_p))
+        _enc_plans[key] = tuple(out) if rc == 0 else None
+    return _enc_plans[key]
 
 
 def msda_encoder_supported(value, shapes, Lq, n_heads, n_levels, n_points, batch):
     """True when kinet_msda_encoder_forward takes the call: f16 head-major values of head_dim
-    32, 4 levels x 4 points, an encoder-sized query set (>= 2048 per frame) and at least the
-    coarsest level fitting the LDS map (with max W + 1 zero rows on each side)."""
+    32, 4 levels x 4 points, an encoder-sized query set (>= 2048 per frame) and a strip plan
+    that fits the LDS map (kinet_msda_encoder_plan)."""
     if value.dim() != 4 or value.dtype != torch.float16 or value.shape[-1] != 32 or value.stride(2) != 32:
         return False
     if n_levels != 4 or n_points != 4 or Lq < 2048 or shapes is None or len(shapes) != 4:
         return False
-    h, w = shapes[-1]
-    if h * w + 2 * (w + 1) > ENC_MAP_ROWS or batch * Lq >= (1 << 24):
+    if batch * Lq >= (1 << 24) or msda_encoder_plan(shapes, batch, n_heads, Lq) is None:
         return False
     return value.data_ptr() % 16 == 0 and value.stride(1) % 8 == 0 and value.stride(0) % 8 == 0
 

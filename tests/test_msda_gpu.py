@@ -421,13 +421,67 @@ def test_encoder_kernel_large_magnitudes():
 
 
 def test_encoder_kernel_rejects_unstaged_geometry():
-    """Shapes whose coarsest level does not fit the LDS map are refused (the module falls back
-    to kinet_msda_fused_forward: msda_encoder_supported is False for them)."""
+    """Shapes whose levels do not fit the LDS map even as strips (12 staged rows of a
+    250-pixel-wide coarsest level) are refused: msda_encoder_supported is False and the module
+    falls back to kinet_msda_fused_forward."""
     from kinet_amd import kernels as K
-    shapes = ((100, 110), (70, 80), (56, 60), (48, 50))
+    shapes = ((20, 250), (20, 250), (20, 250), (20, 250))
     B, M, P = 1, 8, 4
     Lq = sum(h * w for h, w in shapes)
     value, ss, offlog, ref, _ = _fused_inputs(B, shapes, Lq, M, P, 2, 1.0, 3, dtype=torch.float16)
+    assert K.msda_encoder_plan(shapes, B, M, Lq) is None
     assert not K.msda_encoder_supported(value, shapes, Lq, M, 4, 4, B)
-    with pytest.raises(RuntimeError, match='coarsest level'):
+    with pytest.raises(RuntimeError, match='no strip plan'):
         K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, out_dtype=torch.bfloat16)
+
+
+def _encoder_refs(shapes, B):
+    """The encoder's reference points (deformable_transformer.py:get_reference_points with
+    valid ratios 1): query q = pixel (i, j) of its level -> ((j + .5) / W, (i + .5) / H) at
+    every level."""
+    pts = []
+    for h, w in shapes:
+        yy, xx = torch.meshgrid(torch.arange(h, dtype=torch.float32) + 0.5, torch.arange(w, dtype=torch.float32) + 0.5,
+                                indexing='ij')
+        pts.append(torch.stack([xx.reshape(-1) / w, yy.reshape(-1) / h], -1))
+    r = torch.cat(pts, 0)
+    return r[None, :, None, :].expand(B, -1, len(shapes), -1).contiguous().cuda()
+
+
+@pytest.mark.parametrize('shapes', [
+    ((100, 167), (50, 84), (25, 42), (13, 21)),    # config 2 (800x1333): level 0 gathered, 1-3 staged
+    ((60, 70), (40, 50), (45, 50), (10, 13)),      # wide level 2: levels 2-3 staged
+    ((25, 40), (15, 20), (8, 10), (4, 5)),         # every level staged whole
+])
+@pytest.mark.parametrize('noise', [0.5, 3.0, 25.0])
+def test_encoder_kernel_strips_staged_and_far(shapes, noise):
+    """Encoder geometry (queries = the pixels of the levels, references at their centres, tiles
+    in row-sorted order): small offsets read the strip's staged rows, large ones (noise 25 px)
+    leave them and are gathered from the head map -- both against the fast kernel, within the
+    bound of test_encoder_kernel_matches_fast_kernel, and the plan is the expected one."""
+    from kinet_amd import kernels as K
+    B, M, P = 2, 8, 4
+    S = sum(h * w for h, w in shapes)
+    value, ss, offlog, _, qmask = _fused_inputs(B, shapes, S, M, P, 2, noise, 11 + int(noise), dtype=torch.float16)
+    ref = _encoder_refs(shapes, B)
+    # offsets in pixels of each level: the reference's normaliser divides x by H and y by W
+    # (ms_deform_attn.py:77-79), so scale the noise back to pixels per level
+    offlog = offlog.half()
+    plan = K.msda_encoder_plan(shapes, B, M, S)
+    assert plan is not None
+    if shapes[0] == (100, 167):
+        assert plan[0] == 1 and plan[1] >= 8, plan
+    order = K.encoder_tile_order(shapes, value.device)
+    o_enc = K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, qmask, out_dtype=torch.bfloat16,
+                           query_tile_order=order)
+    o_nat = K.msda_encoder(value, shapes, _hm(offlog, M), ref, M, qmask, out_dtype=torch.bfloat16)
+    o_fast = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, head_major=True, out_dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    # natural order: other strips, other staged rows, same result bit for bit
+    assert torch.equal(o_enc, o_nat)
+    d = (o_enc.float() - o_fast.float()).abs()
+    vmax = value.float().abs().max().item()
+    big = torch.maximum(o_fast.float().abs(), o_enc.float().abs())
+    assert (d <= big * 2.0 ** -7 + (2.0 ** -7 + 2.0 ** -11) * vmax).all(), d.max().item()
+    assert d.mean().item() <= 2e-3, d.mean().item()
+    assert (o_enc.float()[qmask] == 0).all()
