@@ -220,6 +220,14 @@ __device__ __forceinline__ void setup_tile(const TileIn& in, const EncLevels& lv
     }
 }
 
+// the lane id recomputed where it is used (volatile: not hoisted out of the tile loop, so the
+// lane-constant offsets derived from it cost a VALU op instead of a register across the loop)
+__device__ __forceinline__ int lane_id_here() {
+    int x;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
+    return x;
+}
+
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
     if constexpr (I < N) {
@@ -293,48 +301,6 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
         __builtin_amdgcn_make_buffer_rsrc((void*)a.qmask, (short)0, a.qmask ? a.B * Lq : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, a.B * Lq * a.M * 64, 0x00020000);
 
-    // ---- the strip's staged rows (every wave derives the same values) ----
-    float ylo, yhi;
-    strip_rows(a, lv, t0, t1, lane, ylo, yhi);
-    int ra_[EL], lb_[EL];
-#pragma unroll
-    for (int l = FL; l < EL; ++l) {
-        const int H = a.H[l], W = a.W[l], cap = a.cap[l];
-        const int hmin = (int)floorf(ylo * (float)H - 0.5f), hmax = (int)floorf(yhi * (float)H - 0.5f) + 1;
-        int r = hmin - max(0, (cap - (hmax - hmin + 1)) / 2);
-        r = max(-1, min(r, H + 1 - cap));
-        ra_[l] = __builtin_amdgcn_readfirstlane(r);
-        lb_[l] = a.base[l] + 1 - ra_[l] * W;
-    }
-    if (lane < EL && lane >= FL) {   // identical values from every wave
-        int r = ra_[FL], bb = lb_[FL];
-#pragma unroll
-        for (int l = FL + 1; l < EL; ++l)
-            if (lane == l) { r = ra_[l]; bb = lb_[l]; }
-        lv.ra[lane] = r;
-        lv.lb[lane] = bb;
-    }
-
-    // ---- LDS-DMA fill of the staged regions (pieces of 16 map pixels = 1 KiB per wave-instruction;
-    // map pixels outside every region, rows outside the image: the range check's zeros) ----
-    {
-        const int npiece = (a.used + 15) >> 4;
-        for (int j = wave; j < npiece; j += EW) {
-            const int x = j * 16 + (lane >> 2);
-            uint32_t off = TAF;
-#pragma unroll
-            for (int l = FL; l < EL; ++l) {
-                const int W = a.W[l];
-                const int k = x - a.base[l] - 1;                  // -1 .. cap*W within the region
-                const int rel = ra_[l] * W + k;                   // level pixel it mirrors
-                const bool in = k >= -1 && k <= a.cap[l] * W && rel >= 0 && rel < a.H[l] * W;
-                off = in ? (uint32_t)(lv.start[l] + rel) * 64u + (uint32_t)(lane & 3) * 16u : off;
-            }
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(vmap + j * 64), 16,
-                                                     off, 0, 0, 0);
-        }
-    }
-
     const char* vm = reinterpret_cast<const char*>(vmap) + cb;
     int wb[EL];
 #pragma unroll
@@ -366,8 +332,52 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
             g[p][3] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o1 + 64u, 0, 0));
         }
     };
+    // ---- the strip's staged rows (every wave derives the same values) ----
+    float ylo, yhi;
+    strip_rows(a, lv, t0, t1, lane, ylo, yhi);
+    int ra_[EL], lb_[EL];
+#pragma unroll
+    for (int l = FL; l < EL; ++l) {
+        const int H = a.H[l], W = a.W[l], cap = a.cap[l];
+        const int hmin = (int)floorf(ylo * (float)H - 0.5f), hmax = (int)floorf(yhi * (float)H - 0.5f) + 1;
+        int r = hmin - max(0, (cap - (hmax - hmin + 1)) / 2);
+        r = max(-1, min(r, H + 1 - cap));
+        ra_[l] = __builtin_amdgcn_readfirstlane(r);
+        lb_[l] = a.base[l] + 1 - ra_[l] * W;
+    }
+    if (lane < EL && lane >= FL) {   // identical values from every wave
+        int r = ra_[FL], bb = lb_[FL];
+#pragma unroll
+        for (int l = FL + 1; l < EL; ++l)
+            if (lane == l) { r = ra_[l]; bb = lb_[l]; }
+        lv.ra[lane] = r;
+        lv.lb[lane] = bb;
+    }
+
+    // the first tile's phase-1 inputs ahead of the DMA (so waiting for them does not wait for it)
+    if (has) load_tile<REFD, QM>(in, ro, rr, rq, b, Lq, q0 + qi, l1);
+    // ---- LDS-DMA fill of the staged regions, in flight with the first tile's setup and gathers (pieces
+    // of 16 map pixels = 1 KiB per wave-instruction; map pixels outside every region and rows
+    // outside the image: the range check's zeros) ----
+    {
+        const int npiece = (a.used + 15) >> 4;
+        for (int j = wave; j < npiece; j += EW) {
+            const int x = j * 16 + (lane >> 2);
+            uint32_t off = TAF;
+#pragma unroll
+            for (int l = FL; l < EL; ++l) {
+                const int W = a.W[l];
+                const int k = x - a.base[l] - 1;                  // -1 .. cap*W within the region
+                const int rel = ra_[l] * W + k;                   // level pixel it mirrors
+                const bool in = k >= -1 && k <= a.cap[l] * W && rel >= 0 && rel < a.H[l] * W;
+                off = in ? (uint32_t)(lv.start[l] + rel) * 64u + (uint32_t)(lane & 3) * 16u : off;
+            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(vmap + j * 64), 16,
+                                                     off, 0, 0, 0);
+        }
+    }
+
     if (has) {
-        load_tile<REFD, QM>(in, ro, rr, rq, b, Lq, q0 + qi, l1);
         setup_tile<FL, REFD>(in, lv, l1, q0 + qi < Lq, rec_o, rec_w01, rec_w23);
         if constexpr (NGL > 0) issue(std::integral_constant<int, 0>{});
     }
@@ -382,7 +392,10 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
         const bool more = tn < t1;
         const int qn0 = more ? tile_q0(tn) : 0;
         // the next tile's phase-1 inputs, behind this tile's gathers
-        if (more) load_tile<REFD, QM>(in, ro, rr, rq, b, Lq, qn0 + qi, l1);
+        if (more) {
+            const int li = lane_id_here();
+            load_tile<REFD, QM>(in, ro, rr, rq, b, Lq, qn0 + (li >> 2), li & 3);
+        }
         f32x2 acc[4] = {};
         // the gathered level: weights fetched from the quad again (registers are the limit)
         auto consume = [&](auto lvc) {
@@ -466,7 +479,8 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
                 if constexpr (s + 1 < NGL) issue(std::integral_constant<int, s + 1>{});
             }
         });
-        const int q = q0 + qi;
+        const int lis = lane_id_here();
+        const int q = q0 + (lis >> 2);
         if (q < Lq) {
             VecT<TO, 8> o;
 #pragma unroll
@@ -474,13 +488,16 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
                 o.v[2 * j] = Cvt<TO>::from(acc[j][0]);
                 o.v[2 * j + 1] = Cvt<TO>::from(acc[j][1]);
             }
-            const uint32_t oo = ((uint32_t)(b * Lq + q) * (uint32_t)a.M * 32u + (uint32_t)m * 32u + (uint32_t)l1 * 8u) * 2u;
+            const uint32_t oo = ((uint32_t)(b * Lq + q) * (uint32_t)a.M * 32u + (uint32_t)m * 32u + (uint32_t)(lis & 3) * 8u) * 2u;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, o), rw, oo, 0, 0);
         }
         if (!more) break;
         t = tn;
         q0 = qn0;
-        setup_tile<FL, REFD>(in, lv, l1, q0 + qi < Lq, rec_o, rec_w01, rec_w23);
+        {
+            const int li = lane_id_here();
+            setup_tile<FL, REFD>(in, lv, li & 3, q0 + (li >> 2) < Lq, rec_o, rec_w01, rec_w23);
+        }
         if constexpr (NGL > 0) issue(std::integral_constant<int, 0>{});
     }
 }
