@@ -457,6 +457,10 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         KINET_CHECK_ARG(a.N <= 320, "gemm: fused LayerNorm needs N <= 320 (got %d)", a.N);
         bm = a.M <= 8192 ? 32 : 64;     // small M (decoder queries): more workgroups
         bn = a.N <= 256 ? 256 : 320;
+        // rows of 257..320 (d = 288, configs 3-5) at encoder sizes: 128 x 320 LDS-DMA tiles --
+        // the 64 x 320 register-staged tile re-reads the whole 320 x K weight through its
+        // staging registers for every 64 rows (~100 TF/s at M = 172k)
+        if (sizeof(T) == 2 && a.N > 256 && a.M >= 8192 && a.A2 == nullptr && a.kchunk == 0) bm = 128;
     } else if (a.kchunk && a.M <= 4096) {
         bm = bn = 64;                   // split-K slices of a small-M, long-K problem
     } else if (a.M <= 4096 && a.N <= 1024) {
@@ -513,6 +517,11 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         dim3 grid((unsigned)nblk, (unsigned)nslice), block(256);
         // 8-wave LDS-DMA tiles (16-bit operands, no load-time A2 add; LayerNorm on 256-wide rows)
         if constexpr (sizeof(T) == 2) {
+            if (ln && tbm == 128 && tbn == 320) {
+                hipLaunchKernelGGL((gemm_dma_kernel<T, TO, 128, 320, 2, 2, CONV, true, 2>), grid, block, 0, stream, g, nNt);
+                KINET_LAUNCH_CHECK();
+                return KINET_OK;
+            }
             if (g.A2 == nullptr && (tbm == 256 || tbn == 256)) {
                 const dim3 blk(512);
                 if (ln)

@@ -267,6 +267,31 @@ def test_big_gemm_vs_fp32(K, big, M, N, Kd, mode):
     assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
 
 
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('M,N', [(20011, 288), (9000, 320), (8192, 300)])
+def test_wide_layernorm_gemm_vs_fp32(K, M, N, dtype):
+    """output_proj + residual + LayerNorm over rows wider than 256 (d = 288 of configs 3-5) at
+    encoder sizes (the 128 x 320 LDS-DMA tile with the fused LayerNorm epilogue), against torch
+    fp32 on the same 16-bit operands: f32 accumulation and normalisation, one output rounding
+    (bound stated with slack for the accumulation order)."""
+    g = torch.Generator().manual_seed(M + N)
+    Kd = N
+    x = torch.randn(M, Kd, generator=g).to(dtype)
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).to(dtype)
+    b = torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g).to(dtype)
+    gam, bet = torch.rand(N, generator=g) + 0.5, torch.randn(N, generator=g)
+    pre = F.linear(x.float(), w.float(), b) + r.float()
+    ref = F.layer_norm(pre, (N,), gam, bet, 1e-5)
+    y = K.linear(x.cuda(), w.cuda(), b.cuda(), residual=r.cuda(), ln=(gam.cuda(), bet.cuda(), 1e-5))
+    torch.cuda.synchronize()
+    u = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    rstd = 1.0 / pre.std(-1, unbiased=False, keepdim=True)
+    err = (y.float().cpu() - ref).abs()
+    bound = (pre.abs() * rstd * gam.abs() * 2 * u) + ref.abs() * 2 * u + 1e-3
+    assert (err <= bound).all(), (err / bound).max().item()
+
+
 @pytest.mark.parametrize('M,N,Kd', [(20000, 256, 256), (16411, 1024, 264), (16390, 128, 1024)])
 def test_big_gemm_matches_small_kernel(K, gemm_flags, M, N, Kd):
     """Both kernels accumulate the same bf16 products in the same K-step order in f32, so

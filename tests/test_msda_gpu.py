@@ -189,11 +189,11 @@ def test_fused_module_path_matches_reference(golden_dir):
 
 # ---- specialised fused kernel (16-bit values, head_dim 32, L*P in {16, 32}) vs the generic one ----
 
-def _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, seed, dtype=torch.bfloat16):
+def _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, seed, dtype=torch.bfloat16, D=32):
     g = torch.Generator().manual_seed(seed)
     L = len(shapes)
     S = sum(h * w for h, w in shapes)
-    value = torch.randn(M, B, S, 32, generator=g).to(dtype)
+    value = torch.randn(M, B, S, D, generator=g).to(dtype)
     ref = torch.rand(B, Lq, L, ref_dim, generator=g)
     if ref_dim == 4:
         ref[..., 2:] = ref[..., 2:] * 0.5 + 0.05
@@ -211,14 +211,16 @@ def _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, seed, dtype=torch.bfloat1
     (((23, 31), (12, 16), (6, 8), (3, 4), (23, 31), (12, 16), (6, 8), (3, 4)), 517, 2, 2.0),  # 8 levels (2 frames)
 ])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
-def test_fast_fused_kernel_matches_generic(shapes, Lq, ref_dim, noise, dtype):
-    """The specialised 16-bit kernel (msda_fused_fast_kernel) against the generic fused kernel
-    run in f32 on the same values (exactly representable in f32): locations and attention
-    weights to a few ulp, outputs within one 16-bit output rounding plus the f16 tap-weight
-    quantisation (2^-11 relative per weight)."""
+@pytest.mark.parametrize('D', [32, 36])
+def test_fast_fused_kernel_matches_generic(shapes, Lq, ref_dim, noise, dtype, D):
+    """The specialised 16-bit kernel (msda_fused_fast_kernel; head_dim 32: 4 lanes x 16-byte
+    gathers per query, head_dim 36 of d = 288: 9 lanes x 8-byte gathers) against the generic
+    fused kernel run in f32 on the same values (exactly representable in f32): locations and
+    attention weights to a few ulp, outputs within one 16-bit output rounding plus the f16
+    tap-weight quantisation (2^-11 relative per weight)."""
     from kinet_amd import kernels as K
     B, M, P = 2, 8, 4
-    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, Lq, dtype)
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, Lq, dtype, D=D)
     L = len(shapes)
     out_f, loc_f, aw_f = K.msda_fused(value, ss, offlog, ref, M, L, P, qmask, want_loc_attw=True, head_major=True)
     out_g, loc_g, aw_g = K.msda_fused(value.float(), ss, offlog, ref, M, L, P, qmask, want_loc_attw=True,
@@ -233,13 +235,15 @@ def test_fast_fused_kernel_matches_generic(shapes, Lq, ref_dim, noise, dtype):
     assert (out_f.float()[qmask] == 0).all()
 
 
-def test_fast_fused_kernel_vs_oracle():
-    """The specialised kernel against the C oracle (through loc/attw it reports)."""
+@pytest.mark.parametrize('D,dtype', [(32, torch.bfloat16), (36, torch.float16)])
+def test_fast_fused_kernel_vs_oracle(D, dtype):
+    """The specialised kernel against the C oracle (through loc/attw it reports); head_dim 36
+    is the d = 288 of configs 3-5 in their f16 compute dtype."""
     from kinet_amd import kernels as K
     from oracle import msda_oracle as O
     shapes = ((40, 50), (20, 25), (10, 13), (5, 7))
     B, M, P, Lq = 2, 8, 4, 700
-    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 5)
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 5, dtype=dtype, D=D)
     out, loc, aw = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, want_loc_attw=True, head_major=True)
     torch.cuda.synchronize()
     v = value.float().permute(1, 2, 0, 3).contiguous().cpu().numpy()          # (B, S, M, D)
