@@ -478,10 +478,11 @@ def main():
         mfma_ms = sum(fam[f]['ms'] for f in ('gemm', 'conv') if f in fam)
         mfma_flops = sum(fam[f]['flops'] for f in ('gemm', 'conv') if f in fam)
         # Headline roofline: the MSDA sampling kernel with the most device time in the
-        # rocprofv3 summary (profiles/).  config 2: msda_enc_lds_kernel, which runs the 6
+        # rocprofv3 summary (profiles/).  config 2: msda_enc_kernel, which runs the 6
         # encoder calls per frame batch (avg_launch_ms = the rocprof average of that kernel
         # name); the 6 decoder calls run msda_fused_fast_kernel, reported beside it.
-        # config 5 (D=36): the generic msda_fused_kernel over all its launches.
+        # config 5 (D=36): the generic msda_fused_kernel -- the encoder launches, the decoder
+        # launches beside them.
         msda_roof = None
         if msda:
             def roof(launches, kname, pmc_name):
@@ -508,8 +509,14 @@ def main():
                               bytes_basis='value rows touched by the bilinear corners (counted from one forward) + '
                                           'offsets/logits + references + output')
                 msda_roof['all_msda_launches'] = roof(msda, 'encoder + decoder launches', None)
+            elif enc:
+                msda_roof = roof(enc, 'msda_fused_kernel<f16_t, 4> (D=36, encoder launches, Lq = S = %d)' % enc[0][0],
+                                 None)
+                if dec:
+                    msda_roof['decoder_kernel'] = roof(dec, 'msda_fused_kernel<f16_t, 4> (D=36, decoder launches)', None)
+                msda_roof['all_msda_launches'] = roof(msda, 'encoder + decoder launches', None)
             else:
-                msda_roof = roof(msda, 'msda_fused_kernel<f16_t, 4> (D=36, encoder + decoder launches)', None)
+                msda_roof = roof(msda, 'msda_fused_kernel (all launches)', None)
             msda_roof['encoder_launch'] = {'ms': msda_enc_ms, 'bytes': enc[0][3] if enc else None}
             msda_roof['decoder_launch'] = {'ms': msda_dec_ms, 'bytes': dec[0][3] if dec else None}
         mfma_ach = mfma_flops / (mfma_ms * 1e-3) / 1e12 if mfma_ms else 0.0

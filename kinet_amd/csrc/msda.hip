@@ -494,23 +494,15 @@ __device__ __forceinline__ void widen2(uint32_t u, f32x2& x) {
     }
 }
 
-// MH heads (waves) per workgroup, SG samples gathered per group (SG x 4 loads in flight per lane).
-// D = 32: 4 lanes x 8 channels (16-byte gathers) per query, 16 queries per wave; D = 36 (d = 288,
-// configs 3-5): 9 lanes x 4 channels (8-byte gathers) per query, 7 queries per pass, 4 passes
-// per 28-query tile (lane 63 idle).
-template <typename T, typename TO, typename TL, int L, int P, int MH = kThreads / 64, int SG = 4, int D = 32>
+// MH heads (waves) per workgroup, SG samples gathered per group (SG x 4 loads in flight per lane)
+template <typename T, typename TO, typename TL, int L, int P, int MH = kThreads / 64, int SG = 4>
 __global__ __launch_bounds__(MH * 64) void msda_fused_fast_kernel(
     const T* __restrict__ value, long vsb, int vss, long vsm, int head_bytes, const int64_t* __restrict__ shapes,
     const TL* __restrict__ offlog, int ld_off, const float* __restrict__ ref, int ref_dim,
     const uint8_t* __restrict__ qmask, float* __restrict__ loc_out, float* __restrict__ attw_out,
     TO* __restrict__ out, int S, int M, int Lq, const int* __restrict__ torder) {
     static_assert(sizeof(T) == 2 && sizeof(TO) == 2, "16-bit values and output");
-    static_assert(D == 32 || D == 36, "head_dim 32 or 36");
-    constexpr int LPQ = D == 32 ? 4 : 9;            // lanes per query in phase 2
-    constexpr int CPL = D / LPQ;                    // channels per lane (8 or 4)
-    constexpr int QPW = 64 / LPQ;                   // queries per phase-2 pass (16 or 7)
-    constexpr int NPASS = D == 32 ? 1 : 4;
-    constexpr int QT = QPW * NPASS, LP = L * P, NT = MH * 64;
+    constexpr int D = 32, QT = 16, LP = L * P, NT = MH * 64;
     static_assert((LP & (LP - 1)) == 0 && LP <= 64 && L <= kMaxLevels, "L*P: power of two <= 64");
     constexpr int NSB = MH * QT * LP;               // samples per workgroup
     constexpr unsigned OOB = 0x80000000u;
@@ -627,73 +619,60 @@ __global__ __launch_bounds__(MH * 64) void msda_fused_fast_kernel(
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int m = mh0 + wave;
     if (m >= M) return;
+    const int qi = lane >> 2, q = q0 + qi;
+    const unsigned cb = (unsigned)(lane & 3) * 16u;   // this lane's 8 channels, bytes
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(value + (long)b * vsb + (long)m * vsm), (short)0, head_bytes, 0x00020000);
-    const int ql = lane / LPQ, cl = lane - ql * LPQ;
-    const unsigned cb = (unsigned)cl * (unsigned)(CPL * 2);   // this lane's channels, bytes
+    const int4* tpo = toff + (wave * QT + qi) * LP;
+    const uint2* tpw = twt + (wave * QT + qi) * LP;
+    f32x2 acc[4] = {};
 #pragma unroll 1
-    for (int pass = 0; pass < NPASS; ++pass) {
-        const int qi = pass * QPW + ql, q = q0 + qi;
-        const bool lane_on = D == 32 || lane < QPW * LPQ;
-        const int4* tpo = toff + (wave * QT + (lane_on ? qi : 0)) * LP;
-        const uint2* tpw = twt + (wave * QT + (lane_on ? qi : 0)) * LP;
-        f32x2 acc[CPL / 2] = {};
-#pragma unroll 1
-        for (int s = 0; s < LP; s += SG) {
-            typedef uint32_t WV __attribute__((ext_vector_type(CPL / 2)));
-            WV v[SG][4];
+    for (int s = 0; s < LP; s += SG) {
+        u32x4v v[SG][4];
 #pragma unroll
-            for (int g = 0; g < SG; ++g) {
-                const int4 o = tpo[s + g];
-                if constexpr (D == 32) {
-                    v[g][0] = __builtin_bit_cast(WV, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.x + cb, 0, 0));
-                    v[g][1] = __builtin_bit_cast(WV, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.y + cb, 0, 0));
-                    v[g][2] = __builtin_bit_cast(WV, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.z + cb, 0, 0));
-                    v[g][3] = __builtin_bit_cast(WV, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.w + cb, 0, 0));
+        for (int g = 0; g < SG; ++g) {
+            const int4 o = tpo[s + g];
+            v[g][0] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.x + cb, 0, 0));
+            v[g][1] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.y + cb, 0, 0));
+            v[g][2] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.z + cb, 0, 0));
+            v[g][3] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, (unsigned)o.w + cb, 0, 0));
+        }
+        uint2 wq[SG];
+#pragma unroll
+        for (int g = 0; g < SG; ++g) wq[g] = tpw[s + g];
+#pragma unroll
+        for (int g = 0; g < SG; ++g)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t wp = k < 2 ? wq[g].x : wq[g].y;   // f16 weights of corners (k & ~1, k | 1)
+                if constexpr (std::is_same<T, f16_t>::value) {
+                    // f16 values x f16 weights, f32 accumulate: one v_fma_mix_f32 per MAC
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        acc[j][0] = (k & 1) ? fma_mix16_lo_hi(acc[j][0], v[g][k][j], wp) : fma_mix16_lo_lo(acc[j][0], v[g][k][j], wp);
+                        acc[j][1] = (k & 1) ? fma_mix16_hi_hi(acc[j][1], v[g][k][j], wp) : fma_mix16_hi_lo(acc[j][1], v[g][k][j], wp);
+                    }
                 } else {
-                    v[g][0] = __builtin_bit_cast(WV, __builtin_amdgcn_raw_buffer_load_b64(rv, (unsigned)o.x + cb, 0, 0));
-                    v[g][1] = __builtin_bit_cast(WV, __builtin_amdgcn_raw_buffer_load_b64(rv, (unsigned)o.y + cb, 0, 0));
-                    v[g][2] = __builtin_bit_cast(WV, __builtin_amdgcn_raw_buffer_load_b64(rv, (unsigned)o.z + cb, 0, 0));
-                    v[g][3] = __builtin_bit_cast(WV, __builtin_amdgcn_raw_buffer_load_b64(rv, (unsigned)o.w + cb, 0, 0));
-                }
-            }
-            uint2 wq[SG];
+                    // bf16 values: widen by shift / mask, then v_pk_fma_f32 (1.5 VALU per MAC)
+                    const float wk = (float)__builtin_bit_cast(f16_t, (uint16_t)((k & 1) ? (wp >> 16) : (wp & 0xffffu)));
+                    const f32x2 w2 = {wk, wk};
 #pragma unroll
-            for (int g = 0; g < SG; ++g) wq[g] = tpw[s + g];
-#pragma unroll
-            for (int g = 0; g < SG; ++g)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t wp = k < 2 ? wq[g].x : wq[g].y;   // f16 weights of corners (k & ~1, k | 1)
-                    if constexpr (std::is_same<T, f16_t>::value) {
-                        // f16 values x f16 weights, f32 accumulate: one v_fma_mix_f32 per MAC
-#pragma unroll
-                        for (int j = 0; j < CPL / 2; ++j) {
-                            acc[j][0] = (k & 1) ? fma_mix16_lo_hi(acc[j][0], v[g][k][j], wp) : fma_mix16_lo_lo(acc[j][0], v[g][k][j], wp);
-                            acc[j][1] = (k & 1) ? fma_mix16_hi_hi(acc[j][1], v[g][k][j], wp) : fma_mix16_hi_lo(acc[j][1], v[g][k][j], wp);
-                        }
-                    } else {
-                        // bf16 values: widen by shift / mask, then v_pk_fma_f32 (1.5 VALU per MAC)
-                        const float wk = (float)__builtin_bit_cast(f16_t, (uint16_t)((k & 1) ? (wp >> 16) : (wp & 0xffffu)));
-                        const f32x2 w2 = {wk, wk};
-#pragma unroll
-                        for (int j = 0; j < CPL / 2; ++j) {
-                            f32x2 x;
-                            widen2<T>(v[g][k][j], x);
-                            acc[j] = __builtin_elementwise_fma(x, w2, acc[j]);
-                        }
+                    for (int j = 0; j < 4; ++j) {
+                        f32x2 x;
+                        widen2<T>(v[g][k][j], x);
+                        acc[j] = __builtin_elementwise_fma(x, w2, acc[j]);
                     }
                 }
-        }
-        if (!lane_on || q >= Lq) continue;
-        VecT<TO, CPL> o;
-#pragma unroll
-        for (int j = 0; j < CPL / 2; ++j) {
-            o.v[2 * j] = Cvt<TO>::from(acc[j][0]);
-            o.v[2 * j + 1] = Cvt<TO>::from(acc[j][1]);
-        }
-        *reinterpret_cast<VecT<TO, CPL>*>(out + ((long)b * Lq + q) * M * D + (long)m * D + cl * CPL) = o;
+            }
     }
+    if (q >= Lq) return;
+    VecT<TO, 8> o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        o.v[2 * j] = Cvt<TO>::from(acc[j][0]);
+        o.v[2 * j + 1] = Cvt<TO>::from(acc[j][1]);
+    }
+    *reinterpret_cast<VecT<TO, 8>*>(out + ((long)b * Lq + q) * M * D + (long)m * D + (lane & 3) * 8) = o;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1367,7 +1346,7 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
     KINET_CHECK_ARG(c.lpq <= 64, "msda fused: head_dim/vec (%d) exceeds a wave", c.lpq);
     if (N == 0 || Lq == 0) return KINET_OK;
     if constexpr (sizeof(T) == 2) {
-        // specialised kernel: head_dim 32 or 36, (L, P) in {(4, 4), (8, 4)}, aligned vectors
+        // specialised kernel: head_dim 32, (L, P) in {(4, 4), (8, 4)}, 16-byte aligned vectors
         const long long head_bytes = ((long long)(S - 1) * vss + D) * (long long)sizeof(T);
         if (D == 32 && P == 4 && (L == 4 || L == 8) && vss % 8 == 0 && vsb % 8 == 0 && vsm % 8 == 0 &&
             ((uintptr_t)value % 16) == 0 && head_bytes < (1LL << 31)) {
@@ -1384,23 +1363,6 @@ int launch_fused(const void* value, long vsb, int vss, long vsm, const int64_t* 
                                    (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v, ld_off,
                                    ref, ref_dim, qmask, loc_out,
                                    attw_out, (TO*)out, S, M, Lq, torder);
-            KINET_LAUNCH_CHECK();
-            return KINET_OK;
-        }
-        // head_dim 36 (d = 288): 9 lanes x 8-byte gathers per query, 28-query tiles (natural
-        // order: query_tile_order indexes 16-query tiles and is ignored here, as it is by the
-        // generic kernel; outputs do not depend on the order)
-        if (D == 36 && P == 4 && (L == 4 || L == 8) && vss % 4 == 0 && vsb % 4 == 0 && vsm % 4 == 0 &&
-            ((uintptr_t)value % 8) == 0 && head_bytes < (1LL << 31)) {
-            dim3 g2((Lq + 27) / 28, N, (M + 1) / 2);
-            if (L == 4)
-                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 4, 4, 2, 2, 36>), g2, dim3(128), 0, stream,
-                                   (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v,
-                                   ld_off, ref, ref_dim, qmask, loc_out, attw_out, (TO*)out, S, M, Lq, nullptr);
-            else
-                hipLaunchKernelGGL((msda_fused_fast_kernel<T, TO, TL, 8, 4, 2, 2, 36>), g2, dim3(128), 0, stream,
-                                   (const T*)value, vsb, vss, vsm, (int)head_bytes, shapes, (const TL*)offlog_v,
-                                   ld_off, ref, ref_dim, qmask, loc_out, attw_out, (TO*)out, S, M, Lq, nullptr);
             KINET_LAUNCH_CHECK();
             return KINET_OK;
         }
