@@ -415,43 +415,49 @@ void launch_cfg(const GemmArgs& a, hipStream_t stream) {
 }
 
 // deepest DMA ring (<= 4 row tiles) that keeps the workgroup within 80 KiB of LDS (two per CU)
-template <int KC, int BMR, bool HAS_R, bool LN, bool HAS_A2>
+template <int KC, int BMR, bool HAS_R, bool LN, bool HAS_A2, int NT = 4>
 constexpr int ring_depth() {
-    constexpr int base = RwCfg<KC, 4, BMR, 1, HAS_R, LN, HAS_A2>::BYTES -
-                         RwCfg<KC, 4, BMR, 1, HAS_R, LN, HAS_A2>::STAGE;
-    constexpr int stage = RwCfg<KC, 4, BMR, 1, HAS_R, LN, HAS_A2>::STAGE;
+    constexpr int base = RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2>::BYTES -
+                         RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2>::STAGE;
+    constexpr int stage = RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2>::STAGE;
     return (80 * 1024 - base) / stage >= 4 ? 4 : (80 * 1024 - base) / stage;
 }
 
-template <typename T, typename TO, int KC, bool HAS_R, bool LN, bool HAS_A2>
+template <typename T, typename TO, int KC, bool HAS_R, bool LN, bool HAS_A2, int NT = 4>
 void launch_ring(const GemmArgs& a, hipStream_t stream) {
     // 16-row tiles when a tile carries a second operand (residual / A2) or the LayerNorm
-    // epilogue (which needs them at K = 256 to stay in 256 VGPRs): a 4-deep ring then fits;
-    // K = 64 rows (128 B) need 32-row tiles for whole 4 KiB DMA rounds
-    constexpr int BMR = (KC == 2 || (!HAS_R && !LN && !HAS_A2)) ? 32 : 16;
-    constexpr int NS = ring_depth<KC, BMR, HAS_R, LN, HAS_A2>();
+    // epilogue (which needs them at K = 256 to stay in 256 VGPRs) or a K of 512+ (1-2 KiB
+    // rows): a 2-4 deep ring then fits; K = 64 rows (128 B) need 32-row tiles for whole 4 KiB
+    // DMA rounds
+    constexpr int BMR = (KC == 2 || (KC <= 8 && !HAS_R && !LN && !HAS_A2)) ? 32 : 16;
+    constexpr int NS = ring_depth<KC, BMR, HAS_R, LN, HAS_A2, NT>();
     static_assert(NS >= 2, "LDS budget");
-    launch_cfg<T, TO, KC, BMR, NS, HAS_R, LN, HAS_A2>(a, stream);
+    launch_cfg<T, TO, KC, BMR, NS, HAS_R, LN, HAS_A2, NT>(a, stream);
 }
 
-template <typename T, typename TO, int KC>
+template <typename T, typename TO, int KC, int NT = 4>
 void launch_k(const GemmArgs& a, hipStream_t stream) {
     const bool r = a.R != nullptr, ln = a.ln_g != nullptr;
     if (a.A2 != nullptr) {
         // the query + position-embedding projections (no residual / LayerNorm there)
         if (r || ln) return;
-        launch_ring<T, TO, KC, false, false, true>(a, stream);
-    } else if (r && ln) launch_ring<T, TO, KC, true, true, false>(a, stream);
-    else if (r) launch_ring<T, TO, KC, true, false, false>(a, stream);
-    else if (ln) launch_ring<T, TO, KC, false, true, false>(a, stream);
-    else launch_ring<T, TO, KC, false, false, false>(a, stream);
+        launch_ring<T, TO, KC, false, false, true, NT>(a, stream);
+    } else if (r && ln) launch_ring<T, TO, KC, true, true, false, NT>(a, stream);
+    else if (r) launch_ring<T, TO, KC, true, false, false, NT>(a, stream);
+    else if (ln) launch_ring<T, TO, KC, false, true, false, NT>(a, stream);
+    else launch_ring<T, TO, KC, false, false, false, NT>(a, stream);
 }
 
+// K = 512 (the ResNet 1x1 convs into the layer-2 bottlenecks, input_proj of level 0): the
+// weight slice stays at 128 VGPRs per wave by narrowing the column group to 128 columns
+// (NT = 2) -- the host routes only N <= 256 without residual / LayerNorm / A2 here (at most
+// 2 column groups, which share each row tile through the XCD's L2)
 template <typename T, typename TO>
 void launch_t(const GemmArgs& a, hipStream_t stream) {
     if (a.K == 64) launch_k<T, TO, 2>(a, stream);
     else if (a.K == 128) launch_k<T, TO, 4>(a, stream);
-    else launch_k<T, TO, 8>(a, stream);
+    else if (a.K == 256) launch_k<T, TO, 8>(a, stream);
+    else launch_ring<T, TO, 16, false, false, false, 2>(a, stream);   // K == 512
 }
 
 bool al16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
@@ -464,7 +470,9 @@ thread_local int rw_min_m = 4096;   // smallest M routed to the resident-weight 
 // fits it; false leaves the call to the tiled kernel.
 bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t stream) {
     if (in_dtype != KINET_BF16 && in_dtype != KINET_F16) return false;
-    if (a.M < rw_min_m || (a.K != 64 && a.K != 128 && a.K != 256)) return false;
+    if (a.M < rw_min_m || (a.K != 64 && a.K != 128 && a.K != 256 && a.K != 512)) return false;
+    if (a.K == 512 && (a.N > 256 || a.R != nullptr || a.ln_g != nullptr || a.A2 != nullptr || (kinet_gemm_flags & 256)))
+        return false;
     if (a.A2 != nullptr && (a.R != nullptr || a.ln_g != nullptr || !al16(a.A2))) return false;
     if (a.N % 8 != 0 || (a.ln_g != nullptr && a.N > 256)) return false;
     const bool o16 = out_dtype == in_dtype || (in_dtype == KINET_BF16 && out_dtype == KINET_F16);

@@ -353,7 +353,7 @@ def test_big_conv_vs_fp32(K, big, B, H, W, Cin, Cout, k, s, p):
     assert (err <= 1e-2 * y_ref.abs() + 2e-2).all(), err.max().item()
 
 
-# ---- resident-weight streaming kernel (gemm_rw.hip: 16-bit, K in {64, 128, 256}, M >= 4096) ----
+# ---- resident-weight streaming kernel (gemm_rw.hip: 16-bit, K in {64, 128, 256, 512}, M >= 4096) ----
 
 def _rw_case(M, N, Kd, mode, seed):
     g = torch.Generator().manual_seed(seed)
@@ -392,6 +392,7 @@ def _rw_case(M, N, Kd, mode, seed):
     (8197, 200, 256, 'res_ln'), (8197, 200, 128, 'relu_mask'), (16800, 256, 64, 'res_relu'),
     (16800, 512, 128, 'res'), (5000, 64, 64, 'plain'), (4099, 1032, 256, 'f32'),
     (20001, 256, 256, 'res_relu_mask'),
+    (9001, 128, 512, 'relu'), (8200, 256, 512, 'plain'), (8197, 200, 512, 'f32'),   # K = 512: 128-column groups
 ])
 def test_rw_gemm_vs_fp32(K, M, N, Kd, mode):
     x, w, b, kw, ref = _rw_case(M, N, Kd, mode, M + N + Kd)
@@ -404,7 +405,8 @@ def test_rw_gemm_vs_fp32(K, M, N, Kd, mode):
 
 
 @pytest.mark.parametrize('M,N,Kd,mode', [(10001, 256, 256, 'res_ln_mask'), (12345, 1024, 256, 'relu'),
-                                         (8200, 384, 256, 'add_f32'), (16800, 256, 64, 'res_relu')])
+                                         (8200, 384, 256, 'add_f32'), (16800, 256, 64, 'res_relu'),
+                                         (9001, 128, 512, 'relu'), (8200, 256, 512, 'mask')])
 def test_rw_matches_tiled_kernel(K, gemm_flags, M, N, Kd, mode):
     """Same bf16 products summed in the same K order in f32: the two kernels agree to
     (nearly) the last bit."""
@@ -436,18 +438,21 @@ def test_rw_headmajor_value_proj(K):
     assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
 
 
-@pytest.mark.parametrize('Cin,Cout', [(64, 256), (256, 64), (128, 512), (256, 1024)])
-def test_rw_conv1x1(K, Cin, Cout):
+@pytest.mark.parametrize('Cin,Cout,res', [(64, 256, True), (256, 64, True), (128, 512, True), (256, 1024, True),
+                                          (512, 128, False), (512, 256, False)])
+def test_rw_conv1x1(K, Cin, Cout, res):
     B, H, W = 4, 60, 70
     g = torch.Generator().manual_seed(Cin + Cout)
     x = torch.randn(B, Cin, H, W, generator=g).bfloat16()
     w = (torch.randn(Cout, Cin, 1, 1, generator=g) * (2.0 / Cin) ** 0.5).bfloat16()
     scale = torch.rand(Cout, generator=g) + 0.5
     bias = torch.randn(Cout, generator=g) * 0.1
-    res = torch.randn(B, Cout, H, W, generator=g).bfloat16()
-    ref = F.relu(F.conv2d(x.float(), w.float()) * scale[None, :, None, None] + bias[None, :, None, None] + res.float())
+    r = torch.randn(B, Cout, H, W, generator=g).bfloat16() if res else None
+    ref = F.conv2d(x.float(), w.float()) * scale[None, :, None, None] + bias[None, :, None, None]
+    ref = F.relu(ref + r.float() if res else ref)
     y = K.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().cuda(), K.pack_conv_weight(w.cuda(), torch.bfloat16), 1, 0,
-                      scale=scale.cuda(), bias=bias.cuda(), relu=True, residual=res.permute(0, 2, 3, 1).contiguous().cuda())
+                      scale=scale.cuda(), bias=bias.cuda(), relu=True,
+                      residual=r.permute(0, 2, 3, 1).contiguous().cuda() if res else None)
     torch.cuda.synchronize()
     err = (y.permute(0, 3, 1, 2).float().cpu() - ref).abs()
     assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
