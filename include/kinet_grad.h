@@ -75,6 +75,55 @@ int kinet_mha_backward(const float* Q, int ldq, const float* K, int ldk, const f
                        int heads, int head_dim, float scale, const uint8_t* key_mask, float* workspace,
                        float dropout_p, const int64_t* dropout_seed, kinet_stream_t stream);
 
+/* ---- training-path glue (kinet_amd/csrc/train_ops.hip), f32, replacing torch elementwise ops.
+ * Dropout keep masks: the counter hash of kinet_dropout_mask (include/kinet_ops.h) over the
+ * element's flat index, keyed by the device int64 *dropout_seed; kept values scaled 1/(1-p). */
+
+/* Post-norm residual sub-layer y = LayerNorm(x + dropout_p(r)) over rows of d <= 1024
+ * (deformable_transformer.py:100,108,186,196,199: `norm(src + dropout(src2))`). */
+int kinet_dropout_add_layernorm(const float* x, const float* r, const float* gamma, const float* beta, float* y,
+                                int rows, int d, float eps, float dropout_p, const int64_t* dropout_seed,
+                                kinet_stream_t stream);
+/* Its backward (x + dropout(r) recomputed from x, r and the seed): dx = dL/d(x + Z r), dr = Z dx,
+ * dgamma / dbeta (both or neither; fixed-order partial sums in `workspace`, sized by
+ * kinet_dropout_add_layernorm_backward_workspace floats).  dx or dr may be NULL. */
+int64_t kinet_dropout_add_layernorm_backward_workspace(int rows, int d);
+int kinet_dropout_add_layernorm_backward(const float* dy, const float* x, const float* r, const float* gamma,
+                                         float* dx, float* dr, float* dgamma, float* dbeta, int rows, int d,
+                                         float eps, float dropout_p, const int64_t* dropout_seed, float* workspace,
+                                         kinet_stream_t stream);
+
+/* y = dropout_p(relu ? max(x, 0) : x), n elements (the FFN hidden, deformable_transformer.py:99,185);
+ * backward dx = Z * dy * (relu ? [y > 0] : 1).  16-byte aligned buffers. */
+int kinet_dropout_act(const float* x, float* y, int64_t n, int relu, float dropout_p, const int64_t* dropout_seed,
+                      kinet_stream_t stream);
+int kinet_dropout_act_backward(const float* dy, const float* y, float* dx, int64_t n, int relu, float dropout_p,
+                               const int64_t* dropout_seed, kinet_stream_t stream);
+
+/* MSDeformAttn sampling preparation (ms_deform_attn.py:64-82) from the packed projection output
+ * offlog (nq = N*Lq rows of stride ld floats: heads*L*P*2 sampling offsets (m, l, p, xy), then
+ * heads*L*P attention logits (m, l, p) -- one GEMM over the concatenated sampling_offsets |
+ * attention_weights weights): per (row, head) attw = softmax over the L*P logits (0 where
+ * query_mask), loc = ref + off / (H_l, W_l) for 2-d refs (the reference's divisor order) or
+ * ref_xy + off / P * ref_wh * 0.5 for 4-d refs.  loc (nq, heads, L, P, 2), attw (nq, heads, L, P),
+ * refs (nq, L, ref_dim), shapes (L, 2) int64 (H, W). */
+int kinet_msda_prep(const float* offlog, int64_t ld, const float* refs, const int64_t* shapes,
+                    const uint8_t* query_mask, float* loc, float* attw, int64_t nq, int heads, int levels, int points,
+                    int ref_dim, kinet_stream_t stream);
+/* Its backward: grad_offlog (same layout and stride as offlog: offset gradients, then the softmax
+ * backward through attw), grad_refs (summed over heads and points); either may be NULL.  heads a
+ * power of two <= 64. */
+int kinet_msda_prep_backward(const float* grad_loc, const float* grad_attw, const float* attw, const float* offlog,
+                             int64_t ld, const float* refs, const int64_t* shapes, float* grad_offlog,
+                             float* grad_refs, int64_t nq, int heads, int levels, int points, int ref_dim,
+                             kinet_stream_t stream);
+
+/* inverse_sigmoid (util/misc.py:609-613): y = log(max(c, eps) / max(1 - c, eps)), c = clamp(x, 0, 1),
+ * and its backward through the clamps' gradient masks. */
+int kinet_inverse_sigmoid(const float* x, float* y, int64_t n, float eps, kinet_stream_t stream);
+int kinet_inverse_sigmoid_backward(const float* dy, const float* x, float* dx, int64_t n, float eps,
+                                   kinet_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,15 @@ _SIGS = {
     'kinet_mha_backward': [P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, F, P, P, F, P, P],
     'kinet_mha_core_dropout': [P, I, P, I, P, I, P, I] + [I] * 5 + [F, I, P, F, P, P],
     'kinet_dropout_mask': [P, I64, F, P, P],
+    'kinet_dropout_add_layernorm': [P] * 5 + [I, I, F, F, P, P],
+    'kinet_dropout_add_layernorm_backward_workspace': [I, I],
+    'kinet_dropout_add_layernorm_backward': [P] * 8 + [I, I, F, F, P, P, P],
+    'kinet_dropout_act': [P, P, I64, I, F, P, P],
+    'kinet_dropout_act_backward': [P, P, P, I64, I, F, P, P],
+    'kinet_msda_prep': [P, I64] + [P] * 5 + [I64, I, I, I, I, P],
+    'kinet_msda_prep_backward': [P] * 4 + [I64] + [P] * 4 + [I64, I, I, I, I, P],
+    'kinet_inverse_sigmoid': [P, P, I64, F, P],
+    'kinet_inverse_sigmoid_backward': [P, P, P, I64, F, P],
     'kinet_last_error': [],
     'kinet_version': [],
 }
@@ -74,6 +83,7 @@ _RESTYPES = {'kinet_last_error': ctypes.c_char_p, 'kinet_version': ctypes.c_char
              'kinet_groupnorm_workspace': ctypes.c_long,
              'kinet_gemm_tn_workspace': ctypes.c_int64, 'kinet_colsum_workspace': ctypes.c_int64,
              'kinet_layernorm_backward_workspace': ctypes.c_int64,
+             'kinet_dropout_add_layernorm_backward_workspace': ctypes.c_int64,
              'kinet_groupnorm_backward_workspace': ctypes.c_int64,
              'kinet_mha_backward_workspace': ctypes.c_int64}
 

@@ -6,14 +6,21 @@ The reference trains the detector with `losses.backward()` (src/trackformer/engi
 (cuDNN / cuBLAS); kinet_amd's autograd path (DeformableDETR._forward_reference and the
 transformer / backbone modules under autograd) calls these functions instead, so a
 training step runs no vendor GEMM / convolution library kernel.  Compute dtype is f32, as
-the reference trains (no AMP anywhere in src/); elementwise glue (ReLU masks, adds,
-sigmoid, dropout, softmax of the sampling weights) stays in torch.
+the reference trains (no AMP anywhere in src/).  The transformer's elementwise glue runs on
+kinet kernels too (csrc/train_ops.hip): residual dropout + LayerNorm, dropout(relu) of the
+FFN hidden, the MSDA softmax / sampling-location preparation and inverse_sigmoid, one kernel
+each way; what stays in torch is autograd's own gradient accumulation, the loss and the
+sigmoid / masked_fill glue of the heads.
 
     linear(x, weight, bias)                 nn.Linear
     layer_norm(x, weight, bias, eps)        nn.LayerNorm over the last dim
     group_norm_nhwc(x, groups, w, b, eps)   nn.GroupNorm on (B, HW, C)
     conv_nhwc(x, weight, ...)               nn.Conv2d (+ FrozenBatchNorm2d, residual, ReLU) on NHWC
     mha_core(q, k, v, heads, key_mask)      the softmax(QK^T / sqrt(d)) V core of nn.MultiheadAttention
+    dropout_add_layer_norm(x, r, ln, drop)  ln(x + drop(r)), the post-norm residual sub-layer
+    dropout_act(x, drop)                    drop(relu(x)), the FFN hidden
+    msda_prep(off, logits, refs, ...)       MSDeformAttn sampling locations + softmaxed weights
+    inverse_sigmoid(x)                      util/misc.py:609-613
 
 Weight gradients are reductions over the row (pixel / token) dimension (kinet_gemm_tn,
 split-K with a fixed-order finalize), input gradients are GEMMs against the transposed
@@ -236,3 +243,125 @@ def multihead_attention(mod, query, key, value, key_padding_mask=None):
     p = mod.dropout if mod.training else 0.0
     o = mha_core(q, k, v, mod.num_heads, mod.head_dim ** -0.5, key_padding_mask, dropout_p=p)
     return linear(o, mod.out_proj.weight, mod.out_proj.bias)
+
+
+# ------------------------------------------------------- training glue (csrc/train_ops.hip)
+_ZERO_SEED = {}
+
+
+def _seed(device, p):
+    """A fresh device seed when dropout is active, else a cached zero seed (p = 0 keeps all)."""
+    if p > 0:
+        return K.dropout_seed(device)
+    s = _ZERO_SEED.get(device)
+    if s is None:
+        s = _ZERO_SEED[device] = torch.zeros(1, dtype=torch.int64, device=device)
+    return s
+
+
+def _drop_p(drop):
+    return float(drop.p) if drop is not None and drop.training else 0.0
+
+
+class _DropoutAddLayerNorm(Function):
+    @staticmethod
+    def forward(ctx, x, r, weight, bias, eps, p, seed):
+        _f32(x)
+        _f32(r)
+        y = K.dropout_add_layernorm(x, r, weight.detach(), bias.detach(), eps, p, seed)
+        ctx.save_for_backward(x, r, weight, seed)
+        ctx.conf = (eps, p)
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        x, r, weight, seed = ctx.saved_tensors
+        eps, p = ctx.conf
+        ng = ctx.needs_input_grad
+        dx, dr, dg, db = K.dropout_add_layernorm_backward(dy.float(), x, r, weight, eps, p, seed, need_x=ng[0],
+                                                          need_r=ng[1], need_params=ng[2] or ng[3])
+        return dx, dr, dg if ng[2] else None, db if ng[3] else None, None, None, None
+
+
+def dropout_add_layer_norm(x, r, ln, drop):
+    """ln(x + drop(r)) -- the post-norm residual sub-layer (deformable_transformer.py:100,108,
+    186,196,199) as one kernel forward and one backward; `drop` an nn.Dropout (its p applies in
+    training mode), the keep mask from a device seed drawn from torch's CUDA generator."""
+    p = _drop_p(drop)
+    return _DropoutAddLayerNorm.apply(x, r, ln.weight, ln.bias, float(ln.eps), p, _seed(x.device, p))
+
+
+class _DropoutAct(Function):
+    @staticmethod
+    def forward(ctx, x, p, seed, relu):
+        _f32(x)
+        y = K.dropout_act(x, p, seed, relu)
+        ctx.save_for_backward(y if relu else None, seed)
+        ctx.conf = (p, relu)
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        y, seed = ctx.saved_tensors
+        p, relu = ctx.conf
+        return K.dropout_act_backward(dy.float(), y, p, seed, relu), None, None, None
+
+
+def dropout_act(x, drop, relu=True):
+    """drop(relu(x)) (the FFN hidden, deformable_transformer.py:99,185) in one kernel each way."""
+    p = _drop_p(drop)
+    return _DropoutAct.apply(x, p, _seed(x.device, p), relu)
+
+
+class _MSDAPrep(Function):
+    @staticmethod
+    def forward(ctx, offlog, refs, shapes, query_mask, heads, levels, points):
+        _f32(offlog)
+        loc, attw = K.msda_prep(offlog, refs.float(), shapes, query_mask, heads, levels, points)
+        ctx.save_for_backward(attw, offlog, refs, shapes)
+        ctx.conf = (heads, levels, points)
+        return loc, attw
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dloc, dattw):
+        attw, offlog, refs, shapes = ctx.saved_tensors
+        heads, levels, points = ctx.conf
+        ng = ctx.needs_input_grad
+        dloc = torch.zeros(attw.shape + (2,), dtype=torch.float32, device=attw.device) if dloc is None else dloc.float()
+        dattw = torch.zeros_like(attw) if dattw is None else dattw.float()
+        dol, dref = K.msda_prep_backward(dloc, dattw, attw, offlog, refs.float(), shapes, heads, levels, points,
+                                         need_offlog=ng[0], need_refs=ng[1])
+        if dref is not None and dref.dtype != refs.dtype:
+            dref = dref.to(refs.dtype)
+        return dol, dref, None, None, None, None, None
+
+
+def msda_prep(offlog, refs, shapes, query_mask, heads, levels, points):
+    """(sampling_locations, attention_weights) of MSDeformAttn (ms_deform_attn.py:64-82) from the
+    packed projection offlog (N, Lq, M*L*P*2 offsets | M*L*P logits) and refs (N, Lq, L, 2|4):
+    loc (N, Lq, M, L, P, 2), attw (N, Lq, M, L, P) (softmax over L*P, 0 at masked queries);
+    differentiable w.r.t. offlog and refs, one kernel each way."""
+    return _MSDAPrep.apply(offlog, refs, shapes, query_mask, heads, levels, points)
+
+
+class _InverseSigmoid(Function):
+    @staticmethod
+    def forward(ctx, x, eps):
+        xc = x.contiguous()
+        ctx.save_for_backward(xc)
+        ctx.eps = eps
+        return K.inverse_sigmoid(xc, eps)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        x, = ctx.saved_tensors
+        return K.inverse_sigmoid_backward(dy.float(), x, ctx.eps), None
+
+
+def inverse_sigmoid(x, eps=1e-5):
+    """util/misc.py:609-613 on f32 device tensors, one kernel each way."""
+    return _InverseSigmoid.apply(x, float(eps))

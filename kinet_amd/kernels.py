@@ -752,6 +752,111 @@ def layernorm_backward(dy, x, gamma, eps, need_params=True):
     return dx.view(x.shape), dg, db
 
 
+def _rows(t, d):
+    t = t.reshape(-1, d)
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def dropout_add_layernorm(x, r, weight, bias, eps, p, seed):
+    """LayerNorm(x + dropout_p(r)) over the last dim, f32 (kinet_dropout_add_layernorm)."""
+    d = x.shape[-1]
+    x2, r2 = _rows(x, d), _rows(r, d)
+    y = torch.empty_like(x2)
+    N.call('kinet_dropout_add_layernorm', N.ptr(x2), N.ptr(r2), N.ptr(f32(weight)), N.ptr(f32(bias)), N.ptr(y),
+           x2.shape[0], d, float(eps), float(p), N.ptr(seed), N.stream(x.device),
+           work={'family': 'norm', 'bytes': 3 * x2.numel() * 4})
+    return y.view(x.shape)
+
+
+def dropout_add_layernorm_backward(dy, x, r, gamma, eps, p, seed, need_x=True, need_r=True, need_params=True):
+    d = x.shape[-1]
+    dy2, x2, r2 = _rows(dy, d), _rows(x, d), _rows(r, d)
+    rows = x2.shape[0]
+    dx = torch.empty_like(x2) if need_x else None
+    dr = torch.empty_like(x2) if need_r else None
+    dg = torch.empty(d, dtype=torch.float32, device=x.device) if need_params else None
+    db = torch.empty(d, dtype=torch.float32, device=x.device) if need_params else None
+    ws = torch.empty(max(1, N.lib().kinet_dropout_add_layernorm_backward_workspace(rows, d)) if need_params else 1,
+                     dtype=torch.float32, device=x.device)
+    N.call('kinet_dropout_add_layernorm_backward', N.ptr(dy2), N.ptr(x2), N.ptr(r2), N.ptr(f32(gamma)), N.ptr(dx),
+           N.ptr(dr), N.ptr(dg), N.ptr(db), rows, d, float(eps), float(p), N.ptr(seed), N.ptr(ws), N.stream(x.device),
+           work={'family': 'norm', 'bytes': 5 * x2.numel() * 4})
+    return (None if dx is None else dx.view(x.shape)), (None if dr is None else dr.view(x.shape)), dg, db
+
+
+def dropout_act(x, p, seed, relu):
+    """dropout_p(relu(x)) (relu optional), f32 (kinet_dropout_act)."""
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    N.call('kinet_dropout_act', N.ptr(x), N.ptr(y), x.numel(), int(relu), float(p), N.ptr(seed), N.stream(x.device),
+           work={'family': 'eltwise', 'bytes': 2 * x.numel() * 4})
+    return y
+
+
+def dropout_act_backward(dy, y, p, seed, relu):
+    dy = dy.contiguous()
+    dx = torch.empty_like(dy)
+    N.call('kinet_dropout_act_backward', N.ptr(dy), N.ptr(y), N.ptr(dx), dy.numel(), int(relu), float(p), N.ptr(seed),
+           N.stream(dy.device), work={'family': 'eltwise', 'bytes': 3 * dy.numel() * 4})
+    return dx
+
+
+def _packed_rows(t):
+    """(N, Lq, C) with unit column stride and packed batches -> its row stride (elements)."""
+    if t.stride(-1) != 1 or t.stride(0) != t.shape[1] * t.stride(1):
+        t = t.contiguous()
+    return t, t.stride(1)
+
+
+def msda_prep(offlog, refs, shapes, query_mask, heads, levels, points):
+    """Sampling locations (N, Lq, M, L, P, 2) and attention weights (N, Lq, M, L, P) from the
+    packed [sampling offsets | attention logits] projection (N, Lq, >= M*L*P*3)
+    (ms_deform_attn.py:64-82), f32 (kinet_msda_prep)."""
+    Nb, Lq = offlog.shape[:2]
+    ol, ld = _packed_rows(offlog)
+    rf = refs.contiguous()
+    loc = torch.empty((Nb, Lq, heads, levels, points, 2), dtype=torch.float32, device=ol.device)
+    attw = torch.empty((Nb, Lq, heads, levels, points), dtype=torch.float32, device=ol.device)
+    qm = query_mask.to(torch.uint8).contiguous() if query_mask is not None else None
+    N.call('kinet_msda_prep', N.ptr(ol), ld, N.ptr(rf), N.ptr(shapes.contiguous()), N.ptr(qm), N.ptr(loc),
+           N.ptr(attw), Nb * Lq, heads, levels, points, rf.shape[-1], N.stream(ol.device),
+           work={'family': 'msda_glue', 'bytes': 2 * (loc.numel() + attw.numel()) * 4})
+    return loc, attw
+
+
+def msda_prep_backward(grad_loc, grad_attw, attw, offlog, refs, shapes, heads, levels, points,
+                       need_offlog=True, need_refs=True):
+    """Gradients of msda_prep: w.r.t. the packed offlog (its layout, contiguous) and refs."""
+    Nb, Lq = offlog.shape[:2]
+    dev = offlog.device
+    gl, ga = grad_loc.contiguous(), grad_attw.contiguous()
+    ol = offlog.contiguous()      # the gradient takes offlog's (contiguous) layout
+    ld = ol.shape[-1]
+    rf = refs.contiguous()
+    dol = torch.empty(ol.shape, dtype=torch.float32, device=dev) if need_offlog else None
+    dref = torch.empty(rf.shape, dtype=torch.float32, device=dev) if need_refs else None
+    N.call('kinet_msda_prep_backward', N.ptr(gl), N.ptr(ga), N.ptr(attw), N.ptr(ol), ld, N.ptr(rf),
+           N.ptr(shapes.contiguous()), N.ptr(dol), N.ptr(dref), Nb * Lq, heads, levels, points, rf.shape[-1],
+           N.stream(dev), work={'family': 'msda_glue', 'bytes': 3 * (gl.numel() + ga.numel()) * 4})
+    return dol, dref
+
+
+def inverse_sigmoid(x, eps=1e-5):
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    N.call('kinet_inverse_sigmoid', N.ptr(x), N.ptr(y), x.numel(), float(eps), N.stream(x.device),
+           work={'family': 'eltwise', 'bytes': 2 * x.numel() * 4})
+    return y
+
+
+def inverse_sigmoid_backward(dy, x, eps=1e-5):
+    dy = dy.contiguous()
+    dx = torch.empty_like(dy)
+    N.call('kinet_inverse_sigmoid_backward', N.ptr(dy), N.ptr(x), N.ptr(dx), dy.numel(), float(eps),
+           N.stream(dy.device), work={'family': 'eltwise', 'bytes': 3 * dy.numel() * 4})
+    return dx
+
+
 def groupnorm_backward(dy, x, gamma, groups, eps, need_params=True):
     """x, dy (B, HW, C) NHWC."""
     B, HW, C = x.shape

@@ -96,8 +96,10 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, src):
-        src2 = A.linear_module(self.dropout2(self.activation(A.linear_module(src, self.linear1))), self.linear2)
-        return A.layer_norm(src + self.dropout3(src2), self.norm2)
+        # linear2(dropout2(relu(linear1(src)))), norm2(src + dropout3(src2)): the dropout / relu /
+        # residual / LayerNorm glue in one kernel each way (csrc/train_ops.hip)
+        src2 = A.linear_module(A.dropout_act(A.linear_module(src, self.linear1), self.dropout2), self.linear2)
+        return A.dropout_add_layer_norm(src, src2, self.norm2, self.dropout3)
 
     def forward(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None,
                 shapes_host=None):
@@ -105,7 +107,7 @@ class DeformableTransformerEncoderLayer(nn.Module):
             return self.forward_fast(src, pos, reference_points, spatial_shapes, padding_mask, query_order,
                                      shapes_host)
         src2 = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, spatial_shapes, padding_mask)
-        src = A.layer_norm(src + self.dropout1(src2), self.norm1)
+        src = A.dropout_add_layer_norm(src, src2, self.norm1, self.dropout1)
         return self.forward_ffn(src)
 
     def forward_fast(self, src, pos, reference_points, spatial_shapes, padding_mask=None, query_order=None,
@@ -182,8 +184,8 @@ class DeformableTransformerDecoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, tgt):
-        tgt2 = A.linear_module(self.dropout3(self.activation(A.linear_module(tgt, self.linear1))), self.linear2)
-        return A.layer_norm(tgt + self.dropout4(tgt2), self.norm3)
+        tgt2 = A.linear_module(A.dropout_act(A.linear_module(tgt, self.linear1), self.dropout3), self.linear2)
+        return A.dropout_add_layer_norm(tgt, tgt2, self.norm3, self.dropout4)
 
     def forward(self, tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask=None,
                 query_attn_mask=None, value=None, out=None):
@@ -193,10 +195,10 @@ class DeformableTransformerDecoderLayer(nn.Module):
         q = k = self.with_pos_embed(tgt, query_pos)
         # nn.MultiheadAttention on (L, B, E) transposes (:371) == the batch-first kinet path
         tgt2 = A.multihead_attention(self.self_attn, q, k, tgt, key_padding_mask=query_attn_mask)
-        tgt = A.layer_norm(tgt + self.dropout2(tgt2), self.norm2)
+        tgt = A.dropout_add_layer_norm(tgt, tgt2, self.norm2, self.dropout2)
         tgt2 = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_spatial_shapes,
                                src_padding_mask, query_attn_mask)
-        tgt = A.layer_norm(tgt + self.dropout1(tgt2), self.norm1)
+        tgt = A.dropout_add_layer_norm(tgt, tgt2, self.norm1, self.dropout1)
         return self.forward_ffn(tgt)
 
     def forward_fast(self, tgt, query_pos, reference_points, src, src_spatial_shapes, src_padding_mask=None,

@@ -78,6 +78,10 @@ def nested_tensor_from_tensor_list(tensor_list: List[Tensor]):
 
 
 def inverse_sigmoid(x, eps=1e-5):
+    if x.is_cuda and x.dtype == torch.float32:
+        # one HIP kernel each way (csrc/train_ops.hip) instead of 6 / 8 torch launches
+        from kinet_amd import autograd as A
+        return A.inverse_sigmoid(x, eps)
     x = x.clamp(min=0, max=1)
     x1 = x.clamp(min=eps)
     x2 = (1 - x).clamp(min=eps)

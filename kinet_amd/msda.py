@@ -154,28 +154,25 @@ class MSDeformAttn(nn.Module):
 
     def _forward_autograd(self, query, reference_points, input_flatten, input_spatial_shapes,
                           input_padding_mask, query_attn_mask):
-        # ms_deform_attn.py:64-88, step by step
-        import torch.nn.functional as F
+        # ms_deform_attn.py:64-88
         N, Len_q, _ = query.shape
         N, Len_in, _ = input_flatten.shape
         value = A.linear_module(input_flatten, self.value_proj)
         if input_padding_mask is not None:
             value = value.masked_fill(input_padding_mask[..., None], float(0))
         value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
-        sampling_offsets = A.linear_module(query, self.sampling_offsets).view(N, Len_q, self.n_heads, self.n_levels, self.n_points, 2)
-        attention_weights = A.linear_module(query, self.attention_weights).view(N, Len_q, self.n_heads, self.n_levels * self.n_points)
-        attention_weights = F.softmax(attention_weights, -1).view(N, Len_q, self.n_heads, self.n_levels, self.n_points)
-        if query_attn_mask is not None:
-            attention_weights = attention_weights.masked_fill(query_attn_mask[..., None, None, None], float(0))
-        if reference_points.shape[-1] == 2:
-            sampling_locations = reference_points[:, :, None, :, None, :] \
-                + sampling_offsets / input_spatial_shapes[None, None, None, :, None, :]
-        elif reference_points.shape[-1] == 4:
-            sampling_locations = reference_points[:, :, None, :, None, :2] \
-                + sampling_offsets / self.n_points * reference_points[:, :, None, :, None, 2:] * 0.5
-        else:
+        if reference_points.shape[-1] not in (2, 4):
             raise ValueError('Last dim of reference_points must be 2 or 4, but get {} instead.'
                              .format(reference_points.shape[-1]))
+        # :67-82 (softmax over L*P, query mask, locations from the reference points) in one
+        # kernel each way (kinet_msda_prep)
+        # ONE projection GEMM over [sampling_offsets ; attention_weights] (one input-gradient GEMM
+        # in the backward instead of two plus the add of their results)
+        so, aw = self.sampling_offsets, self.attention_weights
+        offlog = A.linear(query, torch.cat([so.weight, aw.weight], 0), torch.cat([so.bias, aw.bias], 0))
+        sampling_locations, attention_weights = A.msda_prep(
+            offlog, reference_points, input_spatial_shapes, query_attn_mask, self.n_heads, self.n_levels,
+            self.n_points)
         output = MSDeformAttnFunction.apply(value, input_spatial_shapes, sampling_locations,
                                             attention_weights, self.im2col_step)
         return A.linear_module(output, self.output_proj)

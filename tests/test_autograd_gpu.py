@@ -259,3 +259,120 @@ def test_colsum_vs_f64_and_deterministic(rows, cols):
     ref = a.sum(0)
     assert torch.equal(out, out2)
     assert ((out.double().cpu() - ref).abs() <= 1e-6 * a.abs().sum(0) + 1e-6).all()
+
+
+# ------------------------------------------------- training glue (csrc/train_ops.hip)
+def _leaf(t):
+    return t.detach().clone().requires_grad_()
+
+
+@pytest.mark.parametrize('rows,d,p', [(3001, 288, 0.1), (517, 256, 0.5), (64, 256, 0.0), (7, 90, 0.3)])
+def test_dropout_add_layernorm_fixed_mask(rows, d, p):
+    """LayerNorm(x + dropout(r)) (deformable_transformer.py:100,108,186,196,199) and its
+    gradients equal torch fp32 autograd of F.layer_norm(x + r * Z) with the SAME keep mask Z
+    (kinet_dropout_mask of the seed the kernels used)."""
+    from kinet_amd import autograd as A
+    from kinet_amd import kernels as K
+    ln = torch.nn.LayerNorm(d).cuda()
+    with torch.no_grad():
+        ln.weight.copy_(1 + 0.1 * _g(d, seed=40))
+        ln.bias.copy_(0.1 * _g(d, seed=41))
+    drop = torch.nn.Dropout(p).train()
+    x, r = _g(2, rows, d, seed=42).requires_grad_(), _g(2, rows, d, seed=43).requires_grad_()
+    go = _g(2, rows, d, seed=44)
+    torch.manual_seed(5)
+    y = A.dropout_add_layer_norm(x, r, ln, drop)
+    (y * go).sum().backward()
+    got = [y.detach(), x.grad, r.grad, ln.weight.grad.clone(), ln.bias.grad.clone()]
+    torch.manual_seed(5)
+    seed = A._seed(x.device, p)     # the same draw from the CUDA generator
+    keep = (K.dropout_mask(seed, x.numel(), p).view(x.shape).float() if p > 0 else torch.ones_like(x))
+    ln.zero_grad()
+    x2, r2 = _leaf(x), _leaf(r)
+    y2 = F.layer_norm(x2 + r2 * keep / (1 - p), (d,), ln.weight, ln.bias, ln.eps)
+    (y2 * go).sum().backward()
+    for n, a, b in zip(['y', 'dx', 'dr', 'dg', 'db'], got, [y2.detach(), x2.grad, r2.grad, ln.weight.grad,
+                                                           ln.bias.grad]):
+        _close(a, b, rel=2e-5 if n in ('y', 'dx', 'dr') else 1e-4, name=n)
+    if p > 0:
+        rate = keep.mean().item()
+        assert abs(rate - (1 - p)) < 0.02
+        drop.eval()
+        y0 = A.dropout_add_layer_norm(x.detach(), r.detach(), ln, drop)
+        _close(y0, F.layer_norm(x + r, (d,), ln.weight, ln.bias, ln.eps).detach(), rel=2e-5, name='eval')
+
+
+@pytest.mark.parametrize('n,p,relu', [(4096 * 1024 + 3, 0.1, True), (1000, 0.0, True), (999, 0.5, False)])
+def test_dropout_act_fixed_mask(n, p, relu):
+    from kinet_amd import autograd as A
+    from kinet_amd import kernels as K
+    drop = torch.nn.Dropout(p).train()
+    x = _g(n, seed=45).requires_grad_()
+    go = _g(n, seed=46)
+    torch.manual_seed(6)
+    y = A.dropout_act(x, drop, relu=relu)
+    (y * go).sum().backward()
+    torch.manual_seed(6)
+    seed = A._seed(x.device, p)
+    keep = K.dropout_mask(seed, n, p).float() if p > 0 else torch.ones_like(x)
+    x2 = _leaf(x)
+    y2 = (F.relu(x2) if relu else x2) * keep / (1 - p)
+    (y2 * go).sum().backward()
+    assert torch.equal(y.detach(), y2.detach())
+    assert torch.equal(x.grad, x2.grad)
+
+
+def _msda_prep_torch(off, logit, ref, shapes, qmask, M, L, P):
+    # ms_deform_attn.py:70-82 op for op
+    Nb, Lq = off.shape[:2]
+    so = off.view(Nb, Lq, M, L, P, 2)
+    aw = F.softmax(logit.view(Nb, Lq, M, L * P), -1).view(Nb, Lq, M, L, P)
+    if qmask is not None:
+        aw = aw.masked_fill(qmask[..., None, None, None], 0.0)
+    if ref.shape[-1] == 2:
+        loc = ref[:, :, None, :, None, :] + so / shapes[None, None, None, :, None, :]
+    else:
+        loc = ref[:, :, None, :, None, :2] + so / P * ref[:, :, None, :, None, 2:] * 0.5
+    return loc, aw
+
+
+@pytest.mark.parametrize('refd,mask,M,L,P', [(2, True, 8, 4, 4), (4, False, 8, 4, 4), (4, True, 8, 8, 4),
+                                             (2, False, 4, 3, 2)])
+def test_msda_prep_vs_torch(refd, mask, M, L, P):
+    """Sampling locations + softmaxed attention weights (ms_deform_attn.py:70-82) from the packed
+    [offsets | logits] projection, and their gradients w.r.t. it and the reference points, vs
+    torch fp32 autograd of the reference's op sequence."""
+    from kinet_amd import autograd as A
+    Nb, Lq = 2, 777
+    C2, C1 = M * L * P * 2, M * L * P
+    shapes = torch.tensor([[100 // (2 ** i), 150 // (2 ** i)] for i in range(L)], dtype=torch.int64, device='cuda')
+    offlog = torch.cat([_g(Nb, Lq, C2, seed=47) * 3, _g(Nb, Lq, C1, seed=48)], -1).requires_grad_()
+    ref = torch.rand(Nb, Lq, L, refd, device='cuda').requires_grad_()
+    qm = (torch.rand(Nb, Lq, device='cuda') < 0.2) if mask else None
+    gl = _g(Nb, Lq, M, L, P, 2, seed=49)
+    ga = _g(Nb, Lq, M, L, P, seed=50)
+    loc, aw = A.msda_prep(offlog, ref, shapes, qm, M, L, P)
+    ((loc * gl).sum() + (aw * ga).sum()).backward()
+    got = [loc.detach(), aw.detach(), offlog.grad, ref.grad]
+    ol2, ref2 = _leaf(offlog), _leaf(ref)
+    loc2, aw2 = _msda_prep_torch(ol2[..., :C2], ol2[..., C2:], ref2, shapes, qm, M, L, P)
+    ((loc2 * gl).sum() + (aw2 * ga).sum()).backward()
+    for n, a, b in zip(['loc', 'attw', 'doffl', 'dref'], got, [loc2.detach(), aw2.detach(), ol2.grad, ref2.grad]):
+        _close(a, b, rel=1e-5, name=n)
+
+
+def test_inverse_sigmoid_vs_torch():
+    """util/misc.py:609-613 forward and gradient (through the clamps' masks) incl. values at
+    and outside [0, 1] and inside the eps band."""
+    from kinet_amd import autograd as A
+    x = torch.cat([torch.rand(10000, device='cuda'), torch.tensor([0.0, 1.0, -0.5, 1.5, 1e-6, 1 - 1e-6, 0.5, 1e-5],
+                                                                    device='cuda')]).requires_grad_()
+    go = _g(x.numel(), seed=51)
+    y = A.inverse_sigmoid(x)
+    (y * go).sum().backward()
+    x2 = _leaf(x)
+    xc = x2.clamp(min=0, max=1)
+    y2 = torch.log(xc.clamp(min=1e-5) / (1 - xc).clamp(min=1e-5))
+    (y2 * go).sum().backward()
+    _close(y.detach(), y2.detach(), rel=1e-6, name='y')
+    _close(x.grad, x2.grad, rel=1e-6, name='dx')
