@@ -226,6 +226,29 @@ def mha_core(q, k, v, heads, scale, key_mask=None, dropout_p=0.0, seed=None):
     return _MHACore.apply(q, k, v, heads, scale, key_mask, float(dropout_p), seed)
 
 
+class _MHACoreQK(Function):
+    """mha_core with q and k the two halves of one packed projection qk (B, L, 2E): the
+    backward returns the packed gradient (one q|k input-gradient GEMM, no add of two)."""
+
+    @staticmethod
+    def forward(ctx, qk, v, heads, scale, key_mask, dropout_p, seed):
+        _f32(qk)
+        qk, v = qk.contiguous(), v.contiguous()
+        E = qk.shape[-1] // 2
+        o = K.mha_core(qk[..., :E], qk[..., E:], v, heads, scale, key_mask=key_mask, dropout_p=dropout_p, seed=seed)
+        ctx.save_for_backward(qk, v)
+        ctx.conf = (heads, scale, key_mask, dropout_p, seed)
+        return o
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, do):
+        qk, v = ctx.saved_tensors
+        heads, scale, key_mask, dropout_p, seed = ctx.conf
+        dqk, dv = K.mha_backward_qk(qk, v, do.float(), heads, scale, key_mask, dropout_p, seed)
+        return dqk, dv, None, None, None, None, None
+
+
 def multihead_attention(mod, query, key, value, key_padding_mask=None):
     """nn.MultiheadAttention(query, key, value, key_padding_mask)[0] for batch-first inputs
     (the decoder self-attention, deformable_transformer.py:371, transposes to (L, B, E) and
@@ -237,10 +260,18 @@ def multihead_attention(mod, query, key, value, key_padding_mask=None):
     statistics and by gradients under a fixed mask, tests/test_autograd_gpu.py)."""
     E = mod.embed_dim
     w, b = mod.in_proj_weight, mod.in_proj_bias
+    p = mod.dropout if mod.training else 0.0
+    if query is key:
+        # self-attention with q = k inputs (deformable_transformer.py:370): ONE GEMM for the
+        # packed q|k projection, its gradient packed the same way
+        qk = linear(query, w[:2 * E], b[:2 * E])
+        v = linear(value, w[2 * E:], b[2 * E:])
+        seed = K.dropout_seed(qk.device) if p > 0 else None
+        o = _MHACoreQK.apply(qk, v, mod.num_heads, mod.head_dim ** -0.5, key_padding_mask, float(p), seed)
+        return linear(o, mod.out_proj.weight, mod.out_proj.bias)
     q = linear(query, w[:E], b[:E])
     k = linear(key, w[E:2 * E], b[E:2 * E])
     v = linear(value, w[2 * E:], b[2 * E:])
-    p = mod.dropout if mod.training else 0.0
     o = mha_core(q, k, v, mod.num_heads, mod.head_dim ** -0.5, key_padding_mask, dropout_p=p)
     return linear(o, mod.out_proj.weight, mod.out_proj.bias)
 

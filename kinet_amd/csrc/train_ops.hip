@@ -158,14 +158,21 @@ __global__ __launch_bounds__(256) void drop_add_ln_bwd_kernel(const float* __res
     }
 }
 
-// fixed-order sum of the per-workgroup partials: out[c] = sum_b part[b][c]
+// fixed-order sum of the per-workgroup partials: out[c] = sum_b part[b][c]; one workgroup per
+// column, 256 threads striding over the partials, then a fixed tree (deterministic)
 __global__ __launch_bounds__(256) void partial_sum_kernel(const float* __restrict__ part, float* __restrict__ out,
                                                           int nb, int d) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= d) return;
+    __shared__ float red[256];
+    const int c = blockIdx.x;
     float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += part[(long)b * d + c];
-    out[c] = s;
+    for (int k = threadIdx.x; k < nb; k += 256) s += part[(long)k * d + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[c] = red[0];
 }
 
 // ------------------------------------------------------------------- dropout(relu(x))
@@ -280,6 +287,134 @@ __global__ __launch_bounds__(256) void msda_prep_kernel(const float* __restrict_
                 lo[k] = rx + o[k] / (float)P * rw * 0.5f;
                 lo[k + 1] = ry + o[k + 1] / (float)P * rh * 0.5f;
             }
+        }
+    }
+}
+
+// Vector form for P = 4 (every config): one thread per (query row, head, level) -- its 4 points'
+// 8 offsets / 4 logits are 2 + 1 16-byte loads, consecutive threads read consecutive 32 / 16
+// bytes (coalesced); the head's softmax max / sum over its L levels by shuffles inside groups of
+// L lanes (L a power of two <= 16).
+template <int L>
+__global__ __launch_bounds__(256) void msda_prep_v4_kernel(const float* __restrict__ offlog, int64_t ld,
+                                                           const float* __restrict__ ref,
+                                                           const int64_t* __restrict__ shapes,
+                                                           const uint8_t* __restrict__ qmask, float* __restrict__ loc,
+                                                           float* __restrict__ attw, int64_t nq, int M, int refd) {
+    constexpr int P = 4;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool on = t < nq * M * L;
+    const int64_t tt = on ? t : 0;
+    const int64_t hm = tt / L;              // (row, head)
+    const int l = (int)(tt - hm * L);
+    const int64_t nqi = hm / M;
+    const int m = (int)(hm - nqi * M);
+    const float* row = offlog + nqi * ld;
+    const float4 o0 = *reinterpret_cast<const float4*>(row + ((int64_t)m * L + l) * P * 2);
+    const float4 o1 = *reinterpret_cast<const float4*>(row + ((int64_t)m * L + l) * P * 2 + 4);
+    const float4 lg = *reinterpret_cast<const float4*>(row + (int64_t)M * L * P * 2 + ((int64_t)m * L + l) * P);
+    float mx = fmaxf(fmaxf(lg.x, lg.y), fmaxf(lg.z, lg.w));
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    const float e0 = expf(lg.x - mx), e1 = expf(lg.y - mx), e2 = expf(lg.z - mx), e3 = expf(lg.w - mx);
+    float s = ((e0 + e1) + e2) + e3;
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) s += __shfl_xor(s, o);
+    if (!on) return;
+    const bool masked = qmask && qmask[nqi];
+    *reinterpret_cast<float4*>(attw + tt * P) =
+        masked ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(e0 / s, e1 / s, e2 / s, e3 / s);
+    const float* rf = ref + (nqi * L + l) * refd;
+    float4 a, b;
+    if (refd == 2) {
+        const float rx = rf[0], ry = rf[1];
+        const float sh = (float)shapes[2 * l], sw = (float)shapes[2 * l + 1];
+        a = make_float4(rx + o0.x / sh, ry + o0.y / sw, rx + o0.z / sh, ry + o0.w / sw);
+        b = make_float4(rx + o1.x / sh, ry + o1.y / sw, rx + o1.z / sh, ry + o1.w / sw);
+    } else {
+        const float4 r = *reinterpret_cast<const float4*>(rf);
+        const float fp = (float)P;
+        a = make_float4(r.x + o0.x / fp * r.z * 0.5f, r.y + o0.y / fp * r.w * 0.5f, r.x + o0.z / fp * r.z * 0.5f,
+                        r.y + o0.w / fp * r.w * 0.5f);
+        b = make_float4(r.x + o1.x / fp * r.z * 0.5f, r.y + o1.y / fp * r.w * 0.5f, r.x + o1.z / fp * r.z * 0.5f,
+                        r.y + o1.w / fp * r.w * 0.5f);
+    }
+    *reinterpret_cast<float4*>(loc + tt * P * 2) = a;
+    *reinterpret_cast<float4*>(loc + tt * P * 2 + 4) = b;
+}
+
+// its backward, same thread map; d_ref[n, q, l] sums over the M heads of a row: lanes l, l + L,
+// ... of the row's M*L-lane group (M*L <= 64), reduced by shuffles
+template <int L>
+__global__ __launch_bounds__(256) void msda_prep_v4_bwd_kernel(const float* __restrict__ dloc,
+                                                               const float* __restrict__ dattw,
+                                                               const float* __restrict__ attw,
+                                                               const float* __restrict__ offlog, int64_t ld,
+                                                               const float* __restrict__ ref,
+                                                               const int64_t* __restrict__ shapes,
+                                                               float* __restrict__ doffl, float* __restrict__ dref,
+                                                               int64_t nq, int M, int refd) {
+    constexpr int P = 4;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool on = t < nq * M * L;
+    const int64_t tt = on ? t : 0;
+    const int64_t hm = tt / L;
+    const int l = (int)(tt - hm * L);
+    const int64_t nqi = hm / M;
+    const int m = (int)(hm - nqi * M);
+    const float4 g = *reinterpret_cast<const float4*>(dattw + tt * P);
+    const float4 av = *reinterpret_cast<const float4*>(attw + tt * P);
+    float sga = ((g.x * av.x + g.y * av.y) + g.z * av.z) + g.w * av.w;
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) sga += __shfl_xor(sga, o);
+    const float4 d0 = *reinterpret_cast<const float4*>(dloc + tt * P * 2);
+    const float4 d1 = *reinterpret_cast<const float4*>(dloc + tt * P * 2 + 4);
+    float* drow = doffl ? doffl + nqi * ld : nullptr;
+    const float* rf = ref + (nqi * L + l) * refd;
+    float sx = ((d0.x + d0.z) + d1.x) + d1.z, sy = ((d0.y + d0.w) + d1.y) + d1.w, sw = 0.f, sh = 0.f;
+    if (on && drow) {
+        *reinterpret_cast<float4*>(drow + (int64_t)M * L * P * 2 + ((int64_t)m * L + l) * P) =
+            make_float4(av.x * (g.x - sga), av.y * (g.y - sga), av.z * (g.z - sga), av.w * (g.w - sga));
+    }
+    if (refd == 2) {
+        if (on && drow) {
+            const float hh = (float)shapes[2 * l], ww = (float)shapes[2 * l + 1];
+            float* dof = drow + ((int64_t)m * L + l) * P * 2;
+            *reinterpret_cast<float4*>(dof) = make_float4(d0.x / hh, d0.y / ww, d0.z / hh, d0.w / ww);
+            *reinterpret_cast<float4*>(dof + 4) = make_float4(d1.x / hh, d1.y / ww, d1.z / hh, d1.w / ww);
+        }
+    } else {
+        const float4 r = *reinterpret_cast<const float4*>(rf);
+        const float fp = (float)P;
+        const float* orow = offlog + nqi * ld + ((int64_t)m * L + l) * P * 2;
+        const float4 o0 = *reinterpret_cast<const float4*>(orow);
+        const float4 o1 = *reinterpret_cast<const float4*>(orow + 4);
+        const float4 h0 = make_float4(d0.x * 0.5f, d0.y * 0.5f, d0.z * 0.5f, d0.w * 0.5f);
+        const float4 h1 = make_float4(d1.x * 0.5f, d1.y * 0.5f, d1.z * 0.5f, d1.w * 0.5f);
+        if (on && drow) {
+            float* dof = drow + ((int64_t)m * L + l) * P * 2;
+            *reinterpret_cast<float4*>(dof) =
+                make_float4(h0.x * r.z / fp, h0.y * r.w / fp, h0.z * r.z / fp, h0.w * r.w / fp);
+            *reinterpret_cast<float4*>(dof + 4) =
+                make_float4(h1.x * r.z / fp, h1.y * r.w / fp, h1.z * r.z / fp, h1.w * r.w / fp);
+        }
+        sw = ((h0.x * (o0.x / fp) + h0.z * (o0.z / fp)) + h1.x * (o1.x / fp)) + h1.z * (o1.z / fp);
+        sh = ((h0.y * (o0.y / fp) + h0.w * (o0.w / fp)) + h1.y * (o1.y / fp)) + h1.w * (o1.w / fp);
+    }
+    if (!dref) return;
+    for (int o = L; o < M * L; o <<= 1) {
+        sx += __shfl_xor(sx, o);
+        sy += __shfl_xor(sy, o);
+        sw += __shfl_xor(sw, o);
+        sh += __shfl_xor(sh, o);
+    }
+    if (on && m == 0) {
+        float* dr = dref + (nqi * L + l) * refd;
+        dr[0] = sx;
+        dr[1] = sy;
+        if (refd == 4) {
+            dr[2] = sw;
+            dr[3] = sh;
         }
     }
 }
@@ -416,7 +551,7 @@ extern "C" int kinet_dropout_add_layernorm(const float* x, const float* r, const
 }
 
 namespace {
-constexpr int kLnRowsPerWave = 16;
+constexpr int kLnRowsPerWave = 8;   // ~22 waves per CU at the encoder rows
 }
 
 extern "C" int64_t kinet_dropout_add_layernorm_backward_workspace(int rows, int d) {
@@ -449,8 +584,8 @@ extern "C" int kinet_dropout_add_layernorm_backward(const float* dy, const float
                        1.f / (1.f - dropout_p));
     KINET_LAUNCH_CHECK();
     if (dgamma) {
-        hipLaunchKernelGGL(partial_sum_kernel, dim3((d + 255) / 256), dim3(256), 0, s, pg, dgamma, blocks, d);
-        hipLaunchKernelGGL(partial_sum_kernel, dim3((d + 255) / 256), dim3(256), 0, s, pb, dbeta, blocks, d);
+        hipLaunchKernelGGL(partial_sum_kernel, dim3(d), dim3(256), 0, s, pg, dgamma, blocks, d);
+        hipLaunchKernelGGL(partial_sum_kernel, dim3(d), dim3(256), 0, s, pb, dbeta, blocks, d);
         KINET_LAUNCH_CHECK();
     }
     return KINET_OK;
@@ -484,6 +619,17 @@ extern "C" int kinet_dropout_act_backward(const float* dy, const float* y, float
     return KINET_OK;
 }
 
+namespace {
+// the vector kernels' conditions: P = 4, L a power of two <= 16, 16-byte aligned rows / outputs
+bool prep_v4_ok(const float* offlog, int64_t ld, const float* refs, const float* a, const float* b, int heads,
+                int levels, int points, int ref_dim) {
+    const bool lpow = levels == 1 || levels == 2 || levels == 4 || levels == 8 || levels == 16;
+    const bool al = ((((uintptr_t)offlog) | ((uintptr_t)a) | ((uintptr_t)b) |
+                      (ref_dim == 4 ? (uintptr_t)refs : 0)) & 15) == 0 && ld % 4 == 0;
+    return points == 4 && lpow && al && heads * levels <= 1024;
+}
+}  // namespace
+
 extern "C" int kinet_msda_prep(const float* offlog, int64_t ld, const float* refs, const int64_t* shapes,
                                const uint8_t* query_mask, float* loc, float* attw, int64_t nq, int heads, int levels,
                                int points, int ref_dim, kinet_stream_t stream) {
@@ -492,6 +638,19 @@ extern "C" int kinet_msda_prep(const float* offlog, int64_t ld, const float* ref
                     "msda_prep: bad arguments");
     if (nq == 0) return KINET_OK;
     const int64_t n = nq * heads;
+    if (prep_v4_ok(offlog, ld, refs, loc, attw, heads, levels, points, ref_dim)) {
+        const dim3 grid((unsigned)((n * levels + 255) / 256)), blk(256);
+        hipStream_t s = (hipStream_t)stream;
+        switch (levels) {
+            case 1: hipLaunchKernelGGL(msda_prep_v4_kernel<1>, grid, blk, 0, s, offlog, ld, refs, shapes, query_mask, loc, attw, nq, heads, ref_dim); break;
+            case 2: hipLaunchKernelGGL(msda_prep_v4_kernel<2>, grid, blk, 0, s, offlog, ld, refs, shapes, query_mask, loc, attw, nq, heads, ref_dim); break;
+            case 4: hipLaunchKernelGGL(msda_prep_v4_kernel<4>, grid, blk, 0, s, offlog, ld, refs, shapes, query_mask, loc, attw, nq, heads, ref_dim); break;
+            case 8: hipLaunchKernelGGL(msda_prep_v4_kernel<8>, grid, blk, 0, s, offlog, ld, refs, shapes, query_mask, loc, attw, nq, heads, ref_dim); break;
+            default: hipLaunchKernelGGL(msda_prep_v4_kernel<16>, grid, blk, 0, s, offlog, ld, refs, shapes, query_mask, loc, attw, nq, heads, ref_dim); break;
+        }
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
     hipLaunchKernelGGL(msda_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, offlog,
                        ld, refs, shapes, query_mask, loc, attw, nq, heads, levels, points, ref_dim);
     KINET_LAUNCH_CHECK();
@@ -509,8 +668,21 @@ extern "C" int kinet_msda_prep_backward(const float* grad_loc, const float* grad
                     "msda_prep_backward: heads must be a power of two <= 64 (got %d)", heads);
     if (nq == 0) return KINET_OK;
     const int64_t n = nq * heads;
-    const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
     hipStream_t s = (hipStream_t)stream;
+    if (prep_v4_ok(offlog, ld, refs, grad_loc, grad_attw, heads, levels, points, ref_dim) &&
+        (((uintptr_t)attw | (uintptr_t)grad_offlog) & 15) == 0 && heads * levels <= 64) {
+        const dim3 g4((unsigned)((n * levels + 255) / 256)), b4(256);
+        switch (levels) {
+            case 1: hipLaunchKernelGGL(msda_prep_v4_bwd_kernel<1>, g4, b4, 0, s, grad_loc, grad_attw, attw, offlog, ld, refs, shapes, grad_offlog, grad_refs, nq, heads, ref_dim); break;
+            case 2: hipLaunchKernelGGL(msda_prep_v4_bwd_kernel<2>, g4, b4, 0, s, grad_loc, grad_attw, attw, offlog, ld, refs, shapes, grad_offlog, grad_refs, nq, heads, ref_dim); break;
+            case 4: hipLaunchKernelGGL(msda_prep_v4_bwd_kernel<4>, g4, b4, 0, s, grad_loc, grad_attw, attw, offlog, ld, refs, shapes, grad_offlog, grad_refs, nq, heads, ref_dim); break;
+            case 8: hipLaunchKernelGGL(msda_prep_v4_bwd_kernel<8>, g4, b4, 0, s, grad_loc, grad_attw, attw, offlog, ld, refs, shapes, grad_offlog, grad_refs, nq, heads, ref_dim); break;
+            default: hipLaunchKernelGGL(msda_prep_v4_bwd_kernel<16>, g4, b4, 0, s, grad_loc, grad_attw, attw, offlog, ld, refs, shapes, grad_offlog, grad_refs, nq, heads, ref_dim); break;
+        }
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
+    const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
 #define KINET_PREP_BWD(MM)                                                                                  \
     hipLaunchKernelGGL(msda_prep_bwd_kernel<MM>, grid, blk, 0, s, grad_loc, grad_attw, attw, offlog, ld, refs, \
                        shapes, grad_offlog, grad_refs, nq, levels, points, ref_dim)

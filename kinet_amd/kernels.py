@@ -872,6 +872,28 @@ def groupnorm_backward(dy, x, gamma, groups, eps, need_params=True):
     return dx, dg, db
 
 
+def mha_backward_qk(qk, v, do, heads, scale, key_mask=None, dropout_p=0.0, seed=None):
+    """Backward of mha_core on the packed [q | k] projection qk (B, L, 2E) (self-attention,
+    q = k input): returns dqk (B, L, 2E, the same packing -- the input gradient of ONE q|k
+    projection GEMM) and dv."""
+    B, L, E2 = qk.shape
+    E = E2 // 2
+    qk, v, do = qk.contiguous(), v.contiguous(), do.contiguous()
+    for t in (qk, v, do):
+        if t.dtype != torch.float32:
+            raise RuntimeError('mha_backward_qk: f32 operands')
+    dqk = torch.empty((B, L, E2), dtype=torch.float32, device=qk.device)
+    dv = torch.empty((B, L, E), dtype=torch.float32, device=qk.device)
+    ws = torch.empty(max(1, N.lib().kinet_mha_backward_workspace(B, L, L, heads)), dtype=torch.float32,
+                     device=qk.device)
+    km = key_mask.to(torch.uint8).contiguous() if key_mask is not None else None
+    N.call('kinet_mha_backward', N.ptr(qk), E2, N.ptr(qk[..., E:]), E2, N.ptr(v), E, N.ptr(do), E, N.ptr(dqk),
+           N.ptr(dqk[..., E:]), N.ptr(dv), B, L, L, heads, E // heads, float(scale), N.ptr(km), N.ptr(ws),
+           float(dropout_p), N.ptr(seed) if dropout_p > 0 else None, N.stream(qk.device),
+           work={'family': 'attn', 'flops': 8.0 * B * heads * L * L * (E // heads)})
+    return dqk, dv
+
+
 def mha_backward(q, k, v, do, heads, scale, key_mask=None, dropout_p=0.0, seed=None):
     """Backward of mha_core (f32): returns dq, dk, dv with the layouts of q, k, v."""
     B, Lq, E = q.shape

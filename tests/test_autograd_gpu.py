@@ -296,7 +296,7 @@ def test_dropout_add_layernorm_fixed_mask(rows, d, p):
         _close(a, b, rel=2e-5 if n in ('y', 'dx', 'dr') else 1e-4, name=n)
     if p > 0:
         rate = keep.mean().item()
-        assert abs(rate - (1 - p)) < 0.02
+        assert abs(rate - (1 - p)) < 5 * (p * (1 - p) / keep.numel()) ** 0.5
         drop.eval()
         y0 = A.dropout_add_layer_norm(x.detach(), r.detach(), ln, drop)
         _close(y0, F.layer_norm(x + r, (d,), ln.weight, ln.bias, ln.eps).detach(), rel=2e-5, name='eval')
@@ -376,3 +376,28 @@ def test_inverse_sigmoid_vs_torch():
     (y2 * go).sum().backward()
     _close(y.detach(), y2.detach(), rel=1e-6, name='y')
     _close(x.grad, x2.grad, rel=1e-6, name='dx')
+
+
+def test_multihead_attention_packed_qk_matches_module():
+    """q = k (the decoder self-attention, deformable_transformer.py:370): the packed q|k
+    projection path (one GEMM each way) == nn.MultiheadAttention, incl. the in_proj gradient."""
+    from kinet_amd import autograd as A
+    E, H, B, L = 288, 8, 2, 300
+    mod = torch.nn.MultiheadAttention(E, H, dropout=0.0).cuda()
+    x = _g(B, L, E, seed=52).requires_grad_()
+    pos = _g(B, L, E, seed=53)
+    go = _g(B, L, E, seed=54)
+    km = torch.zeros(B, L, dtype=torch.bool, device='cuda')
+    km[0, -17:] = True
+    qk = x + pos
+    y = A.multihead_attention(mod, qk, qk, x, key_padding_mask=km)
+    (y * go).sum().backward()
+    got = [y.detach(), x.grad, mod.in_proj_weight.grad.clone(), mod.in_proj_bias.grad.clone()]
+    mod.zero_grad()
+    x2 = _leaf(x)
+    qk2 = (x2 + pos).transpose(0, 1)
+    y2 = mod(qk2, qk2, x2.transpose(0, 1), key_padding_mask=km)[0].transpose(0, 1)
+    (y2 * go).sum().backward()
+    for n, a, r in zip(['y', 'dx', 'dWin', 'dbin'], got, [y2.detach(), x2.grad, mod.in_proj_weight.grad,
+                                                         mod.in_proj_bias.grad]):
+        _close(a, r, rel=2e-4, name=n)
