@@ -41,8 +41,8 @@ struct FfnArgs {
     float eps;
     int ldx, ldy, M, F;
     int x_bytes, w_bytes, y_bytes;
-    int dbg;   // diagnostic timing knob (kinet_ffn_set_debug): 1 = no weight DMA after the
-               // prologue (results are garbage)
+    int dbg;   // diagnostic knobs (kinet_ffn_set_debug): 1 = no weight DMA after the prologue
+               // (timing only, results are garbage); 2 = the 4-wave x 32-row tile at D = 256
 };
 
 thread_local int ffn_debug = 0;   // test-only knob (kinet_ffn_set_debug), per calling thread
@@ -412,6 +412,11 @@ int launch_ffn(const FfnArgs& a, hipStream_t s) {
     if (a.M >= 16384) {
         const int nt = (a.M + 127) / 128;
         if constexpr (FfnGeo<D>::FR % 8 == 0) {
+            if (a.dbg & 2) {   // A/B knob: 4 waves x 32 rows (half the LDS weight reads per MFMA)
+                const int n2 = (a.M + 127) / 128;
+                hipLaunchKernelGGL((ffn_fused_kernel<T, D, 2, 4>), dim3(n2 < 256 ? n2 : 256), dim3(256), 0, s, a, n2);
+                return KINET_OK;
+            }
             // 8 waves x 16 rows: two waves per SIMD hide each other's LDS / VALU latency
             hipLaunchKernelGGL((ffn_fused_kernel<T, D, 1, 8>), dim3(nt < 256 ? nt : 256), dim3(512), 0, s, a, nt);
         } else {

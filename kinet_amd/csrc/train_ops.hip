@@ -27,13 +27,14 @@ __device__ __forceinline__ float wsum(float v) {
 }
 
 // ------------------------------------------------------------------ dropout + add + LN
-// y = LN(x + Z * r), Z in {0, 1/(1-p)} from (seed, row*d + c); one wave per row, d <= 1024
+// y = LN(x + Z * r), Z in {0, 1/(1-p)} from (seed, row*d + c); one wave per row, d <= 64 * MAXV
+// (MAXV = ceil(d / 64) instantiated for the model widths: no dead unrolled iterations)
+template <int MAXV>
 __global__ __launch_bounds__(256) void drop_add_ln_kernel(const float* __restrict__ x, const float* __restrict__ r,
                                                           const float* __restrict__ g, const float* __restrict__ b,
                                                           float* __restrict__ y, int rows, int d, float eps,
                                                           const int64_t* __restrict__ seedp, uint32_t thresh,
                                                           float keep_scale) {
-    constexpr int MAXV = 16;
     const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (row >= rows) return;
@@ -68,14 +69,14 @@ __global__ __launch_bounds__(256) void drop_add_ln_kernel(const float* __restric
 }
 
 // backward: z = x + Z*r recomputed; dz = LN backward; dx = dz, dr = Z * dz; per-workgroup
-// partial dgamma / dbeta (4 waves x rpw rows), summed in order by colsum_final_kernel
+// partial dgamma / dbeta (4 waves x rpw rows), summed in order by partial_sum_kernel
+template <int MAXV>
 __global__ __launch_bounds__(256) void drop_add_ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                               const float* __restrict__ r, const float* __restrict__ gamma,
                                                               float* __restrict__ dx, float* __restrict__ dr,
                                                               float* __restrict__ pg, float* __restrict__ pb, int rows,
                                                               int d, float eps, int rpw, const int64_t* __restrict__ seedp,
                                                               uint32_t thresh, float keep_scale) {
-    constexpr int MAXV = 16;
     extern __shared__ float red[];   // [4][2][d]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t seed = (uint64_t)*seedp;
@@ -544,8 +545,21 @@ extern "C" int kinet_dropout_add_layernorm(const float* x, const float* r, const
                     "dropout_add_layernorm: bad arguments (d must be in [1, 1024])");
     KINET_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f, "dropout_add_layernorm: p must be in [0, 1)");
     if (rows == 0) return KINET_OK;
-    hipLaunchKernelGGL(drop_add_ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, x, r, gamma, beta, y,
-                       rows, d, eps, dropout_seed, dropout_thresh(dropout_p), 1.f / (1.f - dropout_p));
+    const dim3 grid((rows + 3) / 4), blk(256);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t th = dropout_thresh(dropout_p);
+    const float ks = 1.f / (1.f - dropout_p);
+#define KINET_DLN(NV) hipLaunchKernelGGL(drop_add_ln_kernel<NV>, grid, blk, 0, s, x, r, gamma, beta, y, rows, d, eps, \
+                                         dropout_seed, th, ks)
+    switch ((d + 63) / 64) {
+        case 1: KINET_DLN(1); break;
+        case 2: KINET_DLN(2); break;
+        case 3: KINET_DLN(3); break;
+        case 4: KINET_DLN(4); break;
+        case 5: KINET_DLN(5); break;
+        default: KINET_DLN(16); break;
+    }
+#undef KINET_DLN
     KINET_LAUNCH_CHECK();
     return KINET_OK;
 }
@@ -579,9 +593,19 @@ extern "C" int kinet_dropout_add_layernorm_backward(const float* dy, const float
     const int blocks = (rows + 4 * kLnRowsPerWave - 1) / (4 * kLnRowsPerWave);
     float* pg = dgamma ? workspace : nullptr;
     float* pb = dgamma ? workspace + (int64_t)blocks * d : nullptr;
-    hipLaunchKernelGGL(drop_add_ln_bwd_kernel, dim3(blocks), dim3(256), 8 * d * sizeof(float), s, dy, x, r, gamma, dx, dr,
-                       pg, pb, rows, d, eps, kLnRowsPerWave, dropout_seed, dropout_thresh(dropout_p),
-                       1.f / (1.f - dropout_p));
+    const uint32_t th = dropout_thresh(dropout_p);
+    const float ks = 1.f / (1.f - dropout_p);
+#define KINET_DLNB(NV) hipLaunchKernelGGL(drop_add_ln_bwd_kernel<NV>, dim3(blocks), dim3(256), 8 * d * sizeof(float), s, \
+                                          dy, x, r, gamma, dx, dr, pg, pb, rows, d, eps, kLnRowsPerWave, dropout_seed, th, ks)
+    switch ((d + 63) / 64) {
+        case 1: KINET_DLNB(1); break;
+        case 2: KINET_DLNB(2); break;
+        case 3: KINET_DLNB(3); break;
+        case 4: KINET_DLNB(4); break;
+        case 5: KINET_DLNB(5); break;
+        default: KINET_DLNB(16); break;
+    }
+#undef KINET_DLNB
     KINET_LAUNCH_CHECK();
     if (dgamma) {
         hipLaunchKernelGGL(partial_sum_kernel, dim3(d), dim3(256), 0, s, pg, dgamma, blocks, d);

@@ -15,7 +15,23 @@ ap.add_argument('--iters', type=int, default=5)
 a = ap.parse_args()
 lin1, lin2, norm = torch.nn.Linear(256, 1024).cuda(), torch.nn.Linear(1024, 256).cuda(), torch.nn.LayerNorm(256).cuda()
 x = torch.randn(a.rows, 256, device='cuda', dtype=torch.bfloat16)
-for _ in range(a.iters):
-    K.ffn_fused(x, lin1, lin2, norm)
-torch.cuda.synchronize()
+from kinet_amd import _native as N  # noqa: E402
+ref = None
+for knob in (0, 2):
+    N.lib().kinet_ffn_set_debug(knob)
+    for _ in range(2):
+        y = K.ffn_fused(x, lin1, lin2, norm)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(a.iters):
+        y = K.ffn_fused(x, lin1, lin2, norm)
+    e.record()
+    torch.cuda.synchronize()
+    us = s.elapsed_time(e) * 1e3 / a.iters
+    tf = 4.0 * a.rows * 256 * 1024 / (us * 1e-6) / 1e12
+    same = 'ref' if ref is None else ('bit-identical' if torch.equal(ref, y) else
+                                     'max diff %.3g' % (ref.float() - y.float()).abs().max().item())
+    ref = y if ref is None else ref
+    print('ffn_probe knob %d: rows %d, %.1f us, %.0f TF/s, %s' % (knob, a.rows, us, tf, same))
+N.lib().kinet_ffn_set_debug(0)
 print('ffn_probe done')
