@@ -431,10 +431,30 @@ def nms(boxes, scores, iou_threshold):
 
 
 # --------------------------------------------------------------------------- attention
+_SEED_POOL = {}     # device index -> [seeds tensor, next index, generator state key after the draw]
+_SEED_BLOCK = 64
+
+
+def _gen_key(gen):
+    return (gen.initial_seed(), gen.get_offset())
+
+
 def dropout_seed(device):
     """A device int64 seed for the dropout kernels, drawn from torch's generator of `device`
-    (as F.dropout draws its Philox offset from it), without a host sync."""
-    return torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, device=device)
+    (as F.dropout draws its Philox offset from it), without a host sync.  Seeds are drawn 64 at
+    a time (one launch instead of one per dropout site); the block is redrawn whenever the
+    generator has moved since the draw (torch.manual_seed, other random ops), so a reseeded
+    run replays the same seeds."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    gen = torch.cuda.default_generators[idx]
+    ent = _SEED_POOL.get(idx)
+    if ent is None or ent[1] >= _SEED_BLOCK or ent[2] != _gen_key(gen):
+        seeds = torch.randint(0, 2 ** 62, (_SEED_BLOCK,), dtype=torch.int64, device=torch.device('cuda', idx))
+        ent = _SEED_POOL[idx] = [seeds, 0, _gen_key(gen)]
+    s = ent[0][ent[1]:ent[1] + 1]
+    ent[1] += 1
+    return s
 
 
 def dropout_mask(seed, n, p):
