@@ -72,6 +72,8 @@ def parse():
     ap.add_argument('--no-train', action='store_true', help='skip the config-4 training sub-benchmark')
     ap.add_argument('--train-steps', type=int, default=4)
     ap.add_argument('--cpu-seconds', type=float, default=20.0, help='bound on the CPU baseline sample')
+    ap.add_argument('--ffn-knob', type=int, default=0,
+                    help='fused-FFN tile A/B knob (kinet_ffn_set_debug: 2 = 4 waves x 32 rows at D = 256)')
     ap.add_argument('--gemm-flags', type=int, default=0,
                     help='diagnostic kernel-selection flags (kinet_gemm_set_flags, csrc/gemm.hip) for A/B runs')
     ap.add_argument('--cpu-stub', action='store_true',
@@ -385,6 +387,8 @@ def main():
     from kinet_amd.models import nested_tensor_from_tensor_list
     if a.gemm_flags:
         _native.lib().kinet_gemm_set_flags(a.gemm_flags)
+    if a.ffn_knob:
+        _native.lib().kinet_ffn_set_debug(a.ffn_knob)
     model = build(dev, dtype, wl)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     # one independent batch per in-flight slot (distinct requests, all resident in HBM)
