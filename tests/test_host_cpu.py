@@ -134,3 +134,25 @@ def test_track_reset_last_pos_compat_switch():
     assert len(t.last_pos_relative) == 0
     with pytest.raises(IndexError):
         t.repeat_last_pos()
+
+
+def test_train_glue_entry_points_validate_arguments():
+    """The training-glue C ABI (include/kinet_grad.h, csrc/train_ops.hip) rejects bad arguments
+    with KINET_ERR_ARG and a message before touching the device (no GPU needed)."""
+    from kinet_amd import _native
+    L = _native.lib()
+    fake = 4096   # never dereferenced: every call below fails validation first
+
+    def err(rc):
+        assert rc != 0
+        return L.kinet_last_error().decode()
+
+    assert 'p must be in [0, 1)' in err(L.kinet_dropout_add_layernorm(fake, fake, fake, fake, fake, 10, 288, 1e-5, 1.0,
+                                                                       fake, None))
+    assert 'd must be in [1, 1024]' in err(L.kinet_dropout_add_layernorm(fake, fake, fake, fake, fake, 10, 2048, 1e-5,
+                                                                         0.1, fake, None))
+    assert 'bad arguments' in err(L.kinet_dropout_act(fake, fake, 64, 1, 0.5, None, None))   # p > 0 needs a seed
+    assert 'bad arguments' in err(L.kinet_msda_prep(fake, 384, fake, fake, None, fake, fake, 10, 8, 4, 4, 3, None))
+    assert 'power of two' in err(L.kinet_msda_prep_backward(fake, fake, fake, fake, 288, fake, fake, fake, None, 10, 3,
+                                                            4, 4, 2, None))
+    assert 'bad arguments' in err(L.kinet_inverse_sigmoid(None, fake, 10, 1e-5, None))
