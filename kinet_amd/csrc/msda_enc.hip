@@ -207,14 +207,14 @@ __device__ __forceinline__ void setup_tile(const TileIn& in, const EncLevels& lv
         const float lh = h - hf, lw = w - wf, hh = 1.f - lh, hw = 1.f - lw;
         const bool h0 = hl >= 0, h1 = hl + 1 < H, c0 = wl >= 0, c1 = wl + 1 < W;
         const float av = valid ? a : 0.f;
-        if (in_lds) {
-            const bool staged = hl >= r0 && hl < r1;
-            const uint32_t lo = (uint32_t)(lbase + __mul24(hl, W) + wl) * 64u;
-            const uint32_t go = TAF | (uint32_t)(start + __mul24(hl + 1, W) + wl + 1) * 64u;
-            ro[p] = !valid ? 0u : (staged ? lo : go);
-        } else {
-            ro[p] = valid ? (uint32_t)(start + __mul24(hl, W) + wl) * 64u : TAF;
-        }
+        // branch-free (the level is lane-divergent: lane & 3): both address forms and a select
+        const int pix = __mul24(hl, W) + wl;
+        const uint32_t gofs = (uint32_t)(start + pix) * 64u;                  // head-map offset of (hl, wl)
+        const uint32_t lo = (uint32_t)(lbase + pix) * 64u;                    // LDS map offset
+        const uint32_t go = TAF | (gofs + (uint32_t)(W + 1) * 64u);           // far: corner (hl+1, wl+1)
+        const bool staged = hl >= r0 && hl < r1;
+        const uint32_t lds_o = staged ? lo : go;
+        ro[p] = valid ? (in_lds ? lds_o : gofs) : (in_lds ? 0u : TAF);
         rw01[p] = pack_f16x2((h0 && c0) ? hh * hw * av : 0.f, (h0 && c1) ? hh * lw * av : 0.f);
         rw23[p] = pack_f16x2((h1 && c0) ? lh * hw * av : 0.f, (h1 && c1) ? lh * lw * av : 0.f);
     }
