@@ -50,12 +50,21 @@ constexpr int EREC = EL * EP * 3;  // head-major offsets/logits per query and he
 constexpr int EHALO = 4;           // rows staged beyond a strip's query rows on each side
 constexpr uint32_t TAF = 0x80000000u;   // record flag: an LDS level's sample gathered from HBM
 
+// one level's constants as phase 1 reads them: 48 contiguous bytes = three ds_read_b128 from one
+// address per lane (its level), instead of eleven ds_read_b32 of the per-field arrays
+struct alignas(16) LevelRec {
+    int start, H, W, ok;
+    float Hf, Wf, rH, rW;
+    int r0, r1, lb, pad;   // staged rows [r0, r1] and the LDS map base (LDS levels)
+};
+
 struct EncLevels {
     int start[EL], H[EL], W[EL], ok[EL];
     float Hf[EL], Wf[EL], rH[EL], rW[EL];
     int ra[EL];   // LDS level: first staged row (-1 = the zero row above the image)
     int rn[EL];   // LDS level: staged rows
     int lb[EL];   // LDS level: map pixel of (row r, col c) = lb + r*W + c
+    LevelRec rec[EL];
 };
 
 // launch plan (host): levels [0, fl) are gathered from the head map, levels [fl, EL) staged
@@ -183,12 +192,13 @@ __device__ __forceinline__ void setup_tile(const TileIn& in, const EncLevels& lv
     es = group_reduce<4, false>(es);
     const float ra = (in.qm || !ok) ? 0.f : __builtin_amdgcn_rcpf(es);
     const bool in_lds = l >= FL;
-    const int H = lv.H[l], W = lv.W[l];
-    const int start = lv.start[l];
-    const int r0 = lv.ra[l], r1 = lv.ra[l] + lv.rn[l] - 1;   // staged rows [r0, r1]
-    const int lbase = lv.lb[l];
-    const float Hf = lv.Hf[l], Wf = lv.Wf[l], rH = lv.rH[l], rW = lv.rW[l];
-    const bool lok = lv.ok[l] != 0;
+    const LevelRec L = lv.rec[l];
+    const int H = L.H, W = L.W;
+    const int start = L.start;
+    const int r0 = L.r0, r1 = L.r1;   // staged rows [r0, r1]
+    const int lbase = L.lb;
+    const float Hf = L.Hf, Wf = L.Wf, rH = L.rH, rW = L.rW;
+    const bool lok = L.ok != 0;
 #pragma unroll
     for (int p = 0; p < EP; ++p) {
         float x, y;
@@ -345,13 +355,29 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
         ra_[l] = __builtin_amdgcn_readfirstlane(r);
         lb_[l] = a.base[l] + 1 - ra_[l] * W;
     }
-    if (lane < EL && lane >= FL) {   // identical values from every wave
-        int r = ra_[FL], bb = lb_[FL];
+    if (lane < EL) {   // identical values from every wave
+        int r = lv.ra[lane], bb = lv.lb[lane];
 #pragma unroll
-        for (int l = FL + 1; l < EL; ++l)
+        for (int l = FL; l < EL; ++l)
             if (lane == l) { r = ra_[l]; bb = lb_[l]; }
-        lv.ra[lane] = r;
-        lv.lb[lane] = bb;
+        if (lane >= FL) {
+            lv.ra[lane] = r;
+            lv.lb[lane] = bb;
+        }
+        LevelRec rc;
+        rc.start = lv.start[lane];
+        rc.H = lv.H[lane];
+        rc.W = lv.W[lane];
+        rc.ok = lv.ok[lane];
+        rc.Hf = lv.Hf[lane];
+        rc.Wf = lv.Wf[lane];
+        rc.rH = lv.rH[lane];
+        rc.rW = lv.rW[lane];
+        rc.r0 = r;
+        rc.r1 = r + lv.rn[lane] - 1;
+        rc.lb = bb;
+        rc.pad = 0;
+        lv.rec[lane] = rc;
     }
 
     // the first tile's phase-1 inputs ahead of the DMA (so waiting for them does not wait for it)
