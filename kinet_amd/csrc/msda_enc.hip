@@ -124,14 +124,31 @@ __device__ __forceinline__ void level_sum16(uint32_t (&h)[4], const u32x4v (&v)[
         }
 }
 
-// the level's f16 pair sums into the f32 accumulators (v_fma_mix with an f16 1.0)
+// the level's f16 pair sums into the f32 accumulators (v_fma_mix with an f16 1.0); the tile's
+// first level widens them instead (exact, and no zeroed accumulators to add to)
+template <bool FIRST = false>
 __device__ __forceinline__ void flush16(f32x2 (&acc)[4], const uint32_t (&h)[4]) {
     constexpr uint32_t one = 0x3c003c00u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        acc[j][0] = fma_mix16_lo_lo(acc[j][0], h[j], one);
-        acc[j][1] = fma_mix16_hi_lo(acc[j][1], h[j], one);
+        if constexpr (FIRST) {
+            acc[j][0] = (float)__builtin_bit_cast(f16_t, (uint16_t)(h[j] & 0xffffu));
+            acc[j][1] = (float)__builtin_bit_cast(f16_t, (uint16_t)(h[j] >> 16));
+        } else {
+            acc[j][0] = fma_mix16_lo_lo(acc[j][0], h[j], one);
+            acc[j][1] = fma_mix16_hi_lo(acc[j][1], h[j], one);
+        }
     }
+}
+
+// max / sum over the 4 lanes of a quad, every lane active (phase 1): plain DPP moves, no
+// zeroed "old" operand
+template <bool MAX>
+__device__ __forceinline__ float quad_reduce(float x) {
+    const float a = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xf, 0xf, false));
+    x = MAX ? fmaxf(x, a) : x + a;
+    const float c = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xf, 0xf, false));
+    return MAX ? fmaxf(x, c) : x + c;
 }
 
 // phase-1 inputs of one tile (this lane: query lane >> 2, level lane & 3)
@@ -182,14 +199,14 @@ __device__ __forceinline__ void setup_tile(const TileIn& in, const EncLevels& lv
         lg[p] = (float)__builtin_bit_cast(f16_t, (uint16_t)((p & 1) ? (gw >> 16) : (gw & 0xffffu)));
     }
     float mx = fmaxf(fmaxf(lg[0], lg[1]), fmaxf(lg[2], lg[3]));
-    mx = group_reduce<4, true>(mx);
+    mx = quad_reduce<true>(mx);
     float e[EP], es = 0.f;
 #pragma unroll
     for (int p = 0; p < EP; ++p) {
         e[p] = __expf(lg[p] - mx);
         es += e[p];
     }
-    es = group_reduce<4, false>(es);
+    es = quad_reduce<false>(es);
     const float ra = (in.qm || !ok) ? 0.f : __builtin_amdgcn_rcpf(es);
     const bool in_lds = l >= FL;
     const LevelRec L = lv.rec[l];
@@ -297,6 +314,8 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
     constexpr int NGL = FL;            // levels gathered through the texture path
     constexpr int NLL = EL - FL;       // levels read from LDS
     constexpr int NST = NGL > 1 ? NGL : 1;
+    // the tile's first flush: LDS level FL when slot 0 holds one (below), else gathered level 0
+    constexpr bool LDS_FIRST = NLL / NST > 0;
     const int Lq = a.Lq, ntile = (Lq + EQT - 1) / EQT;
     const int t0 = (int)((long)strip * ntile / a.nstrip), t1 = (int)((long)(strip + 1) * ntile / a.nstrip);
     const int qi = lane >> 2, l1 = lane & 3;
@@ -433,7 +452,7 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
                 w23[p] = quad_bcast<LV>(rec_w23[p]);
             }
             level_sum16(h, g, w01, w23);
-            flush16(acc, h);
+            flush16<!LDS_FIRST && LV == 0>(acc, h);
         };
         // LDS level LV, one point at a time (8 VGPRs of corner data beside the gathers).  A
         // footprint outside the staged rows (record flag TAF) is gathered from the head map:
@@ -485,7 +504,7 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
-            flush16(acc, h);
+            flush16<LDS_FIRST && LV == FL>(acc, h);
         };
         auto lds_level_any = [&](auto lvc) {
             constexpr int LV = decltype(lvc)::value;
