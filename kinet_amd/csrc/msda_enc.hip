@@ -459,10 +459,11 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
         // when any lane of the wave has one at this level, the level runs the FAR variant
         // (per corner pair, the far lanes' corners loaded in place and waited for inside the
         // branch, so the common path keeps its gathers in flight and holds no extra registers)
-        auto lds_level = [&](auto lvc, auto farc) {
+        // the level's f16 sums into h; the flush into acc follows the FAR / common branch merge,
+        // so only h (not the 8 accumulators) crosses it
+        auto lds_level = [&](auto lvc, auto farc, uint32_t (&h)[4]) {
             constexpr int LV = decltype(lvc)::value;
             constexpr bool FAR = decltype(farc)::value;
-            uint32_t h[4];
 #pragma unroll
             for (int p = 0; p < EP; ++p) {
                 const uint32_t o = quad_bcast<LV>(rec_o[p]);
@@ -504,15 +505,16 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
-            flush16<LDS_FIRST && LV == FL>(acc, h);
         };
         auto lds_level_any = [&](auto lvc) {
             constexpr int LV = decltype(lvc)::value;
             const uint32_t f = quad_bcast<LV>(rec_o[0] | rec_o[1] | rec_o[2] | rec_o[3]);
+            uint32_t h[4];
             if (__builtin_amdgcn_ballot_w64((f & TAF) != 0u) != 0)
-                lds_level(lvc, std::true_type{});
+                lds_level(lvc, std::true_type{}, h);
             else
-                lds_level(lvc, std::false_type{});
+                lds_level(lvc, std::false_type{}, h);
+            flush16<LDS_FIRST && LV == FL>(acc, h);
         };
         // LDS levels interleaved between the gathered levels' consumes (slot s: LDS levels
         // FL + [s*NLL/NST, (s+1)*NLL/NST))
