@@ -41,8 +41,6 @@ MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'f16': 2500.0, 'f32': 157.3}   # dense
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command
 # (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950 per MI355X_MICROARCH.md "HBM")
 PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
-MSDA_ENC_KERNEL = 'msda_enc_kernel'         # config-2 encoder calls (msda_enc.hip: coarse levels in LDS)
-MSDA_KERNEL = 'msda_fused_fast_kernel'      # decoder calls
 
 WORKLOADS = {
     'config2': dict(cfgs=('train_deformable',), over={}, h=800, w=1333, batch=16, streams=3, dtype='bf16',
@@ -70,12 +68,16 @@ def parse():
     ap.add_argument('--dtype', default=None, choices=['bf16', 'f16', 'f32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-train', action='store_true', help='skip the config-4 training sub-benchmark')
-    ap.add_argument('--train-steps', type=int, default=4)
+    ap.add_argument('--no-config5', action='store_true', help='skip the config-5 sub-benchmark of the default line')
+    ap.add_argument('--config5-steps', type=int, default=8)
+    ap.add_argument('--train-steps', type=int, default=10)
     ap.add_argument('--cpu-seconds', type=float, default=20.0, help='bound on the CPU baseline sample')
     ap.add_argument('--ffn-knob', type=int, default=0,
                     help='fused-FFN tile A/B knob (kinet_ffn_set_debug: 2 = 4 waves x 32 rows at D = 256)')
     ap.add_argument('--gemm-flags', type=int, default=0,
-                    help='diagnostic kernel-selection flags (kinet_gemm_set_flags, csrc/gemm.hip) for A/B runs')
+                    help='diagnostic kernel-selection flags (kinet_gemm_set_flags, csrc/gemm.hip) for A/B runs; '
+                         'per calling thread, so the train leg\'s autograd backward (torch\'s engine thread) '
+                         'keeps the default kernels')
     ap.add_argument('--cpu-stub', action='store_true',
                     help='tests only: run the launch/timing skeleton with a tiny CPU model over gloo')
     a = ap.parse_args()
@@ -239,7 +241,7 @@ def summarize_trace(trace, steps_traced=1):
         a['bytes'] += work.get('bytes', 0.0)
         a['launches'] += 1
         if f == 'msda':
-            msda.append((work.get('Lq'), work.get('S'), ms, work['bytes']))
+            msda.append((work.get('Lq'), work.get('S'), ms, work['bytes'], work.get('kernel', '?')))
     for a in fam.values():
         for k in ('ms', 'flops', 'bytes', 'launches'):
             a[k] /= steps_traced
@@ -299,13 +301,20 @@ def decoder_touched_bytes(model, samples, extra):
     return statistics.mean(res) if res else None
 
 
-def pmc_traffic(kernel):
-    """(bytes per launch, provenance) of `kernel` from the committed PMC summary, or (None, None)."""
+def kernel_names(launches):
+    """The kernel instantiation(s) the traced MSDA launches ran (reported by kinet_amd.kernels
+    from the launcher's own dispatch), as rocprofv3 names them."""
+    return ' | '.join(sorted({m[4] for m in launches}))
+
+
+def pmc_traffic(key):
+    """(bytes per launch, provenance) of kernel `key` = '<workload>:<kernel name>' from the
+    committed PMC summary (tools/pmc_traffic.py), or (None, None)."""
     try:
         with open(PMC_TRAFFIC) as f:
             d = json.load(f)
-        k = d['kernels'][kernel]
-        return k['hbm_bytes_per_launch'], d.get('source')
+        k = d['kernels'][key]
+        return k['hbm_bytes_per_launch'], d['sources'].get(key.split(':')[0])
     except (OSError, KeyError, ValueError):
         return None, None
 
@@ -374,45 +383,57 @@ def cpu_baseline(seconds):
             'config5_msda_encoder_ms_per_call': min(t5) * 1e3}
 
 
-def main():
-    a = parse()
-    if a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
-        sys.exit(launch_ranks(a.gpus))
-    world, rank, dev = setup_dist(a)
-    if a.cpu_stub:
-        return stub_main(a, world, rank, dev)
-    dtype = {'bf16': torch.bfloat16, 'f16': torch.float16, 'f32': torch.float32}[a.dtype]
-    wl = WORKLOADS[a.workload]
+def train_leg(a, dev, world):
+    """The config-4 training sub-benchmark.  Under `--gpus N` it runs on the bench's own RCCL
+    group; at N = 1 (no launcher, no group) the step still runs under DistributedDataParallel
+    over a 1-rank "nccl" group created here, in this process -- RCCL initialisation, the DDP
+    reducer's bucketed all-reduce and find_unused_parameters (train.py:88-91) then run on the
+    hardware exactly as at N > 1; the group is destroyed after the leg."""
+    from kinet_amd.train import benchmark_train
+    own = False
+    if world == 1 and not dist.is_initialized():
+        dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{_free_port()}', rank=0, world_size=1,
+                                device_id=dev)
+        own = True
+    try:
+        return benchmark_train(steps=a.train_steps, warmup=2, device=dev)
+    finally:
+        if own:
+            dist.destroy_process_group()
+
+
+def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype_name, steps, warmup):
+    """Time `steps` forwards of workload `name` (WORKLOADS) after `warmup`, then trace 3 more on
+    one stream.  Returns (elapsed seconds (max over ranks), trace families, MSDA launches,
+    GEMM/conv roofline split, decoder touched bytes)."""
     from kinet_amd import _native
     from kinet_amd.models import nested_tensor_from_tensor_list
-    if a.gemm_flags:
-        _native.lib().kinet_gemm_set_flags(a.gemm_flags)
-    if a.ffn_knob:
-        _native.lib().kinet_ffn_set_debug(a.ffn_knob)
+    wl = WORKLOADS[name]
+    dtype = {'bf16': torch.bfloat16, 'f16': torch.float16, 'f32': torch.float32}[dtype_name]
     model = build(dev, dtype, wl)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     # one independent batch per in-flight slot (distinct requests, all resident in HBM)
-    nst = max(1, a.streams)
-    batches = [nested_tensor_from_tensor_list([torch.randn(3, a.height, a.width, generator=g, device=dev)
-                                               for _ in range(a.batch)]) for _ in range(nst)]
+    nst = max(1, streams)
+    batches = [nested_tensor_from_tensor_list([torch.randn(3, height, width, generator=g, device=dev)
+                                               for _ in range(batch)]) for _ in range(nst)]
     extra = [() for _ in range(nst)]
     if wl['K']:
         # tracking step inputs per slot: K track queries per frame (hs embeddings + boxes of
         # the previous frame's detections) and the previous frame's backbone features
         K_, d = wl['K'], model.hidden_dim
         for i in range(nst):
-            prev = nested_tensor_from_tensor_list([torch.randn(3, a.height, a.width, generator=g, device=dev)
-                                                   for _ in range(a.batch)])
+            prev = nested_tensor_from_tensor_list([torch.randn(3, height, width, generator=g, device=dev)
+                                                   for _ in range(batch)])
             with torch.no_grad():
                 feats = model(prev)[2]
-            boxes = torch.cat([torch.rand(a.batch, K_, 2, generator=g, device=dev) * 0.8 + 0.1,
-                               torch.rand(a.batch, K_, 2, generator=g, device=dev) * 0.2 + 0.02], -1)
-            hs = torch.randn(a.batch, K_, d, generator=g, device=dev)
-            targets = [{'track_query_hs_embeds': hs[b], 'track_query_boxes': boxes[b]} for b in range(a.batch)]
+            boxes = torch.cat([torch.rand(batch, K_, 2, generator=g, device=dev) * 0.8 + 0.1,
+                               torch.rand(batch, K_, 2, generator=g, device=dev) * 0.2 + 0.02], -1)
+            hs = torch.randn(batch, K_, d, generator=g, device=dev)
+            targets = [{'track_query_hs_embeds': hs[b], 'track_query_boxes': boxes[b]} for b in range(batch)]
             extra[i] = (targets, feats)
         torch.cuda.synchronize()
-    streams = [torch.cuda.Stream(device=dev) for _ in range(nst)]
-    for st in streams:   # the input batches were written on the default stream
+    strs = [torch.cuda.Stream(device=dev) for _ in range(nst)]
+    for st in strs:   # the input batches were written on the default stream
         st.wait_stream(torch.cuda.current_stream(dev))
     samples = batches[0]
 
@@ -422,10 +443,10 @@ def main():
                 return model(batches[0], *extra[0])
             # step i runs batch i % nst on its own stream: the decoder / small-kernel phases of
             # one batch overlap the backbone of the next (no host syncs anywhere in a forward)
-            with torch.cuda.stream(streams[i % nst]):
+            with torch.cuda.stream(strs[i % nst]):
                 return model(batches[i % nst], *extra[i % nst])
 
-    for i in range(max(1, a.warmup)):
+    for i in range(max(1, warmup)):
         out = step(i)
         if i == 0:
             # step 0 fills the weight-pack / geometry caches on its stream; the other
@@ -436,7 +457,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
+    for i in range(steps):
         out = step(i)
     torch.cuda.synchronize()
     if world > 1:
@@ -447,6 +468,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     assert torch.isfinite(out[0]['pred_boxes']).all()
+    del out
 
     # roofline pass: HIP events around every launch of 3 more steps, one stream (the traced
     # kernel durations must not overlap)
@@ -457,16 +479,93 @@ def main():
     trace = _native.trace_end()
     torch.cuda.synchronize()
     fam, msda = summarize_trace(trace, 3)
-    dec_touched = decoder_touched_bytes(model, samples, extra[0]) if a.workload == 'config2' else None
-    split = roofline_split(trace, 3, MFMA_PEAK_TFLOPS[a.dtype])
+    dec_touched = decoder_touched_bytes(model, samples, extra[0]) if name == 'config2' else None
+    split = roofline_split(trace, 3, MFMA_PEAK_TFLOPS[dtype_name])
+    del model, batches, extra, trace
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return elapsed, fam, msda, split, dec_touched
+
+
+def msda_roofline(name, msda, dec_touched):
+    """The MSDA HBM roofline of one workload's traced launches: the encoder kernel (the
+    headline: the kernel with the most MSDA device time) with the decoder kernel and all
+    launches beside it; PMC traffic from the committed per-kernel summary."""
+    if not msda:
+        return None
+    enc = [m for m in msda if m[0] == m[1]]
+    dec = [m for m in msda if m[0] != m[1]]
+
+    def roof(launches, kname, pmc_name):
+        t_ms = sum(m[2] for m in launches)
+        t_b = sum(m[3] for m in launches)
+        ach_ = t_b / (t_ms * 1e-3) / 1e9
+        traffic, src = pmc_traffic(pmc_name) if pmc_name else (None, None)
+        return {'bound': 'hbm', 'kernel': kname, 'achieved': ach_, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': ach_ / HBM_PEAK_GBS, 'traffic': traffic, 'traffic_source': src,
+                'algorithmic_bytes_per_launch': t_b / len(launches),
+                'avg_launch_ms': t_ms / len(launches), 'launches_per_step': len(launches) / 3}
+    # PMC summaries are keyed '<workload>:<kernel base name>' (tools/pmc_traffic.py)
+    def base(launches):
+        return name + ':' + launches[0][4].split('<')[0]
+    if enc:
+        r = roof(enc, '%s (encoder launches, Lq = S = %d)' % (kernel_names(enc), enc[0][0]), base(enc))
+        if dec:
+            r['decoder_kernel'] = roof(dec, '%s (decoder launches)' % kernel_names(dec), base(dec))
+            # the decoder held against the bytes it must touch (value rows its corners reach),
+            # not the whole value map
+            if dec_touched:
+                dk = r['decoder_kernel']
+                ach = dec_touched / (dk['avg_launch_ms'] * 1e-3) / 1e9
+                dk.update(algorithmic_bytes_per_launch=dec_touched, achieved=ach, frac=ach / HBM_PEAK_GBS,
+                          bytes_basis='value rows touched by the bilinear corners (counted from one forward) + '
+                                      'offsets/logits + references + output')
+        r['all_msda_launches'] = roof(msda, 'encoder + decoder launches', None)
+    else:
+        r = roof(msda, '%s (all launches)' % kernel_names(msda), None)
+    r['encoder_launch'] = {'ms': statistics.mean(m[2] for m in enc) if enc else None,
+                           'bytes': enc[0][3] if enc else None}
+    r['decoder_launch'] = {'ms': statistics.mean(m[2] for m in dec) if dec else None,
+                           'bytes': dec[0][3] if dec else None}
+    return r
+
+
+def main():
+    a = parse()
+    if a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(a.gpus))
+    world, rank, dev = setup_dist(a)
+    if a.cpu_stub:
+        return stub_main(a, world, rank, dev)
+    wl = WORKLOADS[a.workload]
+    from kinet_amd import _native
+    if a.gemm_flags:
+        _native.lib().kinet_gemm_set_flags(a.gemm_flags)
+    if a.ffn_knob:
+        _native.lib().kinet_ffn_set_debug(a.ffn_knob)
+    elapsed, fam, msda, split, dec_touched = run_workload(a, a.workload, dev, world, rank, a.batch, a.streams,
+                                                          a.height, a.width, a.dtype, a.steps, a.warmup)
+
+    # config 5 (BASELINE configs[4], the HBM-stress MSDA case) beside the headline: a short
+    # timed run of its own workload with its own MSDA roofline (not part of `value`)
+    c5 = None
+    if a.workload == 'config2' and not a.no_config5:
+        w5 = WORKLOADS['config5']
+        el5, fam5, msda5, split5, _ = run_workload(a, 'config5', dev, world, rank, w5['batch'], w5['streams'],
+                                                   w5['h'], w5['w'], w5['dtype'], a.config5_steps, 2)
+        c5 = {'workload': w5['desc'], 'value': w5['batch'] * a.config5_steps * world / el5, 'unit': 'frames/s',
+              'frames_per_gpu_per_step': w5['batch'], 'in_flight_batches': w5['streams'],
+              'frame': [3, w5['h'], w5['w']], 'dtype': w5['dtype'], 'steps': a.config5_steps, 'warmup': 2,
+              'ms_per_step': el5 / a.config5_steps * 1e3,
+              'roofline': msda_roofline('config5', msda5, None),
+              'roofline_gemm_conv_split': split5,
+              'device_ms_per_step_by_family': {k: round(v['ms'], 4) for k, v in fam5.items()}}
 
     # config-4 training step (BASELINE configs[3]): every rank runs the DDP step, gradients
     # all-reduced over RCCL -- the path whose 1 -> 8 GPU scaling north_star targets
     train = None
     if not a.no_train and a.workload == 'config2':
-        from kinet_amd.train import benchmark_train
-        del out
-        train = benchmark_train(steps=a.train_steps, warmup=2, device=dev)
+        train = train_leg(a, dev, world)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a.cpu_seconds)
@@ -475,54 +574,16 @@ def main():
         frames_total = a.batch * a.steps * world
         value = frames_total / elapsed
         dt_name = a.dtype
+        mfma_ms = sum(fam[f]['ms'] for f in ('gemm', 'conv') if f in fam)
+        mfma_flops = sum(fam[f]['flops'] for f in ('gemm', 'conv') if f in fam)
+        # Headline roofline: the MSDA sampling kernel with the most device time in the
+        # rocprofv3 summary (profiles/): config 2's encoder kernel (6 launches per frame
+        # batch), the 6 decoder launches beside it
+        msda_roof = msda_roofline(a.workload, msda, dec_touched)
         enc = [m for m in msda if m[0] == m[1]]
         dec = [m for m in msda if m[0] != m[1]]
         msda_enc_ms = statistics.mean(m[2] for m in enc) if enc else None
         msda_dec_ms = statistics.mean(m[2] for m in dec) if dec else None
-        mfma_ms = sum(fam[f]['ms'] for f in ('gemm', 'conv') if f in fam)
-        mfma_flops = sum(fam[f]['flops'] for f in ('gemm', 'conv') if f in fam)
-        # Headline roofline: the MSDA sampling kernel with the most device time in the
-        # rocprofv3 summary (profiles/).  config 2: msda_enc_kernel, which runs the 6
-        # encoder calls per frame batch (avg_launch_ms = the rocprof average of that kernel
-        # name); the 6 decoder calls run msda_fused_fast_kernel, reported beside it.
-        # config 5 (D=36): the generic msda_fused_kernel -- the encoder launches, the decoder
-        # launches beside them.
-        msda_roof = None
-        if msda:
-            def roof(launches, kname, pmc_name):
-                t_ms = sum(m[2] for m in launches)
-                t_b = sum(m[3] for m in launches)
-                ach_ = t_b / (t_ms * 1e-3) / 1e9
-                traffic, src = pmc_traffic(pmc_name) if (pmc_name and a.workload == 'config2') else (None, None)
-                return {'bound': 'hbm', 'kernel': kname, 'achieved': ach_, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                        'frac': ach_ / HBM_PEAK_GBS, 'traffic': traffic, 'traffic_source': src,
-                        'algorithmic_bytes_per_launch': t_b / len(launches),
-                        'avg_launch_ms': t_ms / len(launches), 'launches_per_step': len(launches) / 3}
-            if a.workload == 'config2' and enc and dec:
-                msda_roof = roof(enc, MSDA_ENC_KERNEL + '<bf16_t, 2, 2, false> (encoder launches, Lq = S = %d)'
-                                 % enc[0][0], MSDA_ENC_KERNEL)
-                msda_roof['decoder_kernel'] = roof(dec, MSDA_KERNEL + '<f16_t, bf16_t, f16_t, 4, 4> (decoder launches)',
-                                                   MSDA_KERNEL)
-                # the decoder held against the bytes it must touch (value rows its corners
-                # reach), not the whole value map
-                if dec_touched:
-                    dk = msda_roof['decoder_kernel']
-                    t_ms = dk['avg_launch_ms']
-                    ach = dec_touched / (t_ms * 1e-3) / 1e9
-                    dk.update(algorithmic_bytes_per_launch=dec_touched, achieved=ach, frac=ach / HBM_PEAK_GBS,
-                              bytes_basis='value rows touched by the bilinear corners (counted from one forward) + '
-                                          'offsets/logits + references + output')
-                msda_roof['all_msda_launches'] = roof(msda, 'encoder + decoder launches', None)
-            elif enc:
-                msda_roof = roof(enc, 'msda_fused_kernel<f16_t, 4> (D=36, encoder launches, Lq = S = %d)' % enc[0][0],
-                                 None)
-                if dec:
-                    msda_roof['decoder_kernel'] = roof(dec, 'msda_fused_kernel<f16_t, 4> (D=36, decoder launches)', None)
-                msda_roof['all_msda_launches'] = roof(msda, 'encoder + decoder launches', None)
-            else:
-                msda_roof = roof(msda, 'msda_fused_kernel (all launches)', None)
-            msda_roof['encoder_launch'] = {'ms': msda_enc_ms, 'bytes': enc[0][3] if enc else None}
-            msda_roof['decoder_launch'] = {'ms': msda_dec_ms, 'bytes': dec[0][3] if dec else None}
         mfma_ach = mfma_flops / (mfma_ms * 1e-3) / 1e12 if mfma_ms else 0.0
         mfma_roof = {'bound': 'mfma', 'kernel': 'all GEMM + conv launches (gemm_kernel, gemm_rw_kernel)',
                      'achieved': mfma_ach, 'peak': MFMA_PEAK_TFLOPS[dt_name], 'unit': 'TFLOP/s',
@@ -538,7 +599,7 @@ def main():
             'vs_baseline': None, 'dtype': dt_name,
             'data': 'synthetic N(0,1) 3x%dx%d frames, random-init weights (reference init)' % (a.height, a.width),
             'config': {'workload': wl['desc'],
-                       'frames_per_gpu_per_step': a.batch, 'in_flight_batches': nst,
+                       'frames_per_gpu_per_step': a.batch, 'in_flight_batches': max(1, a.streams),
                        'frame': [3, a.height, a.width],
                        'parallelism': f'replicas x{world}'},
             'roofline': roofline,
@@ -546,6 +607,7 @@ def main():
             'roofline_gemm_conv_split': split,
             'msda_ms_per_call': {'encoder': msda_enc_ms, 'decoder': msda_dec_ms},
             'device_ms_per_step_by_family': {k: round(v['ms'], 4) for k, v in fam.items()},
+            'config5': c5,
             'cpu_baseline': cpu,
             'train': train,
         }

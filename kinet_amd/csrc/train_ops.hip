@@ -178,7 +178,9 @@ __global__ __launch_bounds__(256) void partial_sum_kernel(const float* __restric
 
 // ------------------------------------------------------------------- dropout(relu(x))
 // 4 elements per thread; y = Z * act(x); backward dx = Z * dy * act'(x) (act' from y > 0 for
-// relu: a kept positive input is the only way y > 0)
+// relu: a kept positive input is the only way y > 0).  NaN inputs stay NaN as in the torch ops
+// replaced: relu(NaN) = NaN, and dropout multiplies by the 0/scale mask (NaN * 0 = NaN)
+__device__ __forceinline__ float relu_nan(float t) { return (t > 0.f || t != t) ? t : 0.f; }
 __global__ __launch_bounds__(256) void drop_act_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
                                                        const int64_t* __restrict__ seedp, uint32_t thresh,
                                                        float keep_scale, int relu) {
@@ -190,15 +192,15 @@ __global__ __launch_bounds__(256) void drop_act_kernel(const float* __restrict__
             float t[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                if (relu) t[j] = fmaxf(t[j], 0.f);
-                if (seedp) t[j] = dropout_keep(seed, (uint64_t)(i + j), thresh) ? t[j] * keep_scale : 0.f;
+                if (relu) t[j] = relu_nan(t[j]);
+                if (seedp) t[j] *= dropout_keep(seed, (uint64_t)(i + j), thresh) ? keep_scale : 0.f;
             }
             *reinterpret_cast<float4*>(y + i) = make_float4(t[0], t[1], t[2], t[3]);
         } else {
             for (int64_t k = i; k < n; ++k) {
                 float t = x[k];
-                if (relu) t = fmaxf(t, 0.f);
-                if (seedp) t = dropout_keep(seed, (uint64_t)k, thresh) ? t * keep_scale : 0.f;
+                if (relu) t = relu_nan(t);
+                if (seedp) t *= dropout_keep(seed, (uint64_t)k, thresh) ? keep_scale : 0.f;
                 y[k] = t;
             }
         }
@@ -231,8 +233,8 @@ __global__ __launch_bounds__(256) void drop_act_bwd_kernel(const float* __restri
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             float v = g[j];
-            if (relu && !(o[j] > 0.f)) v = 0.f;
-            if (seedp) v = dropout_keep(seed, (uint64_t)(i + j), thresh) ? v * keep_scale : 0.f;
+            if (relu && o[j] <= 0.f) v = 0.f;   // torch threshold_backward: a NaN output passes the gradient
+            if (seedp) v *= dropout_keep(seed, (uint64_t)(i + j), thresh) ? keep_scale : 0.f;
             t[j] = v;
         }
         if (m == 4) {
@@ -507,9 +509,11 @@ __global__ __launch_bounds__(256) void inv_sigmoid_kernel(const float* __restric
                                                           float eps) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float xc = fminf(fmaxf(x[i], 0.f), 1.f);
+    const float xv = x[i];
+    const float xc = fminf(fmaxf(xv, 0.f), 1.f);
     const float x1 = fmaxf(xc, eps), x2 = fmaxf(1.f - xc, eps);
-    y[i] = logf(x1 / x2);
+    // torch's clamp chain propagates a NaN input (fminf / fmaxf would drop it)
+    y[i] = xv != xv ? xv : logf(x1 / x2);
 }
 
 __global__ __launch_bounds__(256) void inv_sigmoid_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,

@@ -15,9 +15,11 @@ so a new mask is re-embedded on every replay instead of reusing the warm-up's va
 Weights: the recording holds the device pointers of the weight casts / packings that
 ``kernels.cached`` built during warm-up.  ``GraphedCall`` keeps every cache entry alive for
 its lifetime (so the allocator cannot hand those buffers to anything else) and, given the
-module's parameters and buffers, snapshots their (_version, data_ptr) at record time: a
-replay after ``load_state_dict``, an optimizer step or ``set_compute_dtype`` raises instead
-of silently running the stale weights.
+module's parameters and buffers, snapshots their (_version, data_ptr, dtype) at record time,
+and, given a ``state_fn``, the module-level state the recorded kernels were chosen by (the
+compute dtype of ``set_compute_dtype``, the ``training`` flag that selects the op-for-op path):
+a replay after ``load_state_dict``, an optimizer step, ``set_compute_dtype`` or ``train()`` /
+``eval()`` raises instead of silently running the stale weights or the wrong kernels.
 """
 import torch
 
@@ -27,9 +29,10 @@ __all__ = ['GraphedCall']
 
 
 class GraphedCall:
-    def __init__(self, fn, tensors, warmup=3, params=()):
+    def __init__(self, fn, tensors, warmup=3, params=(), state_fn=None):
         self.fn = fn
         self.params = [p for p in params if p is not None]
+        self.state_fn = state_fn
         self.static = [t.detach().clone() for t in tensors]
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -44,16 +47,22 @@ class GraphedCall:
             self.out = fn(*self.static)
         self._keep = kernels.cache_values()      # the buffers the graph reads stay allocated
         self._pver = self._param_versions()
+        self._state = state_fn() if state_fn is not None else None
 
     def _param_versions(self):
         return [(p._version, p.data_ptr(), p.dtype) for p in self.params]
 
     def check_weights(self):
-        """RuntimeError when a parameter or buffer changed since the recording."""
+        """RuntimeError when a parameter or buffer, or the recorded module state, changed since
+        the recording."""
         if self._param_versions() != self._pver:
             raise RuntimeError('GraphedCall: the module parameters changed after the recording '
-                               '(load_state_dict / optimizer step / set_compute_dtype); the graph would replay '
+                               '(load_state_dict / optimizer step); the graph would replay '
                                'the old weights -- record a new GraphedCall')
+        if self.state_fn is not None and self.state_fn() != self._state:
+            raise RuntimeError(f'GraphedCall: the module state changed after the recording '
+                               f'({self._state} -> {self.state_fn()}: set_compute_dtype / train() / eval()); '
+                               f'the graph would replay the kernels of the old state -- record a new GraphedCall')
 
     def __call__(self, *tensors):
         if len(tensors) != len(self.static):

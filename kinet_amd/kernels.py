@@ -535,6 +535,8 @@ def encoder_tile_order(shapes, device, qt=16):
 
 _host_shapes = {}
 _enc_plans = {}
+# template-argument spelling of the element types in rocprofv3 kernel names
+_KT = {torch.bfloat16: 'kinet::bf16_t', torch.float16: 'kinet::f16_t', torch.float32: 'float', torch.float64: 'double'}
 
 
 def msda_encoder_plan(shapes, batch, n_heads, Lq):
@@ -608,10 +610,14 @@ def msda_encoder(value, shapes, offlog_hm, reference_points, n_heads, query_attn
         raise RuntimeError('msda_encoder: query_tile_order must be int32 with ceil(Lq/16) entries')
     offlog_hm = offlog_hm.contiguous()
     nsamp = B * Lq * M_ * 16
+    plan = msda_encoder_plan(key, B, M_, Lq)
+    # the instantiation kinet_msda_encoder_forward launches (as rocprofv3 names it)
+    kname = 'msda_enc_kernel<%s, %d, %d, %s>' % (_KT[od], plan[0] if plan else -1, ref.shape[-1],
+                                                   'true' if qm is not None else 'false')
     N.call('kinet_msda_encoder_forward', N.ptr(value), value.stride(1), value.stride(0), N.ptr(hs), N.ptr(offlog_hm),
            N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), B, S, M_, D, 4, Lq, 4, N.dtype_code(od),
            N.ptr(query_tile_order), N.stream(value.device),
-           work={'family': 'msda', 'flops': 10.0 * nsamp * D, 'Lq': Lq, 'S': S,
+           work={'family': 'msda', 'flops': 10.0 * nsamp * D, 'Lq': Lq, 'S': S, 'kernel': kname,
                  # compulsory bytes: value once, f16 offsets + logits, refs, output once
                  'bytes': B * S * M_ * D * 2 + offlog_hm.numel() * 2 + ref.numel() * 4 + out.numel() * out.element_size()})
     return out
@@ -669,6 +675,13 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
         raise RuntimeError('msda_fused: the offsets/logits projection must be f32 or f16')
     ev = value.element_size()
     nsamp = B * Lq * n_heads * n_levels * n_points
+    # the instantiation launch_fused (csrc/msda.hip) picks, as rocprofv3 names it
+    if (ev == 2 and D == 32 and n_points == 4 and n_levels in (4, 8) and vss % 8 == 0 and vsb % 8 == 0
+            and vsm % 8 == 0):
+        kname = 'msda_fused_fast_kernel<%s, %s, %s, %s>' % (_KT[value.dtype], _KT[od], _KT[offlog.dtype],
+                                                             '4, 4, 2, 2' if n_levels == 4 else '8, 4')
+    else:
+        kname = 'msda_fused_kernel<%s, *>' % _KT[value.dtype]
     N.call('kinet_msda_fused_forward', N.ptr(value), vsb, vss, vsm, N.ptr(spatial_shapes), N.ptr(offlog),
            offlog.shape[-1], N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(out), N.ptr(loc), N.ptr(attw), B, S,
            n_heads, D, n_levels, Lq, n_points, N.dtype_code(value.dtype), N.dtype_code(od), N.dtype_code(offlog.dtype),
@@ -678,7 +691,7 @@ def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_level
                  'bytes': B * S * d * ev + nsamp * 3 * offlog.element_size() + ref.numel() * 4
                  + B * Lq * d * out.element_size()
                  + (nsamp * 3 * 4 if want_loc_attw else 0),
-                 'Lq': Lq, 'S': S, 'shape': (B, Lq, S)})
+                 'Lq': Lq, 'S': S, 'shape': (B, Lq, S), 'kernel': kname})
     if want_loc_attw:
         return out, loc, attw
     return out

@@ -504,7 +504,8 @@ def graph_kinet_forward(model, samples, targets=None, warmup=3):
         return model(smp, tgs)[0]
 
     gc = GraphedCall(fn, flat(samples, targets), warmup,
-                     params=list(model.parameters()) + list(model.buffers()))
+                     params=list(model.parameters()) + list(model.buffers()),
+                     state_fn=lambda: (model._compute_dtype, model.training))
 
     def call(smp, tgs=None):
         if (tgs is not None and len(tgs[0]['track_query_hs_embeds_det']) > 0) != has_trk:

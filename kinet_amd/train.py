@@ -117,7 +117,7 @@ def setup_ddp(model, device):
                                                      find_unused_parameters=True)
 
 
-def benchmark_train(steps=5, warmup=2, batch=2, height=800, width=1333, prev_dtype=torch.bfloat16, device=None,
+def benchmark_train(steps=10, warmup=2, batch=2, height=800, width=1333, prev_dtype=torch.bfloat16, device=None,
                     dropout=None, matmul_precision='high'):
     """Config-4 training throughput (BASELINE.json configs[3], cfgs/train_mot17.yaml: `mot17
     deformable multi_frame tracking`, d=288, 500 queries, two-pass track-query training,
@@ -138,6 +138,7 @@ def benchmark_train(steps=5, warmup=2, batch=2, height=800, width=1333, prev_dty
 
 
 def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dropout, matmul_precision):
+    import statistics
     import time
     from kinet_amd.models import build_model
     from kinet_amd.models.config import load_args
@@ -165,17 +166,24 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # every step timed on its own (device synchronised on both sides; the step already syncs
+    # with the host 3 times for the matcher / sampler copies): the median over >= 10 steps is
+    # the reported rate, so one slow step (allocator growth, a host hiccup) cannot move it
+    per_step = []
     t0 = time.perf_counter()
     for _ in range(steps):
+        ts = time.perf_counter()
         loss = step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        per_step.append(time.perf_counter() - ts)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        t = torch.tensor([el] + per_step, device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = t.item()
+        el, per_step = t[0].item(), t[1:].tolist()
+    med = statistics.median(per_step)
     # host glue of the step (matcher + track-query sampler), measured over
     # two extra steps: wall seconds in those functions, the part of it spent waiting for the
     # device in the one-sync-per-call host copies, and the number of such syncs
@@ -192,10 +200,19 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
     # reference runs it: prepare_track_queries -> reference_path), not the bf16 HIP path
     prev_desc = ('float32 (op-for-op path: train-mode dropout %g, as the reference)' % args.dropout
                  if _has_dropout(model) else str(prev_dtype).replace('torch.', ''))
+    fpstep = batch * world
+    pg = 'none (single process)'
+    if world >= 1 and dist.is_available() and dist.is_initialized():
+        pg = f'ddp{world}: DistributedDataParallel over a {world}-rank {dist.get_backend()} process group'
+        if dist.get_backend() == 'nccl':
+            pg += ' (RCCL all-reduce)'
     return {'metric': 'train frames/sec (config 4: mot17 deformable multi_frame tracking, 3x%dx%d pairs)'
                       % (height, width),
-            'value': frames / el, 'unit': 'frames/s', 'images_per_s': 2 * frames / el, 'n_gpus': world,
-            'steps': steps, 'warmup': warmup, 's_per_step': el / steps, 'loss': float(loss), 'scaling': 'weak',
+            'value': fpstep / med, 'unit': 'frames/s', 'images_per_s': 2 * fpstep / med, 'n_gpus': world,
+            'steps': steps, 'warmup': warmup, 's_per_step': med, 's_per_step_median': med,
+            's_per_step_mean': el / steps, 's_per_step_min': min(per_step), 's_per_step_max': max(per_step),
+            'frames_per_s_mean': frames / el, 'rate_basis': 'median of the per-step times (max over ranks)',
+            'loss': float(loss), 'scaling': 'weak',
             'host_glue': {'ms_per_step': glue['glue_s'] / 2 * 1e3,
                           'device_wait_ms_per_step': glue['sync_wait_s'] / 2 * 1e3,
                           'host_only_ms_per_step': (glue['glue_s'] - glue['sync_wait_s']) / 2 * 1e3,
@@ -208,4 +225,4 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
                        'prev_frame_dtype': prev_desc,
                        'grad_frame_dtype': 'f32', 'f32_matmul_precision': matmul_precision +
                        (' (bf16x3 MFMA products)' if matmul_precision != 'highest' else ' (exact f32 MFMA)'),
-                       'parallelism': f'ddp{world} (RCCL all-reduce)'}}
+                       'parallelism': pg}}

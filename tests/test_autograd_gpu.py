@@ -322,6 +322,48 @@ def test_dropout_act_fixed_mask(n, p, relu):
     assert torch.equal(x.grad, x2.grad)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize('relu', [False, True])
+def test_dropout_act_nan_like_torch(relu):
+    """NaN inputs stay NaN in the output (relu(NaN) = NaN; a dropped NaN is NaN * 0 = NaN) and
+    the gradients follow torch's (relu threshold_backward on the output, the mask product)."""
+    from kinet_amd import autograd as A
+    from kinet_amd import kernels as K
+    n, p = 4099, 0.25
+    drop = torch.nn.Dropout(p).train()
+    x0 = _g(n, seed=47)
+    x0[::97] = float('nan')
+    x = x0.clone().requires_grad_()
+    go = _g(n, seed=48)
+    go[5::211] = float('nan')
+    torch.manual_seed(7)
+    y = A.dropout_act(x, drop, relu=relu)
+    (y * go).sum().backward()
+    torch.manual_seed(7)
+    keep = K.dropout_mask(A._seed(x.device, p), n, p).float()
+    x2 = _leaf(x)
+    y2 = (F.relu(x2) if relu else x2) * keep / (1 - p)
+    (y2 * go).sum().backward()
+    assert y.isnan().sum() >= x0.isnan().sum()
+    torch.testing.assert_close(y.detach(), y2.detach(), rtol=0, atol=0, equal_nan=True)
+    torch.testing.assert_close(x.grad, x2.grad, rtol=0, atol=0, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_inverse_sigmoid_nan_like_torch():
+    """A NaN input gives a NaN output and a zero gradient, as the torch clamp chain does."""
+    from kinet_amd import autograd as A
+    x = torch.tensor([0.3, float('nan'), 0.7, float('nan')], device='cuda').requires_grad_()
+    y = A.inverse_sigmoid(x)
+    y.sum().backward()
+    x2 = _leaf(x)
+    xc = x2.clamp(min=0, max=1)
+    y2 = torch.log(xc.clamp(min=1e-5) / (1 - xc).clamp(min=1e-5))
+    y2.sum().backward()
+    torch.testing.assert_close(y.detach(), y2.detach(), equal_nan=True)
+    torch.testing.assert_close(x.grad, x2.grad, equal_nan=True)
+
+
 def _msda_prep_torch(off, logit, ref, shapes, qmask, M, L, P):
     # ms_deform_attn.py:70-82 op for op
     Nb, Lq = off.shape[:2]

@@ -177,3 +177,13 @@ def test_kinet_graph_replay_equals_eager(golden_dir, dtype):
         got = call(s0, tg(1.0))
         torch.cuda.synchronize()
         assert torch.equal(got['pred_boxes'], ref['pred_boxes'])
+        # a new compute dtype / train mode picks other kernels: the replay refuses
+        model.set_compute_dtype(torch.float16 if dtype != torch.float16 else torch.float32)
+        with pytest.raises(RuntimeError, match='module state changed'):
+            call(s0, tg(1.0))
+        model.set_compute_dtype(dtype)
+        call(s0, tg(1.0))
+        model.train()
+        with pytest.raises(RuntimeError, match='module state changed'):
+            call(s0, tg(1.0))
+        model.eval()

@@ -6,8 +6,13 @@ both in KiB; on gfx950 FETCH_SIZE counts exactly half of the bytes of wide strea
 (MI355X_MICROARCH.md "HBM"), WRITE_SIZE is exact for 16-byte stores.  Kernel names are
 shortened to the template name (e.g. msda_fused_fast_kernel) when that is unambiguous.
 
-usage: python tools/pmc_traffic.py FETCH.json WRITE.json OUT.json "provenance text"
+usage: python tools/pmc_traffic.py FETCH.json WRITE.json OUT.json "provenance text" [WORKLOAD]
+
+The per-kernel entries are keyed '<WORKLOAD>:<short name>' (default workload config2) and
+MERGED into OUT when it exists, so one file holds the passes of several workloads
+(bench.py looks its MSDA kernels up there).
 """
+import os
 import json
 import re
 import sys
@@ -38,7 +43,17 @@ def short(name):
 
 def main():
     fetch, write = (json.load(open(p))['counters'] for p in sys.argv[1:3])
-    out = {'source': sys.argv[4] if len(sys.argv) > 4 else '', 'kernels': {}, 'by_full_name': {}}
+    wl = sys.argv[5] if len(sys.argv) > 5 else 'config2'
+    out = {'sources': {}, 'kernels': {}, 'by_full_name': {}}
+    if os.path.exists(sys.argv[3]):
+        old = json.load(open(sys.argv[3]))
+        if 'sources' in old:
+            out = old
+    out['sources'][wl] = sys.argv[4] if len(sys.argv) > 4 else ''
+    for k in [k for k in out['kernels'] if k.startswith(wl + ':')] + \
+             [k for k in out['by_full_name'] if k.startswith(wl + ':')]:
+        out['kernels'].pop(k, None)
+        out['by_full_name'].pop(k, None)
     agg = {}
     for name, c in fetch.items():
         w = write.get(name, {})
@@ -47,15 +62,15 @@ def main():
             continue
         f_b = 2.0 * c.get('FETCH_SIZE', 0.0) * 1024 / nf
         w_b = w.get('WRITE_SIZE', 0.0) * 1024 / nw
-        out['by_full_name'][name] = {'fetch_bytes_x2': f_b, 'write_bytes': w_b, 'hbm_bytes_per_launch': f_b + w_b,
-                                     'dispatches': nf}
+        out['by_full_name'][wl + ':' + name] = {'fetch_bytes_x2': f_b, 'write_bytes': w_b,
+                                                'hbm_bytes_per_launch': f_b + w_b, 'dispatches': nf}
         a = agg.setdefault(short(name), [0.0, 0])
         a[0] += (f_b + w_b) * nf
         a[1] += nf
     for k, (b, n) in agg.items():
-        out['kernels'][k] = {'hbm_bytes_per_launch': b / n, 'dispatches': n}
+        out['kernels'][wl + ':' + k] = {'hbm_bytes_per_launch': b / n, 'dispatches': n}
     json.dump(out, open(sys.argv[3], 'w'), indent=1, sort_keys=True)
-    print(f'[pmc_traffic] {len(out["kernels"])} kernels -> {sys.argv[3]}')
+    print(f'[pmc_traffic] {len(agg)} kernels of {wl} -> {sys.argv[3]}')
 
 
 if __name__ == '__main__':
