@@ -136,6 +136,41 @@ int kinet_msda_encoder_forward(const void* value, int64_t value_sb, int64_t valu
 int kinet_msda_encoder_plan(const int64_t* spatial_shapes_host, int batch, int num_heads, int num_query,
                             int32_t* plan_out);
 
+/* The encoder call's sampling_offsets | attention_weights projection (ms_deform_attn.py:68-69,
+ * one GEMM over query [+ query_add] rows, K = 256) with the rest of the MSDA preparation in its
+ * epilogue -- softmax over the head's L*P logits (:70-71), query_attn_mask (:73-74), sampling
+ * locations from the reference points (:76-82) and the bilinear setup of
+ * ms_deform_im2col_cuda.cuh:227-233 -- written as head-major SAMPLING RECORDS
+ * (num_heads, M, 96 bytes) for kinet_msda_encoder_forward_records:
+ *   bytes [16 l, 16 l + 16): level l's 4 locations, u32 fixed point
+ *       (hl << (16 + fb)) | (round(lh * 2^fb) << 16) | (wl << fb) | round(lw * 2^fb)
+ *       of the top-left corner (hl, wl) and the fractions (lh, lw) in level pixels;
+ *   bytes [64 + 8 l, 72 + 8 l): level l's 4 attention weights, f16.
+ * Corner rows / columns outside the level are folded into the weight (a footprint whose top row
+ * is -1 becomes row 0 with weight a*lh and lh = 0, a bottom row H-1 keeps weight a*(1-lh) and
+ * lh = 0; the same for columns), a sample outside the level has weight 0.
+ * W: (num_heads*48, K) weight rows grouped (head, level, [x0 y0 .. x3 y3 | logit0 .. logit3]);
+ * bias likewise (f32).  A (M, K) rows of stride lda, A2 (optional) added at load (query_pos).
+ * ref_points (M, 4, ref_dim) f32, query_attn_mask (M) bytes or NULL, spatial_shapes_host 4 x
+ * (H, W) on the host, each <= 2^(16 - frac_bits); frac_bits in [6, 10]; num_heads % 4 == 0.
+ * Replaces the offsets / attention-weight nn.Linear + F.softmax + location arithmetic of
+ * ms_deform_attn.py:68-82 (the reference's sampling_locations / attention_weights tensors). */
+int kinet_msda_sample_records(const void* A, const void* A2, const void* W, const float* bias, int M,
+                              int num_heads, int K, int lda, int in_dtype, const float* ref_points,
+                              int ref_dim, const uint8_t* query_attn_mask, const int64_t* spatial_shapes_host,
+                              int num_levels, int num_point, int frac_bits, void* records,
+                              kinet_stream_t stream);
+
+/* kinet_msda_encoder_forward fed by sampling records (kinet_msda_sample_records) instead of
+ * f16 offsets / logits + reference points: the sampling kernel's phase 1 is only the fixed-point
+ * unpack, four packed-f16 weight products and the address choice.  records: (num_heads, batch,
+ * num_query) x 96 bytes; the other arguments as kinet_msda_encoder_forward. */
+int kinet_msda_encoder_forward_records(const void* value, int64_t value_sb, int64_t value_sm,
+                                       const int64_t* spatial_shapes_host, const void* records, int frac_bits,
+                                       void* output, int batch, int spatial_size, int num_heads, int channels,
+                                       int num_levels, int num_query, int num_point, int output_dtype,
+                                       const int32_t* query_tile_order, kinet_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

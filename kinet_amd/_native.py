@@ -25,6 +25,8 @@ _SIGS = {
     'kinet_msda_backward_tune': [I] * 5,
     'kinet_msda_encoder_forward': [P, I64, I64, P, P, P, I, P, P] + [I] * 8 + [P, P],
     'kinet_msda_encoder_plan': [P, I, I, I, P],
+    'kinet_msda_sample_records': [P, P, P, P, I, I, I, I, I, P, I, P, P, I, I, I, P, P],
+    'kinet_msda_encoder_forward_records': [P, I64, I64, P, P, I, P] + [I] * 8 + [P, P],
     'kinet_msda_fused_forward': [P, I64, I64, I64, P, P, I, P, I, P, P, P, P] + [I] * 10 + [P, P],
     'kinet_gemm_set_flags': [I],
     'kinet_gemm_force_tile': [I, I],

@@ -38,6 +38,11 @@ struct GemmArgs {
     int m_begin;
     int Hin, Win, Cin, Hout, Wout, KW, stride, pad;
     int stride_w, pad_w;   // horizontal stride / padding (== stride / pad for square convs)
+    // MSDA sampling-record epilogue (gemm_rw.hip, kinet_msda_sample_records): reference
+    // points (M rows x 4 levels x prep_refd f32), fixed-point fraction bits, level shapes
+    const float* prep_ref;
+    int prep_refd, prep_fb;
+    int prep_H[4], prep_W[4];
 };
 
 // gemm_rw.hip: resident-weight streaming GEMM; false = problem not eligible

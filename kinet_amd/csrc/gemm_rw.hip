@@ -27,13 +27,14 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/kinet_gemm.h"
+#include "../../include/kinet_msda.h"
 #include "common.h"
 #include "gemm_common.h"
 
 namespace kinet {
 namespace {
 
-template <int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2>
+template <int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2, bool PREP = false>
 struct RwCfg {
     static constexpr int ROW = KC * 64;                     // A row bytes (K = 32*KC, 16-bit)
     static constexpr int CPR = ROW / 16;                    // 16-byte chunks per A row
@@ -47,15 +48,17 @@ struct RwCfg {
     static constexpr int R_BYTES = HAS_R ? BMR * R_ROW : 0;
     static constexpr int R_OFF = A_BYTES + A2_BYTES;
     static constexpr int MASK_OFF = R_OFF + R_BYTES;
-    static constexpr int STAGE = MASK_OFF + 1024;           // + one DMA of row-mask bytes
+    static constexpr int REF_OFF = MASK_OFF + 1024;         // PREP: the tile's reference points
+    static constexpr int STAGE = REF_OFF + (PREP ? 1024 : 0);   // + one DMA of row-mask bytes (+ refs)
     static constexpr int PAR = 4 * GW * 4;                  // scale, bias, gamma, beta (f32)
     static constexpr int LNS = LN ? 2 * BMR * 4 * 4 : 0;    // [2][BMR][4 waves] partial sums
     static constexpr int BYTES = PAR + LNS + NS * STAGE;
     static constexpr int A_OPS = A_BYTES / 4096;            // DMA instructions per thread per tile
     static constexpr int R_OPS = R_BYTES / 4096;
-    static constexpr int D = A_OPS * (HAS_A2 ? 2 : 1) + R_OPS + 1;
+    static constexpr int D = A_OPS * (HAS_A2 ? 2 : 1) + R_OPS + 1 + (PREP ? 1 : 0);
+    static_assert(!PREP || (NT == 3 && BMR == 16 && !HAS_R && !LN), "sampling records: 12 columns per lane, 16-row tiles");
     static_assert(A_BYTES % 4096 == 0 && R_BYTES % 4096 == 0, "whole DMA rounds per tile");
-    static_assert((CPR & (CPR - 1)) == 0 && (R_CPR & (R_CPR - 1)) == 0, "power-of-two rows");
+    static_assert((CPR & (CPR - 1)) == 0 && (!HAS_R || (R_CPR & (R_CPR - 1)) == 0), "power-of-two rows");
     static_assert(BMR / 16 <= 64, "mask DMA lanes");
 };
 
@@ -108,13 +111,93 @@ __device__ __forceinline__ void unpack8(const u32x4& u, float* v, bool f16) {
     }
 }
 
+// Sampling records of one (query, head, level) from the 12 projection outputs this lane holds
+// (ms_deform_attn.py:69-82 + the bilinear setup of ms_deform_im2col_cuda.cuh:227-233):
+//   v = [x0 y0 x1 y1 x2 y2 x3 y3 | logit0..3] of level l (offsets in level pixels, the head's
+//   16 logits spread over the 4 lanes lane, lane^16, lane^32, lane^48 -- one per level);
+// softmax over the head's 16 logits, the locations (the reference's offsets / (H, W) on (x, y)
+// quirk for 2-d refs, :77-82), then per point
+//   * the corner rows / columns outside the level folded into the weight: a footprint with its
+//     top row above the level (hl = -1) becomes row 0 with weight a*lh and no second row; a
+//     bottom row below it (hl = H-1) keeps row H-1 with weight a*(1-lh); the same for columns --
+//     so the sampler needs no bounds tests (its second row / column only ever gets weight 0);
+//   * a sample outside the level (cuh:229): weight 0 at the query's own pixel;
+//   * location = fixed point u32 (hl << (16+fb)) | (round(lh 2^fb) << 16) | (wl << fb) | round(lw 2^fb)
+//     (a rounded-up fraction carries into the integer part), weight = f16.
+// out: 4 location words, then the 4 weights as 2 packed f16 words.
+__device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_lds, bool qmasked, int rl, int l,
+                                             const float (&v)[12], uint32_t* out) {
+    const int Hl = l == 0 ? p.prep_H[0] : l == 1 ? p.prep_H[1] : l == 2 ? p.prep_H[2] : p.prep_H[3];
+    const int Wl = l == 0 ? p.prep_W[0] : l == 1 ? p.prep_W[1] : l == 2 ? p.prep_W[2] : p.prep_W[3];
+    const float Hf = (float)Hl, Wf = (float)Wl;
+    const int fb = p.prep_fb;
+    const float fs = (float)(1 << fb);
+    float mx = fmaxf(fmaxf(v[8], v[9]), fmaxf(v[10], v[11]));
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float e[4], es = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        e[q] = __expf(v[8 + q] - mx);
+        es += e[q];
+    }
+    es += __shfl_xor(es, 16);
+    es += __shfl_xor(es, 32);
+    const float ra = qmasked ? 0.f : 1.f / es;
+    float rx, ry, rw = 0.f, rh = 0.f;
+    if (p.prep_refd == 2) {
+        const float2 r = *reinterpret_cast<const float2*>(ref_lds + (rl * 4 + l) * 8);
+        rx = r.x;
+        ry = r.y;
+    } else {
+        const float4 r = *reinterpret_cast<const float4*>(ref_lds + (rl * 4 + l) * 16);
+        rx = r.x;
+        ry = r.y;
+        rw = r.z;
+        rh = r.w;
+    }
+    // the query's own pixel of this level: where a sample outside the level points (weight 0)
+    const int hr = min(max((int)floorf(ry * Hf), 0), Hl - 1), wr = min(max((int)floorf(rx * Wf), 0), Wl - 1);
+    float aw[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        float x, y;
+        if (p.prep_refd == 2) {
+            x = rx + v[2 * q] / Hf;       // :77-79 (offsets / spatial_shapes, (H, W) on (x, y))
+            y = ry + v[2 * q + 1] / Wf;
+        } else {
+            x = rx + v[2 * q] * 0.125f * rw;   // :80-82 (/ n_points * wh * 0.5, n_points = 4)
+            y = ry + v[2 * q + 1] * 0.125f * rh;
+        }
+        float a = e[q] * ra;
+        const float h = y * Hf - 0.5f, w = x * Wf - 0.5f;
+        const bool valid = h > -1.f && w > -1.f && h < Hf && w < Wf;
+        const float hfl = floorf(h), wfl = floorf(w);
+        float lh = h - hfl, lw = w - wfl;
+        int hl = (int)hfl, wl = (int)wfl;
+        if (hl < 0) { a *= lh; hl = 0; lh = 0.f; }
+        else if (hl >= Hl - 1) { a *= 1.f - lh; hl = Hl - 1; lh = 0.f; }
+        if (wl < 0) { a *= lw; wl = 0; lw = 0.f; }
+        else if (wl >= Wl - 1) { a *= 1.f - lw; wl = Wl - 1; lw = 0.f; }
+        int qh = (int)(lh * fs + 0.5f), qw = (int)(lw * fs + 0.5f);
+        if (qh >= (1 << fb)) { qh = 0; ++hl; }
+        if (qw >= (1 << fb)) { qw = 0; ++wl; }
+        if (!valid) { a = 0.f; hl = hr; wl = wr; qh = qw = 0; }
+        out[q] = ((uint32_t)hl << (16 + fb)) | ((uint32_t)qh << 16) | ((uint32_t)wl << fb) | (uint32_t)qw;
+        aw[q] = a;
+    }
+    out[4] = (uint32_t)__builtin_bit_cast(uint16_t, (f16_t)aw[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, (f16_t)aw[1]) << 16);
+    out[5] = (uint32_t)__builtin_bit_cast(uint16_t, (f16_t)aw[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, (f16_t)aw[3]) << 16);
+}
+
 // CR (conv-row mode): A row m is output pixel (img, oh, ow) of a KH x 1, horizontally
 // stride-1 unpadded NHWC convolution (the tap-folded ResNet stem, ops.hip
 // pack_image_kwfold_kernel): K = KH*Cin, logical chunk q of the row = 8 channels of tap
 // kh = q / (Cin/8) read from input row oh*stride - pad + kh (zeros outside the image and past K)
-template <typename T, typename TO, int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2, bool CR>
+template <typename T, typename TO, int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2, bool CR,
+          bool PREP = false>
 __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const int n_mtiles) {
-    using C_ = RwCfg<KC, NT, BMR, NS, HAS_R, LN, HAS_A2>;
+    using C_ = RwCfg<KC, NT, BMR, NS, HAS_R, LN, HAS_A2, PREP>;
     constexpr int TMR = BMR / 16;             // 16-row MFMA tiles per row tile
     constexpr int GW = C_::GW;
     constexpr int NC = NT * 4;                // consecutive columns per lane
@@ -168,6 +251,8 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
     const __amdgpu_buffer_rsrc_t rm =
         __builtin_amdgcn_make_buffer_rsrc((void*)(p.row_mask ? (const void*)p.row_mask : p.A), (short)0,
                                           p.row_mask ? M : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(PREP ? (const void*)p.prep_ref : p.A), (short)0, PREP ? M * 16 * p.prep_refd : 0, 0x00020000);
 
     // per-thread DMA offsets, split into a scalar tile base (m0 * ld) and lane constants
     unsigned a_lo[C_::A_OPS];
@@ -235,6 +320,13 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
         }
         // row-mask bytes m0 .. m0+BMR (every wave writes the same 1 KiB; bytes past M read 0)
         dma16(rm, st + C_::MASK_OFF, lane < TMR ? (unsigned)(m0 + lane * 16) : OOB);
+        // PREP: the tile's reference points, BMR rows x 4 levels x prep_refd f32 (<= 1 KiB; every
+        // wave writes the same bytes, rows past M read 0)
+        if constexpr (PREP) {
+            const unsigned rbytes = (unsigned)(BMR * 16 * p.prep_refd);
+            dma16(rf, st + C_::REF_OFF, (unsigned)lane * 16u < rbytes ? (unsigned)m0 * 16u * (unsigned)p.prep_refd +
+                                                                         (unsigned)lane * 16u : OOB);
+        }
     };
 
     __syncthreads();   // parameters visible; no DMA in flight yet
@@ -250,15 +342,30 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
     // counted waits below know exactly how many vector-memory ops are younger than a DMA
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, p.c_bytes, 0x00020000);
     constexpr int EPC16 = 16 / (int)sizeof(TO);     // elements per 16-byte store
-    constexpr int S = TMR * (NC / EPC16);           // stores per lane per row tile
+    // stores per lane per row tile (PREP: one 16-byte location store + one 8-byte weight store)
+    constexpr int S = TMR * (PREP ? 2 : NC / EPC16);
     static_assert(NS >= 2 && NS <= 4 && (NS - 2) * (C_::D + S) <= 63, "ring depth / vmcnt range");
     // element offset of (row m, column n): m * rs + colpart(n); head-major (hm_rows > 0):
     // ((g*hm_batch + b)*hm_rows + s)*hm_d + d = g*M*hm_d + m*hm_d + d for m = b*hm_rows + s
-    const int rs = p.hm_rows ? p.hm_d : p.ldc;
-    unsigned s_lo[TMR][NC / EPC16];
-    bool s_nok[NC / EPC16];
+    const int rs = PREP ? 96 / (int)sizeof(TO) : (p.hm_rows ? p.hm_d : p.ldc);
+    constexpr int NSL = PREP ? 2 : NC / EPC16;
+    unsigned s_lo[TMR][NSL];
+    bool s_nok[NSL];
+    if constexpr (PREP) {
+        // record (head h, row m) at (h*M + m)*96 bytes: [4 levels x 16 B locations | 4 levels x 8 B weights];
+        // this lane writes level lane >> 4 of head blockIdx.y*4 + wave
+        const unsigned hb = (unsigned)(blockIdx.y * 4 + wave) * (unsigned)M;
+        const unsigned l = (unsigned)(lane >> 4);
 #pragma unroll
-    for (int h = 0; h < NC / EPC16; ++h) {
+        for (int t = 0; t < TMR; ++t) {
+            const unsigned r = (hb + (unsigned)(t * 16 + (lane & 15))) * 96u;
+            s_lo[t][0] = r + l * 16u;
+            s_lo[t][1] = r + 64u + l * 8u;
+        }
+        s_nok[0] = s_nok[1] = false;
+    }
+#pragma unroll
+    for (int h = 0; h < (PREP ? 0 : NC / EPC16); ++h) {
         const int n = ncol0 + cl0 + h * EPC16;
         s_nok[h] = n >= N;
         const int g = p.hm_rows ? n / p.hm_d : 0;
@@ -270,6 +377,18 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
     }
     auto store_pending = [&](bool valid) {
         const unsigned base = (unsigned)pend_m0 * (unsigned)rs * (unsigned)sizeof(TO);
+        if constexpr (PREP) {
+#pragma unroll
+            for (int t = 0; t < TMR; ++t) {
+                const bool mok = valid && pend_m0 + t * 16 + (lane & 15) < M;
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{pend[t][0], pend[t][1], pend[t][2], pend[t][3]}, rc,
+                                                       mok ? base + s_lo[t][0] : OOB, 0, 0);
+                typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2_{pend[t][4], pend[t][5]}, rc, mok ? base + s_lo[t][1] : OOB,
+                                                      0, 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int t = 0; t < TMR; ++t) {
             const bool mok = valid && pend_m0 + t * 16 + (lane & 15) < M;
@@ -325,6 +444,17 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
 
         // ---- epilogue (registers) ----
         float v[TMR][NC];
+        if constexpr (PREP) {
+#pragma unroll
+            for (int t = 0; t < TMR; ++t) {
+#pragma unroll
+                for (int j = 0; j < NC; ++j) v[t][j] = acc[j >> 2][t][j & 3] + par[GW + cl0 + j];
+                prep_records(p, st + C_::REF_OFF, st[C_::MASK_OFF + t * 16 + (lane & 15)] != 0, t * 16 + (lane & 15),
+                             lane >> 4, v[t], pend[t]);
+            }
+            pend_m0 = m0;
+            continue;
+        }
 #pragma unroll
         for (int t = 0; t < TMR; ++t) {
             const int rl = t * 16 + (lane & 15);
@@ -399,7 +529,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
 }
 
 template <typename T, typename TO, int KC, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2 = false, int NT = 4,
-          bool CR = false>
+          bool CR = false, bool PREP = false>
 void launch_cfg(const GemmArgs& a, hipStream_t stream) {
     constexpr int GW = 4 * NT * 16;
     const int n_mtiles = (a.M + BMR - 1) / BMR;
@@ -410,16 +540,16 @@ void launch_cfg(const GemmArgs& a, hipStream_t stream) {
     int P = 512 / ng >= 8 ? 512 / ng / 8 * 8 : 512 / ng;
     if (P > n_mtiles) P = n_mtiles;
     dim3 grid(P, ng), block(256);
-    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR>), grid, block, 0, stream, a,
-                       n_mtiles);
+    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR, PREP>), grid, block, 0, stream,
+                       a, n_mtiles);
 }
 
 // deepest DMA ring (<= 4 row tiles) that keeps the workgroup within 80 KiB of LDS (two per CU)
-template <int KC, int BMR, bool HAS_R, bool LN, bool HAS_A2, int NT = 4>
+template <int KC, int BMR, bool HAS_R, bool LN, bool HAS_A2, int NT = 4, bool PREP = false>
 constexpr int ring_depth() {
-    constexpr int base = RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2>::BYTES -
-                         RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2>::STAGE;
-    constexpr int stage = RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2>::STAGE;
+    constexpr int base = RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2, PREP>::BYTES -
+                         RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2, PREP>::STAGE;
+    constexpr int stage = RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2, PREP>::STAGE;
     return (80 * 1024 - base) / stage >= 4 ? 4 : (80 * 1024 - base) / stage;
 }
 
@@ -519,3 +649,60 @@ bool launch_rw_conv(const GemmArgs& a, int in_dtype, hipStream_t stream) {
 }
 
 }  // namespace kinet
+
+using namespace kinet;
+
+// The MSDA sampling-offsets | attention-weights projection of an encoder call, with the
+// softmax, sampling locations and bilinear setup in its epilogue (prep_records): writes the
+// head-major sampling records kinet_msda_encoder_forward_records reads.  include/kinet_msda.h.
+extern "C" int kinet_msda_sample_records(const void* A, const void* A2, const void* W, const float* bias, int M,
+                                         int num_heads, int K, int lda, int in_dtype, const float* ref_points,
+                                         int ref_dim, const uint8_t* query_attn_mask, const int64_t* spatial_shapes_host,
+                                         int num_levels, int num_point, int frac_bits, void* records,
+                                         kinet_stream_t stream) {
+    KINET_CHECK_ARG(M >= 0 && num_heads > 0 && num_heads % 4 == 0, "msda records: heads must be a multiple of 4 (got %d)",
+                    num_heads);
+    KINET_CHECK_ARG(num_levels == 4 && num_point == 4, "msda records: 4 levels x 4 points (got %d, %d)", num_levels,
+                    num_point);
+    KINET_CHECK_ARG(K == 256 && lda % 8 == 0 && lda >= K, "msda records: K must be 256 (got %d), lda %% 8 == 0", K);
+    KINET_CHECK_ARG(in_dtype == KINET_BF16 || in_dtype == KINET_F16, "msda records: bf16 / f16 operands");
+    KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.",
+                    ref_dim);
+    KINET_CHECK_ARG(frac_bits >= 6 && frac_bits <= 10, "msda records: frac_bits in [6, 10] (got %d)", frac_bits);
+    KINET_CHECK_ARG(spatial_shapes_host != nullptr && ref_points != nullptr && records != nullptr && W != nullptr &&
+                        bias != nullptr, "msda records: NULL argument");
+    KINET_CHECK_ARG((((uintptr_t)A) & 15) == 0 && (((uintptr_t)W) & 15) == 0 && (((uintptr_t)records) & 15) == 0 &&
+                        (A2 == nullptr || (((uintptr_t)A2) & 15) == 0) && (((uintptr_t)ref_points) & 15) == 0,
+                    "msda records: A, A2, W, refs and records must be 16-byte aligned");
+    for (int l = 0; l < 4; ++l) {
+        const long long H = spatial_shapes_host[2 * l], Wd = spatial_shapes_host[2 * l + 1];
+        KINET_CHECK_ARG(H > 0 && Wd > 0 && H <= (1LL << (16 - frac_bits)) && Wd <= (1LL << (16 - frac_bits)),
+                        "msda records: level %d (%lld x %lld) exceeds the %d-bit integer part", l, H, Wd, 16 - frac_bits);
+    }
+    if (M == 0) return KINET_OK;
+    const int N = num_heads * 48;
+    const long long ab = ((long long)(M - 1) * lda + K) * 2, bb = (long long)N * K * 2;
+    const long long cb = (long long)num_heads * M * 96, rb = (long long)M * 16 * ref_dim;
+    KINET_CHECK_ARG(ab < (1LL << 31) && cb < (1LL << 31) && rb < (1LL << 31), "msda records: operands larger than 2 GiB");
+    GemmArgs a{};
+    a.A = A; a.A2 = A2; a.B = W; a.C = records; a.bias = bias; a.row_mask = query_attn_mask;
+    a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = K; a.ldc = N;
+    a.a_bytes = (int)ab; a.b_bytes = (int)bb; a.c_bytes = (int)cb;
+    a.prep_ref = ref_points; a.prep_refd = ref_dim; a.prep_fb = frac_bits;
+    for (int l = 0; l < 4; ++l) {
+        a.prep_H[l] = (int)spatial_shapes_host[2 * l];
+        a.prep_W[l] = (int)spatial_shapes_host[2 * l + 1];
+    }
+    hipStream_t s = (hipStream_t)stream;
+    constexpr int NS2 = ring_depth<8, 16, false, false, true, 3, true>();
+    constexpr int NS1 = ring_depth<8, 16, false, false, false, 3, true>();
+    if (in_dtype == KINET_BF16) {
+        if (A2) launch_cfg<bf16_t, f16_t, 8, 16, NS2, false, false, true, 3, false, true>(a, s);
+        else launch_cfg<bf16_t, f16_t, 8, 16, NS1, false, false, false, 3, false, true>(a, s);
+    } else {
+        if (A2) launch_cfg<f16_t, f16_t, 8, 16, NS2, false, false, true, 3, false, true>(a, s);
+        else launch_cfg<f16_t, f16_t, 8, 16, NS1, false, false, false, 3, false, true>(a, s);
+    }
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}

@@ -86,6 +86,7 @@ struct EncArgs {
     void* out;             // (B, Lq, M*32) row-major
     const int* torder;     // processing order of the 16-query tiles (or null)
     int S, B, M, Lq, nstrip, used, ref_dim;
+    int fb;                // sampling records (REC): fraction bits of the fixed-point locations
 };
 
 // quad broadcast: every lane of a quad takes lane `SRC` of its quad
@@ -159,7 +160,9 @@ struct TileIn {
     uint32_t qm;    // query mask byte
 };
 
-template <int REFD, bool QM>
+// (REC: off = the 4 fixed-point locations, lg = the 4 f16 weights of kinet_msda_sample_records,
+// same offsets in the 96-byte row; no reference point or mask: folded into the records)
+template <int REFD, bool QM, bool REC = false>
 __device__ __forceinline__ void load_tile(TileIn& in, const __amdgpu_buffer_rsrc_t& ro,
                                           const __amdgpu_buffer_rsrc_t& rr, const __amdgpu_buffer_rsrc_t& rq,
                                           int b, int Lq, int q, int l) {
@@ -167,6 +170,7 @@ __device__ __forceinline__ void load_tile(TileIn& in, const __amdgpu_buffer_rsrc
     const uint32_t ob = qq * (uint32_t)(EREC * 2);
     in.off = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(ro, ob + (uint32_t)l * 16u, 0, 0));
     in.lg = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ro, ob + 64u + (uint32_t)l * 8u, 0, 0));
+    if constexpr (REC) return;
     const uint32_t row = (uint32_t)b * (uint32_t)Lq + qq;
     const uint32_t rb = (row * (uint32_t)EL + (uint32_t)l) * (uint32_t)REFD * 4u;
     if constexpr (REFD == 2) {
@@ -247,6 +251,67 @@ __device__ __forceinline__ void setup_tile(const TileIn& in, const EncLevels& lv
     }
 }
 
+// Phase 1 from sampling records (kinet_msda_sample_records: softmax, locations, out-of-level
+// corners and samples already folded into the weights): per point, unpack the fixed-point
+// location, build the 4 corner weights in packed f16 and choose the address -- no bounds tests.
+//   X = (1 + lw, 1 + lh) as f16: the fraction bits shifted into the mantissa of 1.0;
+//   HL = (1 - lh, lh), WL = (1 - lw, lw); A = HL * a; rw01 = WL * A.lo, rw23 = WL * A.hi.
+struct RecK {
+    uint32_t sh_h, fmask2, sh2, wbits;   // 16 + fb, the two fraction fields, (10 - fb) per half, 16 - fb
+};
+__device__ __forceinline__ uint32_t pk_lsl16(uint32_t x, uint32_t sh2) {
+    uint32_t d;
+    asm("v_pk_lshlrev_b16 %0, %1, %2" : "=v"(d) : "s"(sh2), "v"(x));
+    return d;
+}
+// (1 - X.hi, X.hi - 1) and (1 - X.lo, X.lo - 1) for X = (1 + lw, 1 + lh): (2 - x, x - 1)
+__device__ __forceinline__ uint32_t pk_frac_hi(uint32_t x, uint32_t c) {
+    uint32_t d;
+    asm("v_pk_add_f16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[1,0]" : "=v"(d) : "v"(x), "s"(c));
+    return d;
+}
+__device__ __forceinline__ uint32_t pk_frac_lo(uint32_t x, uint32_t c) {
+    uint32_t d;
+    asm("v_pk_add_f16 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1] neg_lo:[1,0]" : "=v"(d) : "v"(x), "s"(c));
+    return d;
+}
+template <int HALF>
+__device__ __forceinline__ uint32_t pk_mul_bcast(uint32_t x, uint32_t y) {   // x * (y.HALF, y.HALF)
+    uint32_t d;
+    if constexpr (HALF == 0) asm("v_pk_mul_f16 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(d) : "v"(x), "v"(y));
+    else asm("v_pk_mul_f16 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(d) : "v"(x), "v"(y));
+    return d;
+}
+
+template <int FL>
+__device__ __forceinline__ void setup_tile_rec(const TileIn& in, const EncLevels& lv, int l, const RecK& rk,
+                                               uint32_t (&ro)[4], uint32_t (&rw01)[4], uint32_t (&rw23)[4]) {
+    const bool in_lds = l >= FL;
+    const LevelRec L = lv.rec[l];
+    const uint32_t W = (uint32_t)L.W;
+    const uint32_t st64 = (uint32_t)L.start * 64u, lb64 = (uint32_t)L.lb * 64u, far64 = (W + 1u) * 64u;
+    const uint32_t r0 = (uint32_t)L.r0, rn = (uint32_t)(L.r1 - L.r0);
+    constexpr uint32_t CF = 0xBC004000u;   // (2.0, -1.0) f16
+#pragma unroll
+    for (int p = 0; p < EP; ++p) {
+        const uint32_t u = in.off[p];
+        const uint32_t hl = u >> rk.sh_h;
+        const uint32_t wl = __builtin_amdgcn_ubfe(u, 16u - rk.wbits, rk.wbits);
+        const uint32_t x = pk_lsl16(u & rk.fmask2, rk.sh2) | 0x3C003C00u;
+        const uint32_t hlw = pk_frac_hi(x, CF), wlw = pk_frac_lo(x, CF);
+        const uint32_t aw = (p & 1) ? pk_mul_bcast<1>(hlw, p < 2 ? in.lg.x : in.lg.y)
+                                    : pk_mul_bcast<0>(hlw, p < 2 ? in.lg.x : in.lg.y);
+        rw01[p] = pk_mul_bcast<0>(wlw, aw);
+        rw23[p] = pk_mul_bcast<1>(wlw, aw);
+        const uint32_t pix = (uint32_t)__mul24((int)hl, (int)W) + wl;
+        const uint32_t gofs = pix * 64u + st64;                              // head-map offset of (hl, wl)
+        const uint32_t lo = pix * 64u + lb64;                                // LDS map offset
+        const uint32_t go = TAF + (gofs + far64);                            // far: corner (hl+1, wl+1)
+        const bool staged = hl - r0 < rn;                                    // rows hl, hl+1 staged
+        ro[p] = in_lds ? (staged ? lo : go) : gofs;
+    }
+}
+
 // the lane id recomputed where it is used (volatile: not hoisted out of the tile loop, so the
 // lane-constant offsets derived from it cost a VALU op instead of a register across the loop)
 __device__ __forceinline__ int lane_id_here() {
@@ -308,7 +373,7 @@ __device__ __forceinline__ void strip_rows(const EncArgs& a, const EncLevels& lv
     }
 }
 
-template <typename TO, int FL, int REFD, bool QM>
+template <typename TO, int FL, int REFD, bool QM, bool REC>
 __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4v* vmap, int b, int m, int strip,
                                           int wave, int lane) {
     constexpr int NGL = FL;            // levels gathered through the texture path
@@ -331,6 +396,14 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, a.B * Lq * a.M * 64, 0x00020000);
 
     const char* vm = reinterpret_cast<const char*>(vmap) + cb;
+    RecK rk;
+    if constexpr (REC) {
+        const uint32_t fb = (uint32_t)a.fb;
+        rk.sh_h = 16u + fb;
+        rk.fmask2 = ((1u << fb) - 1u) * 0x10001u;
+        rk.sh2 = (10u - fb) * 0x10001u;
+        rk.wbits = 16u - fb;
+    }
     int wb[EL];
 #pragma unroll
     for (int l = 0; l < EL; ++l) wb[l] = a.W[l] * 64;
@@ -400,7 +473,7 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
     }
 
     // the first tile's phase-1 inputs ahead of the DMA (so waiting for them does not wait for it)
-    if (has) load_tile<REFD, QM>(in, ro, rr, rq, b, Lq, q0 + qi, l1);
+    if (has) load_tile<REFD, QM, REC>(in, ro, rr, rq, b, Lq, q0 + qi, l1);
     // ---- LDS-DMA fill of the staged regions, in flight with the first tile's setup and gathers (pieces
     // of 16 map pixels = 1 KiB per wave-instruction; map pixels outside every region and rows
     // outside the image: the range check's zeros) ----
@@ -423,7 +496,8 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
     }
 
     if (has) {
-        setup_tile<FL, REFD>(in, lv, l1, q0 + qi < Lq, rec_o, rec_w01, rec_w23);
+        if constexpr (REC) setup_tile_rec<FL>(in, lv, l1, rk, rec_o, rec_w01, rec_w23);
+        else setup_tile<FL, REFD>(in, lv, l1, q0 + qi < Lq, rec_o, rec_w01, rec_w23);
         if constexpr (NGL > 0) issue(std::integral_constant<int, 0>{});
     }
     // every wave: its DMA pieces (and the first gathers) landed, then everyone's
@@ -439,7 +513,7 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
         // the next tile's phase-1 inputs, behind this tile's gathers
         if (more) {
             const int li = lane_id_here();
-            load_tile<REFD, QM>(in, ro, rr, rq, b, Lq, qn0 + (li >> 2), li & 3);
+            load_tile<REFD, QM, REC>(in, ro, rr, rq, b, Lq, qn0 + (li >> 2), li & 3);
         }
         f32x2 acc[4] = {};
         // the gathered level: weights fetched from the quad again (registers are the limit)
@@ -543,13 +617,14 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
         q0 = qn0;
         {
             const int li = lane_id_here();
-            setup_tile<FL, REFD>(in, lv, li & 3, q0 + (li >> 2) < Lq, rec_o, rec_w01, rec_w23);
+            if constexpr (REC) setup_tile_rec<FL>(in, lv, li & 3, rk, rec_o, rec_w01, rec_w23);
+            else setup_tile<FL, REFD>(in, lv, li & 3, q0 + (li >> 2) < Lq, rec_o, rec_w01, rec_w23);
         }
         if constexpr (NGL > 0) issue(std::integral_constant<int, 0>{});
     }
 }
 
-template <typename TO, int FL, int REFD, bool QM>
+template <typename TO, int FL, int REFD, bool QM, bool REC = false>
 __global__ __launch_bounds__(EW * 64) void msda_enc_kernel(const EncArgs a) {
     __shared__ EncLevels lv;
     __shared__ u32x4v vmap[EMAP_PIX * 4];
@@ -586,7 +661,7 @@ __global__ __launch_bounds__(EW * 64) void msda_enc_kernel(const EncArgs a) {
     }
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    enc_tiles<TO, FL, REFD, QM>(a, lv, vmap, b, m, strip, wave, lane);
+    enc_tiles<TO, FL, REFD, QM, REC>(a, lv, vmap, b, m, strip, wave, lane);
 }
 
 // LDS regions for strips of 1/n of the image: rows ceil(H/n) + 3 (pixel centres, the +1 corner
@@ -664,18 +739,24 @@ extern "C" int kinet_msda_encoder_plan(const int64_t* spatial_shapes_host, int b
     return KINET_OK;
 }
 
-extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, int64_t value_sm,
-                                          const int64_t* spatial_shapes_host, const void* offsets_logits_hm,
-                                          const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
-                                          void* output, int batch, int spatial_size, int num_heads, int channels,
-                                          int num_levels, int num_query, int num_point, int output_dtype,
-                                          const int32_t* query_tile_order, kinet_stream_t stream) {
+namespace {
+// kinet_msda_encoder_forward (rec = false: f16 offsets / logits + reference points) and
+// kinet_msda_encoder_forward_records (rec = true: sampling records)
+int encoder_forward(const void* value, int64_t value_sb, int64_t value_sm, const int64_t* spatial_shapes_host,
+                    const void* offlog, const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
+                    int frac_bits, bool rec, void* output, int batch, int spatial_size, int num_heads, int channels,
+                    int num_levels, int num_query, int num_point, int output_dtype, const int32_t* query_tile_order,
+                    kinet_stream_t stream) {
     KINET_CHECK_ARG(batch >= 0 && spatial_size > 0 && num_heads > 0 && num_query >= 0, "msda encoder: bad sizes");
     KINET_CHECK_ARG(channels == 32 && num_levels == EL && num_point == EP,
                     "msda encoder: head_dim 32, 4 levels, 4 points (got %d, %d, %d)", channels, num_levels, num_point);
-    KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.", ref_dim);
+    if (!rec)
+        KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.",
+                        ref_dim);
+    else
+        KINET_CHECK_ARG(frac_bits >= 6 && frac_bits <= 10, "msda encoder: frac_bits in [6, 10] (got %d)", frac_bits);
     KINET_CHECK_ARG(output_dtype == KINET_BF16 || output_dtype == KINET_F16, "msda encoder: output must be bf16 or f16");
-    KINET_CHECK_ARG(((uintptr_t)value % 16) == 0 && ((uintptr_t)offsets_logits_hm % 16) == 0 && value_sb % 8 == 0 &&
+    KINET_CHECK_ARG(((uintptr_t)value % 16) == 0 && ((uintptr_t)offlog % 16) == 0 && value_sb % 8 == 0 &&
                         value_sm % 8 == 0,
                     "msda encoder: value / offsets must be 16-byte aligned");
     KINET_CHECK_ARG(spatial_shapes_host != nullptr, "msda encoder: spatial_shapes_host is NULL");
@@ -684,6 +765,10 @@ extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, i
         KINET_CHECK_ARG(spatial_shapes_host[2 * l] > 0 && spatial_shapes_host[2 * l + 1] > 0 &&
                             spatial_shapes_host[2 * l] * spatial_shapes_host[2 * l + 1] < (1LL << 30),
                         "msda encoder: bad level shape");
+        if (rec)
+            KINET_CHECK_ARG(spatial_shapes_host[2 * l] <= (1LL << (16 - frac_bits)) &&
+                                spatial_shapes_host[2 * l + 1] <= (1LL << (16 - frac_bits)),
+                            "msda encoder: level %d exceeds the records' %d-bit integer part", l, 16 - frac_bits);
         npix += spatial_shapes_host[2 * l] * spatial_shapes_host[2 * l + 1];
     }
     KINET_CHECK_ARG(npix == spatial_size, "msda encoder: spatial_shapes cover %lld tokens, value has %d", npix,
@@ -695,10 +780,11 @@ extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, i
     const long long head_bytes = (long long)spatial_size * 64;
     long long wmax = 0;
     for (int l = 0; l < EL; ++l) wmax = std::max<long long>(wmax, spatial_shapes_host[2 * l + 1]);
+    const int rd = rec ? 2 : ref_dim;
     // far-sample records carry a map offset up to (S + W + 1) * 64 below the TAF flag bit
     KINET_CHECK_ARG((spatial_size + wmax + 2) * 64 < (1LL << 31) && (long long)num_query * EREC * 2 < (1LL << 31) &&
                         (long long)batch * num_query < (1LL << 24) &&
-                        (long long)batch * num_query * EL * ref_dim * 4 < (1LL << 31) &&
+                        (long long)batch * num_query * EL * rd * 4 < (1LL << 31) &&
                         (long long)batch * num_query * num_heads * 64 < (1LL << 31),
                     "msda encoder: problem too large for 32-bit buffer offsets");
     EncArgs a{};
@@ -712,25 +798,28 @@ extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, i
         a.cap[l] = pl.cap[l];
         a.base[l] = pl.base[l];
     }
-    a.offlog = (const f16_t*)offsets_logits_hm;
-    a.ref = ref_points;
-    a.qmask = query_attn_mask;
+    a.offlog = (const f16_t*)offlog;
+    a.ref = rec ? nullptr : ref_points;
+    a.qmask = rec ? nullptr : query_attn_mask;
     a.out = output;
     a.torder = (const int*)query_tile_order;
     a.S = spatial_size;
     a.B = batch;
     a.M = num_heads;
     a.Lq = num_query;
-    a.ref_dim = ref_dim;
+    a.ref_dim = rd;
     a.nstrip = pl.nstrip;
     a.used = pl.used;
+    a.fb = rec ? frac_bits : 0;
     const long long maps = (long long)batch * num_heads;
     KINET_CHECK_ARG(maps * pl.nstrip < (1LL << 31), "msda encoder: grid too large");
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)(maps * pl.nstrip)), block(EW * 64);
 #define EK(TO_, FL_, RD_, QM_) hipLaunchKernelGGL((msda_enc_kernel<TO_, FL_, RD_, QM_>), grid, block, 0, s, a)
 #define EK_QM(TO_, FL_, RD_) if (query_attn_mask) EK(TO_, FL_, RD_, true); else EK(TO_, FL_, RD_, false)
-#define EK_RD(TO_, FL_) if (ref_dim == 2) { EK_QM(TO_, FL_, 2); } else { EK_QM(TO_, FL_, 4); }
+#define EK_RD(TO_, FL_)                                                                                  \
+    if (rec) hipLaunchKernelGGL((msda_enc_kernel<TO_, FL_, 2, false, true>), grid, block, 0, s, a);     \
+    else if (ref_dim == 2) { EK_QM(TO_, FL_, 2); } else { EK_QM(TO_, FL_, 4); }
 #define EK_FL(TO_)                        \
     switch (pl.fl) {                      \
         case 0: EK_RD(TO_, 0) break;      \
@@ -749,4 +838,28 @@ extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, i
 #undef EK
     KINET_LAUNCH_CHECK();
     return KINET_OK;
+}
+}  // namespace
+
+extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, int64_t value_sm,
+                                          const int64_t* spatial_shapes_host, const void* offsets_logits_hm,
+                                          const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
+                                          void* output, int batch, int spatial_size, int num_heads, int channels,
+                                          int num_levels, int num_query, int num_point, int output_dtype,
+                                          const int32_t* query_tile_order, kinet_stream_t stream) {
+    return encoder_forward(value, value_sb, value_sm, spatial_shapes_host, offsets_logits_hm, ref_points, ref_dim,
+                           query_attn_mask, 0, false, output, batch, spatial_size, num_heads, channels, num_levels,
+                           num_query, num_point, output_dtype, query_tile_order, stream);
+}
+
+extern "C" int kinet_msda_encoder_forward_records(const void* value, int64_t value_sb, int64_t value_sm,
+                                                  const int64_t* spatial_shapes_host, const void* records,
+                                                  int frac_bits, void* output, int batch, int spatial_size,
+                                                  int num_heads, int channels, int num_levels, int num_query,
+                                                  int num_point, int output_dtype, const int32_t* query_tile_order,
+                                                  kinet_stream_t stream) {
+    KINET_CHECK_ARG(records != nullptr, "msda encoder: records is NULL");
+    return encoder_forward(value, value_sb, value_sm, spatial_shapes_host, records, nullptr, 2, nullptr, frac_bits,
+                           true, output, batch, spatial_size, num_heads, channels, num_levels, num_query, num_point,
+                           output_dtype, query_tile_order, stream);
 }

@@ -623,6 +623,87 @@ def msda_encoder(value, shapes, offlog_hm, reference_points, n_heads, query_attn
     return out
 
 
+# encoder calls sample through kinet_msda_sample_records + kinet_msda_encoder_forward_records
+# (phase 1 in the projection epilogue) when eligible; False keeps the f16 offsets/logits path
+# (A/B and tests)
+MSDA_RECORDS = [True]
+
+
+def msda_record_frac_bits(shapes):
+    """Fraction bits of the records' fixed-point locations for these level shapes: the most that
+    leave an integer part holding every level's H and W (at most 10), or None (< 6: too large)."""
+    mx = max(max(int(h), int(w)) for h, w in shapes)
+    ib = max(1, (mx - 1).bit_length())
+    fb = min(10, 16 - ib)
+    return fb if fb >= 6 else None
+
+
+def msda_records_supported(query, shapes_host, n_heads, n_levels, n_points):
+    return (MSDA_RECORDS[0] and query.dtype in (torch.bfloat16, torch.float16) and query.shape[-1] == 256
+            and n_heads % 4 == 0 and n_levels == 4 and n_points == 4 and shapes_host is not None
+            and len(shapes_host) == 4 and msda_record_frac_bits(shapes_host) is not None)
+
+
+def msda_sample_records(x, weight, bias, heads, reference_points, shapes_host, x_add=None, query_attn_mask=None):
+    """The encoder MSDA projection with softmax / locations / bilinear setup in the GEMM epilogue
+    (kinet_msda_sample_records): x (B, Lq, 256) [+ x_add], W rows grouped (head, level, 12)
+    (MSDeformAttn.packed_records_weights), reference_points (B, Lq, 4, 2|4) -> (records
+    (heads, B, Lq, 24) int32 = 96 bytes each, frac_bits)."""
+    N.require_gpu(x)
+    B, Lq, K_ = x.shape
+    x2 = x.reshape(B * Lq, K_)
+    a2 = x_add.reshape(B * Lq, K_) if x_add is not None else None
+    if x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16 or \
+            (a2 is not None and (a2.stride() != x2.stride() or a2.data_ptr() % 16)):
+        x2 = x2.contiguous()
+        a2 = a2.contiguous() if a2 is not None else None
+    w = weight_as(weight, x.dtype)
+    key = tuple(tuple(int(v) for v in s) for s in shapes_host)
+    hs = _host_shapes.get(key)
+    if hs is None:
+        hs = _host_shapes[key] = torch.tensor(key, dtype=torch.int64)
+    fb = msda_record_frac_bits(key)
+    ref = reference_points.float().contiguous()
+    qm = query_attn_mask.to(torch.uint8).contiguous() if query_attn_mask is not None else None
+    rec = torch.empty((heads, B, Lq, 24), dtype=torch.int32, device=x.device)
+    e = x.element_size()
+    N.call('kinet_msda_sample_records', N.ptr(x2), N.ptr(a2), N.ptr(w), N.ptr(f32(bias)), B * Lq, heads, K_,
+           x2.stride(0), N.dtype_code(x.dtype), N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(hs), 4, 4, fb, N.ptr(rec),
+           N.stream(x.device),
+           work={'family': 'gemm', 'flops': 2.0 * B * Lq * heads * 48 * K_, 'shape': (B * Lq, heads * 48, K_),
+                 'bytes': (B * Lq * K_ * (2 if a2 is not None else 1) + heads * 48 * K_) * e + ref.numel() * 4
+                 + rec.numel() * 4})
+    return rec, fb
+
+
+def msda_encoder_records(value, shapes, records, frac_bits, out_dtype=None, query_tile_order=None):
+    """Encoder-sized MSDA sampling from sampling records (kinet_msda_encoder_forward_records):
+    value (M, B, S, 32) f16 head-major, records (M, B, Lq, 24) int32 from msda_sample_records
+    -> (B, Lq, M*32)."""
+    M_, B, S, D = value.shape
+    Lq = records.shape[2]
+    key = tuple(tuple(int(v) for v in s) for s in shapes)
+    hs = _host_shapes.get(key)
+    if hs is None:
+        hs = _host_shapes[key] = torch.tensor(key, dtype=torch.int64)
+    od = out_dtype or torch.bfloat16
+    out = torch.empty((B, Lq, M_ * D), dtype=od, device=value.device)
+    if query_tile_order is not None and (query_tile_order.dtype != torch.int32 or
+                                         query_tile_order.numel() != (Lq + 15) // 16):
+        raise RuntimeError('msda_encoder_records: query_tile_order must be int32 with ceil(Lq/16) entries')
+    records = records.contiguous()
+    nsamp = B * Lq * M_ * 16
+    plan = msda_encoder_plan(key, B, M_, Lq)
+    kname = 'msda_enc_kernel<%s, %d, 2, false, true>' % (_KT[od], plan[0] if plan else -1)
+    N.call('kinet_msda_encoder_forward_records', N.ptr(value), value.stride(1), value.stride(0), N.ptr(hs),
+           N.ptr(records), int(frac_bits), N.ptr(out), B, S, M_, D, 4, Lq, 4, N.dtype_code(od),
+           N.ptr(query_tile_order), N.stream(value.device),
+           work={'family': 'msda', 'flops': 10.0 * nsamp * D, 'Lq': Lq, 'S': S, 'kernel': kname,
+                 # compulsory bytes: value once, the 96-byte records, output once
+                 'bytes': B * S * M_ * D * 2 + records.numel() * 4 + out.numel() * out.element_size()})
+    return out
+
+
 def msda_fused(value, spatial_shapes, offlog, reference_points, n_heads, n_levels, n_points,
                query_attn_mask=None, want_loc_attw=False, head_major=False, out_dtype=None,
                query_tile_order=None):

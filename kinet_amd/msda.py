@@ -129,6 +129,20 @@ class MSDeformAttn(nn.Module):
         b = K.cached_multi([so.bias, aw.bias], 'packed_b_hm', lambda a, b: interleave(a, b).float().contiguous())
         return w, b
 
+    def packed_records_weights(self):
+        """The same projection with its rows grouped per (head, level) -- the level's 4 points'
+        (x, y) offset rows, then its 4 logit rows (12 rows) -- the layout whose GEMM epilogue
+        writes the sampling records (kinet_msda_sample_records)."""
+        so, aw = self.sampling_offsets, self.attention_weights
+        M, L, P = self.n_heads, self.n_levels, self.n_points
+
+        def group(a, b):
+            return torch.cat([a.detach().view(M, L, 2 * P, *a.shape[1:]), b.detach().view(M, L, P, *b.shape[1:])],
+                             2).reshape(M * L * 3 * P, *a.shape[1:])
+        w = K.cached_multi([so.weight, aw.weight], 'packed_w_rec', lambda a, b: group(a, b).contiguous())
+        b = K.cached_multi([so.bias, aw.bias], 'packed_b_rec', lambda a, b: group(a, b).float().contiguous())
+        return w, b
+
     def sample(self, query, reference_points, value, input_spatial_shapes, query_attn_mask=None, query_add=None,
                query_order=None, shapes_host=None):
         """value already projected: head-major (M, N, S, D) from project_value (or a
@@ -139,6 +153,13 @@ class MSDeformAttn(nn.Module):
         N_, Lq = query.shape[:2]
         if (query.dtype in (torch.bfloat16, torch.float16) and
                 K.msda_encoder_supported(value, shapes_host, Lq, self.n_heads, self.n_levels, self.n_points, N_)):
+            if K.msda_records_supported(query, shapes_host, self.n_heads, self.n_levels, self.n_points):
+                # phase 1 (softmax, locations, bilinear setup) in the projection's epilogue
+                w, b = self.packed_records_weights()
+                rec, fb = K.msda_sample_records(query, w, b, self.n_heads, reference_points, shapes_host,
+                                                x_add=query_add, query_attn_mask=query_attn_mask)
+                return K.msda_encoder_records(value, shapes_host, rec, fb, out_dtype=query.dtype,
+                                              query_tile_order=query_order)
             w, b = self.packed_offsets_weights_headmajor()
             offlog = K.offsets_proj_headmajor(query, w, b, self.n_heads, x_add=query_add)
             return K.msda_encoder(value, shapes_host, offlog, reference_points, self.n_heads, query_attn_mask,

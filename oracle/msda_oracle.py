@@ -123,3 +123,105 @@ def core_pytorch(value, value_spatial_shapes, sampling_locations, attention_weig
     aw = attention_weights.transpose(1, 2).reshape(N_ * M_, 1, Lq_, L_ * P_)
     out = (torch.stack(sampled, dim=-2).flatten(-2) * aw).sum(-1).view(N_, M_ * D_, Lq_)
     return out.transpose(1, 2).contiguous()
+
+
+# --------------------------------------------------------------------------- sampling records
+# The encoder path's "sampling records" (kinet_msda_sample_records, include/kinet_msda.h): the
+# reference's MSDA preparation (ms_deform_attn.py:68-82) followed by the bilinear setup of
+# ms_deform_im2col_cuda.cuh:227-233, stored per (head, query, level, point) as a fixed-point
+# top-left corner + fraction and an attention weight with the out-of-level corners folded in.
+
+def prep(offlog, ref, shapes, qmask, M, L, P):
+    """ms_deform_attn.py:68-82 op for op (torch CPU, the dtype of offlog): offlog (B, Lq,
+    M*L*P*3) = [sampling_offsets (M, L, P, 2) | attention logits (M, L*P)] -> (loc (B, Lq, M, L,
+    P, 2), attw (B, Lq, M, L, P))."""
+    B, Lq = offlog.shape[:2]
+    so = offlog[..., :M * L * P * 2].reshape(B, Lq, M, L, P, 2)
+    aw = F.softmax(offlog[..., M * L * P * 2:].reshape(B, Lq, M, L * P), -1).reshape(B, Lq, M, L, P)
+    if qmask is not None:
+        aw = aw.masked_fill(qmask[..., None, None, None], 0.0)
+    sh = torch.as_tensor(shapes, dtype=offlog.dtype)
+    if ref.shape[-1] == 2:
+        # the reference divides (x, y) by (H, W) -- spatial_shapes unswapped (:77-79)
+        loc = ref[:, :, None, :, None, :] + so / sh[None, None, None, :, None, :]
+    else:
+        loc = ref[:, :, None, :, None, :2] + so / P * ref[:, :, None, :, None, 2:] * 0.5
+    return loc, aw
+
+
+def sample_records(loc, attw, ref, shapes, fb):
+    """(loc, attw) as above + the (B, Lq, L, 2|4) reference points -> records (M, B, Lq, 24)
+    int32 (96 bytes: [4 levels x 4 u32 locations | 4 levels x 4 f16 weights]), the encoding
+    include/kinet_msda.h states: per sample h = y*H - 0.5, w = x*W - 0.5 (cuh:227-228); outside
+    (-1, H) x (-1, W) (cuh:229) weight 0 at the query's own pixel; a top row -1 becomes row 0 with
+    the weight times lh and lh = 0, a bottom row H-1 keeps the weight times (1 - lh) and lh = 0,
+    the same for columns; fractions rounded to fb bits (a carry moves the corner)."""
+    loc = loc.double()
+    a = attw.double().clone()
+    B, Lq, M, L, P, _ = loc.shape
+    H = torch.tensor([int(h) for h, _ in shapes], dtype=torch.float64)[None, None, None, :, None]
+    W = torch.tensor([int(w) for _, w in shapes], dtype=torch.float64)[None, None, None, :, None]
+    h = loc[..., 1] * H - 0.5
+    w = loc[..., 0] * W - 0.5
+    valid = (h > -1) & (w > -1) & (h < H) & (w < W)
+    hl, wl = torch.floor(h), torch.floor(w)
+    lh, lw = h - hl, w - wl
+    top = hl < 0
+    a = torch.where(top, a * lh, a)
+    bot = ~top & (hl >= H - 1)
+    a = torch.where(bot, a * (1 - lh), a)
+    hl = torch.where(top, torch.zeros_like(hl), torch.where(bot, H - 1 + 0 * hl, hl))
+    lh = torch.where(top | bot, torch.zeros_like(lh), lh)
+    left = wl < 0
+    a = torch.where(left, a * lw, a)
+    right = ~left & (wl >= W - 1)
+    a = torch.where(right, a * (1 - lw), a)
+    wl = torch.where(left, torch.zeros_like(wl), torch.where(right, W - 1 + 0 * wl, wl))
+    lw = torch.where(left | right, torch.zeros_like(lw), lw)
+    s = float(1 << fb)
+    qh, qw = torch.floor(lh * s + 0.5), torch.floor(lw * s + 0.5)
+    hl = torch.where(qh >= s, hl + 1, hl)
+    qh = torch.where(qh >= s, torch.zeros_like(qh), qh)
+    wl = torch.where(qw >= s, wl + 1, wl)
+    qw = torch.where(qw >= s, torch.zeros_like(qw), qw)
+    # outside the level: the query's own pixel, weight 0
+    r = ref.double()[:, :, None, :, None, :]
+    hr = torch.clamp(torch.floor(r[..., 1] * H), torch.zeros_like(H), H - 1).expand_as(hl)
+    wr = torch.clamp(torch.floor(r[..., 0] * W), torch.zeros_like(W), W - 1).expand_as(wl)
+    a = torch.where(valid, a, torch.zeros_like(a))
+    hl = torch.where(valid, hl, hr)
+    wl = torch.where(valid, wl, wr)
+    qh = torch.where(valid, qh, torch.zeros_like(qh))
+    qw = torch.where(valid, qw, torch.zeros_like(qw))
+    word = (hl.long() << (16 + fb)) | (qh.long() << 16) | (wl.long() << fb) | qw.long()   # (B, Lq, M, L, P)
+    word = word.to(torch.int64) & 0xffffffff
+    locw = torch.where(word >= 2 ** 31, word - 2 ** 32, word).to(torch.int32)
+    a16 = a.to(torch.float16).view(torch.int16).to(torch.int32) & 0xffff                      # (B, Lq, M, L, P)
+    aw_words = a16[..., 0::2] | (a16[..., 1::2] << 16)                                          # (B, Lq, M, L, 2)
+    rec = torch.cat([locw.reshape(B, Lq, M, L * P), aw_words.reshape(B, Lq, M, L * 2)], -1)   # (B, Lq, M, 24)
+    return rec.permute(2, 0, 1, 3).contiguous()
+
+
+def decode_records(rec, shapes, fb):
+    """records (M, B, Lq, 24) int32 -> (loc (B, Lq, M, L, P, 2), attw (B, Lq, M, L, P)) float64
+    whose reference sampling (cuh:165-237, `fwd`) is exactly what a record asks for: the corner
+    (hl, wl) + fractions become the location ((wl + lw + 0.5) / W, (hl + lh + 0.5) / H)."""
+    rec = rec.long() & 0xffffffff
+    M, B, Lq, _ = rec.shape
+    L, P = len(shapes), 4
+    locw = rec[..., :L * P].reshape(M, B, Lq, L, P)
+    aww = rec[..., L * P:].reshape(M, B, Lq, L, 2)
+    hl = locw >> (16 + fb)
+    qh = (locw >> 16) & ((1 << fb) - 1)
+    wl = (locw >> fb) & ((1 << (16 - fb)) - 1)
+    qw = locw & ((1 << fb) - 1)
+    s = float(1 << fb)
+    H = torch.tensor([int(h) for h, _ in shapes], dtype=torch.float64)[None, None, None, :, None]
+    W = torch.tensor([int(w) for _, w in shapes], dtype=torch.float64)[None, None, None, :, None]
+    y = (hl.double() + qh.double() / s + 0.5) / H
+    x = (wl.double() + qw.double() / s + 0.5) / W
+    lo = (aww & 0xffff).to(torch.int16)
+    hi = ((aww >> 16) & 0xffff).to(torch.int16)
+    a = torch.stack([lo, hi], -1).reshape(M, B, Lq, L, P).view(torch.float16).double()
+    loc = torch.stack([x, y], -1).permute(1, 2, 0, 3, 4, 5).contiguous()
+    return loc, a.permute(1, 2, 0, 3, 4).contiguous()

@@ -487,3 +487,164 @@ def test_encoder_kernel_strips_staged_and_far(shapes, noise):
     assert (d <= big * 2.0 ** -7 + (2.0 ** -7 + 2.0 ** -11) * vmax).all(), d.max().item()
     assert d.mean().item() <= 2e-3, d.mean().item()
     assert (o_enc.float()[qmask] == 0).all()
+
+
+# ---- sampling records (kinet_msda_sample_records -> kinet_msda_encoder_forward_records) ----
+
+def _record_problem(shapes, B, noise, seed, ref_dim=2, masked=False, dtype=torch.bfloat16):
+    """Encoder-geometry inputs of the records GEMM: x, pos (B, S, 256), the MSDA projection
+    (rows grouped per (head, level) as MSDeformAttn.packed_records_weights), references."""
+    g = torch.Generator().manual_seed(seed)
+    M, L, P = 8, 4, 4
+    S = sum(h * w for h, w in shapes)
+    x = torch.randn(B, S, 256, generator=g).to(dtype)
+    pos = (0.5 * torch.randn(B, S, 256, generator=g)).to(dtype)
+    # offsets ~ noise pixels, logits ~ N(0, 1) (weights scaled so the projections have that spread)
+    w_off = torch.randn(M * L * P * 2, 256, generator=g) * noise / 16.0
+    w_lg = torch.randn(M * L * P, 256, generator=g) / 16.0
+    b_off = torch.randn(M * L * P * 2, generator=g) * noise
+    b_lg = torch.randn(M * L * P, generator=g) * 0.5
+    if ref_dim == 2:
+        ref = _encoder_refs(shapes, B).cpu()
+    else:
+        ref = torch.rand(B, S, L, 4, generator=g)
+        ref[..., 2:] = ref[..., 2:] * 0.5 + 0.05
+    qmask = (torch.rand(B, S, generator=g) < 0.1) if masked else None
+
+    def group(a, b):   # (head, level, [8 offsets | 4 logits])
+        return torch.cat([a.view(M, L, 2 * P, *a.shape[1:]), b.view(M, L, P, *b.shape[1:])], 2).reshape(
+            M * L * 3 * P, *a.shape[1:])
+    w = group(w_off, w_lg).to(dtype)
+    bias = group(b_off, b_lg).float()
+    return x, pos, w, bias, ref, qmask, (w_off, w_lg, b_off, b_lg)
+
+
+def _host_offlog(x, pos, w_off, w_lg, b_off, b_lg, dtype):
+    """The projection in f64 from the operands the GEMM sees (x + pos rounded to the compute
+    dtype, bf16 weights), [offsets | logits] as ms_deform_attn.py:68-69."""
+    q = (x.float() + pos.float()).to(dtype).double()
+    wo, wl = w_off.to(dtype).double(), w_lg.to(dtype).double()
+    return torch.cat([q @ wo.T + b_off.double(), q @ wl.T + b_lg.double()], -1)
+
+
+@pytest.mark.parametrize('shapes', [((100, 167), (50, 84), (25, 42), (13, 21)), ((25, 40), (15, 20), (8, 10), (4, 5))])
+@pytest.mark.parametrize('noise,ref_dim,masked', [(2.0, 2, False), (12.0, 2, True), (3.0, 4, False)])
+def test_sample_records_vs_oracle(shapes, noise, ref_dim, masked):
+    """kinet_msda_sample_records (the GEMM with softmax / locations / bilinear setup in its
+    epilogue) against oracle.sample_records of the reference's preparation (ms_deform_attn.py:
+    68-82, oracle.prep) on the f64 projection of the same operands.  The GEMM's f32
+    accumulation moves a projected value by ~1e-6 relative, which can flip a fraction's last
+    fixed-point bit: locations agree within 1 LSB (2^-fb pixel), weights within f16 rounding;
+    and the two record sets sample the same values (oracle fwd) within 1e-3."""
+    from kinet_amd import kernels as K
+    from oracle import msda_oracle as O
+    B, M = 2, 8
+    x, pos, w, bias, ref, qmask, raw = _record_problem(shapes, B, noise, 41 + int(noise), ref_dim, masked)
+    fb = K.msda_record_frac_bits(shapes)
+    assert fb == 8
+    rec, fb2 = K.msda_sample_records(x.cuda(), w.cuda(), bias.cuda(), M, ref.cuda(), shapes, x_add=pos.cuda(),
+                                     query_attn_mask=qmask.cuda() if masked else None)
+    torch.cuda.synchronize()
+    assert fb2 == fb and rec.shape == (M, B, x.shape[1], 24)
+    offlog = _host_offlog(x, pos, *raw, torch.bfloat16)
+    loc, aw = O.prep(offlog, ref.double(), shapes, qmask, M, 4, 4)
+    exp = O.sample_records(loc, aw, ref, shapes, fb)
+    got = rec.cpu()
+    l_g, a_g = O.decode_records(got, shapes, fb)
+    l_e, a_e = O.decode_records(exp, shapes, fb)
+    H = torch.tensor([h for h, _ in shapes], dtype=torch.float64)[None, None, None, :, None]
+    W = torch.tensor([w_ for _, w_ in shapes], dtype=torch.float64)[None, None, None, :, None]
+    dy = ((l_g[..., 1] - l_e[..., 1]) * H).abs()
+    dx = ((l_g[..., 0] - l_e[..., 0]) * W).abs()
+    lsb = 2.0 ** -fb
+    near = (dy <= 1.01 * lsb) & (dx <= 1.01 * lsb)
+    # a sample whose projected location sits within float noise of a level edge may take the other
+    # fold (or validity) branch: those are the only ones allowed to move further
+    assert near.double().mean().item() >= 0.9999, near.double().mean().item()
+    assert (got[..., :16] == exp[..., :16]).double().mean().item() >= 0.99
+    da = (a_g - a_e).abs()
+    assert (da[near] <= 2.0 ** -10 * a_e.abs()[near] + 1e-6).all(), da[near].max().item()
+    if masked:
+        assert (a_g[qmask] == 0).all()
+    S = sum(h * w_ for h, w_ in shapes)
+    v = torch.randn(B, S, M, 32, generator=torch.Generator().manual_seed(5)).double().numpy()
+    ss = np.array(shapes, dtype=np.int64)
+    o_g = O.fwd(v, ss, l_g.numpy(), a_g.numpy())
+    o_e = O.fwd(v, ss, l_e.numpy(), a_e.numpy())
+    assert np.abs(o_g - o_e).max() <= 2e-3 and np.abs(o_g - o_e).mean() <= 1e-5, np.abs(o_g - o_e).max()
+
+
+@pytest.mark.parametrize('shapes', [
+    ((100, 167), (50, 84), (25, 42), (13, 21)),    # config 2 (800x1333): level 0 gathered, 1-3 staged
+    ((60, 70), (40, 50), (45, 50), (10, 13)),      # wide level 2: levels 2-3 staged
+    ((25, 40), (15, 20), (8, 10), (4, 5)),         # every level staged whole
+])
+@pytest.mark.parametrize('noise,masked', [(0.5, False), (3.0, True), (25.0, False)])
+def test_encoder_records_kernel_vs_oracle(shapes, noise, masked):
+    """The sampling kernel fed records the ORACLE computed on the host (oracle.prep of the
+    reference preparation -> oracle.sample_records), not any kinet kernel's: its output against
+    the C oracle (cuh:165-237 restated) sampling the decoded records.  Small offsets read the
+    strip's staged rows, noise 25 px leaves them (the far path).  Bound: f16 corner-weight
+    products (2^-10 relative), each level's 16 taps summed as f16 pairs (2^-7 max|value|), one
+    bf16 output rounding."""
+    from kinet_amd import kernels as K
+    from oracle import msda_oracle as O
+    B, M, L, P = 2, 8, 4, 4
+    S = sum(h * w for h, w in shapes)
+    g = torch.Generator().manual_seed(17 + int(noise))
+    value = torch.randn(M, B, S, 32, generator=g).half()
+    offlog = torch.cat([noise * torch.randn(B, S, M * L * P * 2, generator=g), torch.randn(B, S, M * L * P, generator=g)],
+                       -1).double()
+    ref = _encoder_refs(shapes, B).cpu()
+    qmask = (torch.rand(B, S, generator=g) < 0.1) if masked else None
+    fb = K.msda_record_frac_bits(shapes)
+    loc, aw = O.prep(offlog, ref.double(), shapes, qmask, M, L, P)
+    rec = O.sample_records(loc, aw, ref, shapes, fb)
+    order = K.encoder_tile_order(shapes, 'cuda')
+    out = K.msda_encoder_records(value.cuda(), shapes, rec.cuda(), fb, out_dtype=torch.bfloat16,
+                                 query_tile_order=order)
+    out_nat = K.msda_encoder_records(value.cuda(), shapes, rec.cuda(), fb, out_dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_nat)   # tile order / strips change only when a tile runs
+    l_d, a_d = O.decode_records(rec, shapes, fb)
+    v = value.float().permute(1, 2, 0, 3).contiguous().double().numpy()
+    ref_out = torch.from_numpy(O.fwd(v, np.array(shapes, dtype=np.int64), l_d.numpy(), a_d.numpy())).reshape(out.shape)
+    d = (out.float().cpu().double() - ref_out).abs()
+    vmax = value.float().abs().max().item()
+    bound = 2.0 ** -7 * ref_out.abs() + (2.0 ** -7 + 2.0 ** -10) * vmax
+    assert (d <= bound).all(), d.max().item()
+    assert d.mean().item() <= 2e-3, d.mean().item()
+    if masked:
+        assert (out.float().cpu()[qmask] == 0).all()
+
+
+def test_encoder_records_path_matches_offlog_path():
+    """MSDeformAttn.sample on an encoder-sized bf16 call: the records path (default) against the
+    f16 offsets / logits path (MSDA_RECORDS off) -- two quantisations of the same locations
+    (2^-8 pixel fixed point vs f16 offsets), within the encoder kernel's bound."""
+    from kinet_amd import kernels as K
+    from kinet_amd.msda import MSDeformAttn
+    shapes = ((100, 167), (50, 84), (25, 42), (13, 21))
+    B, S = 2, sum(h * w for h, w in shapes)
+    torch.manual_seed(3)
+    attn = MSDeformAttn(256, 4, 8, 4).cuda()
+    with torch.no_grad():
+        attn.sampling_offsets.weight.normal_(0, 0.02)
+        attn.attention_weights.weight.normal_(0, 0.05)
+    src = torch.randn(B, S, 256, device='cuda').bfloat16()
+    pos = torch.randn(B, S, 256, device='cuda').bfloat16()
+    ref = _encoder_refs(shapes, B)
+    ss = torch.tensor(shapes, device='cuda')
+    with torch.no_grad():
+        value = attn.project_value(src)
+        o_rec = attn.sample(src, ref, value, ss, query_add=pos, shapes_host=shapes)
+        K.MSDA_RECORDS[0] = False
+        try:
+            o_off = attn.sample(src, ref, value, ss, query_add=pos, shapes_host=shapes)
+        finally:
+            K.MSDA_RECORDS[0] = True
+    torch.cuda.synchronize()
+    d = (o_rec.float() - o_off.float()).abs()
+    vmax = value.float().abs().max().item()
+    assert (d <= o_off.float().abs() * 2.0 ** -6 + 2.0 ** -6 * vmax).all(), d.max().item()
+    assert d.mean().item() <= 2e-3, d.mean().item()
