@@ -100,7 +100,8 @@ int kinet_conv2d_splitk(const void* X, const void* Wt, void* Y, int batch, int H
  * benchmarks to A/B GEMM kernels in one process).  bit 1: allow the 512-thread
  * 256x256-tile LDS-DMA kernel for large-M problems; bit 2: never use the
  * resident-weight streaming kernel; bit 8 (256): keep K = 512 problems off it (the
- * tiled kernel, as before round 3).  Returns the previous flags.  Per CALLING THREAD: torch
+ * tiled kernel, as before round 3); bit 1024: never the direct 3x3 64 -> 64 channel
+ * convolution (the implicit GEMM instead).  Returns the previous flags.  Per CALLING THREAD: torch
  * runs autograd backward for device tensors on its own engine thread, so flags set here do
  * NOT reach the backward kernels launched through autograd (only forward / direct calls). */
 int kinet_gemm_set_flags(int flags);

@@ -45,10 +45,25 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
+def _includes(path, seen=None):
+    """The quoted #include files of `path`, transitively (the headers a TU can depend on)."""
+    import re
+    seen = set() if seen is None else seen
+    with open(path) as f:
+        for ln in f:
+            m = re.match(r'\s*#\s*include\s+"([^"]+)"', ln)
+            if m:
+                q = os.path.normpath(os.path.join(os.path.dirname(path), m.group(1)))
+                if q not in seen and os.path.exists(q):
+                    seen.add(q)
+                    _includes(q, seen)
+    return seen
+
+
 def _file_key(src):
-    """Hash of one translation unit's inputs: its source + every header + the flags."""
+    """Hash of one translation unit's inputs: its source + the headers it includes + the flags."""
     h = hashlib.sha256(' '.join(FLAGS).encode())
-    for p in [src] + sorted(_headers()):
+    for p in [src] + sorted(_includes(src)):
         with open(p, 'rb') as f:
             h.update(f.read())
     return h.hexdigest()[:16]

@@ -40,7 +40,8 @@ namespace {
 // 8 = resident-weight kernel from M >= 256; 16 = LDS-DMA staging for the 4-wave tiles;
 // 32 = never the dedicated stem convolution (stem.hip); 64 = no full-rounds split of the
 // multi-tap convolutions; 128 = KINET_F32_X3 weight-gradient GEMM splitting at fragment-read time;
-// 256 = no XCD placement of that GEMM's K-slices; 512 = the wave-per-row attention backward
+// 256 = no XCD placement of that GEMM's K-slices; 512 = the wave-per-row attention backward;
+// 1024 = never the direct 3x3 64 -> 64 convolution (conv3x3.hip)
 }  // namespace
 // test / A-B selection knobs (kinet_gemm_set_flags, kinet_gemm_force_tile): per calling thread,
 // never read by default paths except as "0 = automatic"
@@ -593,6 +594,10 @@ int launch(const GemmArgs& a, hipStream_t stream) {
 template <bool CONV>
 int dispatch(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t s) {
     if (!CONV && a.kchunk == 0 && !(kinet_gemm_flags & 4) && launch_rw(a, in_dtype, out_dtype, s)) {
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
+    if (CONV && !(kinet_gemm_flags & 1024) && out_dtype == in_dtype && launch_conv3x3_c64(a, in_dtype, s)) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;
     }

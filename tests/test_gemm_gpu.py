@@ -620,3 +620,39 @@ def test_gemm_tn_f32_x3_vs_f64(K, x3_precision, Kd, M, N):
     torch.cuda.synchronize()
     err = (y.double().cpu() - ref).abs()
     assert (err <= _x3_bound(a.T, b)).all(), err.max().item()
+
+
+@pytest.mark.parametrize('B,H,W', [(2, 200, 334), (3, 37, 45), (1, 8, 32), (1, 5, 7)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_direct_conv3x3_c64_vs_fp32(K, B, H, W, dtype):
+    """The direct 3x3 / stride 1 / pad 1, 64 -> 64 conv (csrc/conv3x3.hip: ResNet layer-1 conv2,
+    weights resident in VGPRs, halo tiles in LDS) against torch fp32 F.conv2d + folded BN +
+    ReLU, at the config-2 layer-1 size and at ragged sizes (partial 8 x 32 tiles, an image
+    smaller than one tile); and against the implicit-GEMM path (flag 1024) on the same inputs
+    (same products, other summation order: within one output rounding)."""
+    from kinet_amd import _native
+    g = torch.Generator().manual_seed(H * W + B)
+    x = torch.randn(B, 64, H, W, generator=g).to(dtype)
+    w = (torch.randn(64, 64, 3, 3, generator=g) * (2.0 / 576) ** 0.5).to(dtype)
+    scale = torch.rand(64, generator=g) + 0.5
+    bias = torch.randn(64, generator=g) * 0.1
+    y_ref = F.relu(F.conv2d(x.float(), w.float(), padding=1) * scale[None, :, None, None] + bias[None, :, None, None])
+    xn = x.permute(0, 2, 3, 1).contiguous().cuda()
+    wp = K.pack_conv_weight(w.cuda(), dtype)
+    y = K.conv2d_nhwc(xn, wp, 1, 1, scale=scale.cuda(), bias=bias.cuda(), relu=True)
+    old = _native.lib().kinet_gemm_set_flags(1024)
+    try:
+        y_gemm = K.conv2d_nhwc(xn, wp, 1, 1, scale=scale.cuda(), bias=bias.cuda(), relu=True)
+    finally:
+        _native.lib().kinet_gemm_set_flags(old)
+    torch.cuda.synchronize()
+    err = (y.permute(0, 3, 1, 2).float().cpu() - y_ref).abs()
+    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    assert (err <= 2 * ulp * y_ref.abs() + 1e-3).all(), err.max().item()
+    d = (y.float() - y_gemm.float()).abs()
+    assert (d <= 2 * ulp * y_gemm.float().abs() + 1e-3).all(), d.max().item()
+    # unscaled, no ReLU: negative outputs pass through
+    y2 = K.conv2d_nhwc(xn, wp, 1, 1)
+    torch.cuda.synchronize()
+    r2 = F.conv2d(x.float(), w.float(), padding=1)
+    assert ((y2.permute(0, 3, 1, 2).float().cpu() - r2).abs() <= 2 * ulp * r2.abs() + 1e-3).all()

@@ -1,0 +1,7 @@
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "records or direct_conv" > gpurun_out/r04c_new.log 2>&1; rc=$?; tail -5 gpurun_out/r04c_new.log; [ $rc -eq 0 ] || exit 99
+timeout -k 10 200 python -u tools/conv_ab.py --iters 20 > gpurun_out/r04c_conv_ab.log 2>&1 || exit 98
+head -12 gpurun_out/r04c_conv_ab.log
+bash tools/gpu_suite.sh r04c
