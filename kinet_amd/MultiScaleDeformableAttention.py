@@ -75,5 +75,12 @@ def ms_deform_attn_backward(value, spatial_shapes, sampling_loc, attn_weight, gr
     _n.call('kinet_msda_backward', _n.ptr(value), _n.ptr(spatial_shapes), _n.ptr(sampling_loc),
             _n.ptr(attn_weight), _n.ptr(grad_output), _n.ptr(grad_value), _n.ptr(grad_loc),
             _n.ptr(grad_attw), _n.ptr(ws), N, S, M, D, L, Lq, P, int(im2col_step),
-            _n.dtype_code(value.dtype), _n.dtype_code(sampling_loc.dtype), _n.stream(value.device))
+            _n.dtype_code(value.dtype), _n.dtype_code(sampling_loc.dtype), _n.stream(value.device),
+            work={'family': 'msda_bwd', 'Lq': Lq, 'S': S,
+                  # the launcher's choice (csrc/msda.hip): encoder calls (Lq == S) sum grad_value
+                  # rows on chip, the others scatter per corner
+                  'kernel': 'msda_bwd_list_kernel' if Lq == S else 'msda_bwd_kernel',
+                  # SURVEY 8(d) B_bwd: value + grad_out + loc/attw + f32 grad_value + grad loc/attw
+                  'bytes': (N * S * M * D * value.element_size() + N * Lq * M * D * grad_output.element_size()
+                            + 12 * N * Lq * M * L * P + 4 * N * S * M * D + 12 * N * Lq * M * L * P)})
     return [grad_value, grad_loc, grad_attw]

@@ -117,6 +117,45 @@ def setup_ddp(model, device):
                                                      find_unused_parameters=True)
 
 
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 (the KINET_F32_X3 products run on the bf16 MFMA)
+
+
+def train_rooflines(trace):
+    """Per-family rooflines of one traced training step: the MSDA backward launches against HBM
+    (SURVEY 8(d) B_bwd per call), split encoder (list kernel) / decoder, and every GEMM / conv /
+    weight-gradient launch against the dense MFMA peak."""
+    out = {}
+    bwd = [(w, s.elapsed_time(e)) for name, w, s, e in trace if w.get('family') == 'msda_bwd']
+    if bwd:
+        def roof(items, label):
+            ms = sum(t for _, t in items)
+            by = sum(w['bytes'] for w, _ in items)
+            ach = by / (ms * 1e-3) / 1e9
+            return {'bound': 'hbm', 'kernel': label, 'achieved': ach, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                    'frac': ach / HBM_PEAK_GBS, 'algorithmic_bytes_per_launch': by / len(items),
+                    'avg_launch_ms': ms / len(items), 'launches_per_step': len(items),
+                    'bytes_basis': 'SURVEY 8(d) B_bwd: value + grad_out + loc/attw + f32 grad_value + grad loc/attw'}
+        enc = [x for x in bwd if x[0]['kernel'] == 'msda_bwd_list_kernel']
+        dec = [x for x in bwd if x[0]['kernel'] != 'msda_bwd_list_kernel']
+        r = roof(enc or dec, 'msda_bwd_list_kernel (encoder calls, Lq = S)' if enc else 'msda_bwd_kernel')
+        if enc and dec:
+            r['decoder_kernel'] = roof(dec, 'msda_bwd_kernel (decoder calls)')
+        out['msda_bwd'] = r
+    gr = [(w, s.elapsed_time(e)) for name, w, s, e in trace
+          if w.get('flops') and w.get('family') in ('grad', 'gemm', 'conv')]
+    if gr:
+        ms = sum(t for _, t in gr)
+        fl = sum(w['flops'] for w, _ in gr)
+        ach = fl / (ms * 1e-3) / 1e12
+        out['grad'] = {'bound': 'mfma', 'kernel': 'every GEMM / conv / weight-gradient launch of the step',
+                       'achieved': ach, 'peak': MFMA_BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                       'frac': ach / MFMA_BF16_PEAK_TFLOPS, 'launches_per_step': len(gr), 'device_ms_per_step': ms,
+                       'note': 'f32 operands as three bf16 MFMA passes (KINET_F32_X3): algorithmic flops counted '
+                               'once, so the MFMA pipe runs 3x the reported rate'}
+    return out
+
+
 def benchmark_train(steps=10, warmup=2, batch=2, height=800, width=1333, prev_dtype=torch.bfloat16, device=None,
                     dropout=None, matmul_precision='high'):
     """Config-4 training throughput (BASELINE.json configs[3], cfgs/train_mot17.yaml: `mot17
@@ -194,6 +233,13 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
     torch.cuda.synchronize()
     glue = dict(TR.GLUE)
     TR.GLUE['on'] = False
+    # backward rooflines: HIP events around every kinet launch of one more step (one stream)
+    from kinet_amd import _native
+    _native.trace_begin()
+    step()
+    trace = _native.trace_end()
+    torch.cuda.synchronize()
+    rooflines = train_rooflines(trace)
     frames = batch * steps * world
     from kinet_amd.models.training import _has_dropout
     # with dropout > 0 the previous frame runs op-for-op in f32 (train-mode dropout, as the
@@ -218,6 +264,7 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
                           'host_only_ms_per_step': (glue['glue_s'] - glue['sync_wait_s']) / 2 * 1e3,
                           'device_to_host_syncs_per_step': glue['syncs'] / 2,
                           'what': 'matcher (prev frame + criterion, all output sets) + track-query sampler'},
+            'msda_bwd_roofline': rooflines.get('msda_bwd'), 'dense_grad_roofline': rooflines.get('grad'),
             'dtype': 'f32', 'data': 'synthetic frame pairs, 10-30 boxes, random-init weights',
             'config': {'workload': 'config4 two-pass tracking training step (prev frame no-grad, current frame '
                                    'fwd+bwd, AdamW)', 'batch_per_gpu': batch, 'hidden_dim': args.hidden_dim,
