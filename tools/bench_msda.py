@@ -72,6 +72,9 @@ def main():
     ap.add_argument('--order', action='store_true', help='encoder tile order (kernels.encoder_tile_order)')
     ap.add_argument('--hm', action='store_true',
                     help='encoder kernel on head-major offsets/logits (kinet_msda_encoder_forward)')
+    ap.add_argument('--rec', action='store_true',
+                    help='encoder kernel on sampling records (kinet_msda_encoder_forward_records); the records are '
+                         'made once by kinet_msda_sample_records from an identity-like projection of the offsets')
     a = ap.parse_args()
     value, ss, offlog, ref, (M, L, P) = make_inputs(B=a.batch, noise=a.noise, decoder=a.decoder,
                                                     dtype=torch.float16)
@@ -88,6 +91,25 @@ def main():
         fn = lambda: K.msda_encoder(value, shapes, hm, ref, M, out_dtype=torch.bfloat16,   # noqa: E731
                                     query_tile_order=order)
         kind = 'encoder-hm'
+    if a.rec and not a.decoder:
+        # records of the same offsets / logits: the records GEMM over x = [offsets | logits | 0]
+        # (K = 256) with an identity weight in the (head, level, 12) row grouping
+        B_, Lq_ = offlog.shape[:2]
+        nol = M * L * P * 3
+        x = torch.zeros(B_, Lq_, 256, dtype=torch.float16, device='cuda')
+        x[..., :nol] = offlog
+        rows = []
+        for h in range(M):
+            for l in range(L):
+                base = (h * L + l) * P
+                rows += [2 * base + i for i in range(2 * P)] + [M * L * P * 2 + base + i for i in range(P)]
+        w = torch.zeros(nol, 256, dtype=torch.float16, device='cuda')
+        w[torch.arange(nol), torch.tensor(rows)] = 1.0
+        shapes = [tuple(s) for s in ss.tolist()]
+        rec, fb = K.msda_sample_records(x, w, torch.zeros(nol, device='cuda'), M, ref, shapes)
+        fn = lambda: K.msda_encoder_records(value, shapes, rec, fb, out_dtype=torch.bfloat16,   # noqa: E731
+                                            query_tile_order=order)
+        kind = 'encoder-records'
     ms = time_call(fn, a.iters)
     B, Lq = offlog.shape[:2]
     S = value.shape[2]
