@@ -42,7 +42,8 @@ struct FfnArgs {
     int ldx, ldy, M, F;
     int x_bytes, w_bytes, y_bytes;
     int dbg;   // diagnostic knobs (kinet_ffn_set_debug): 1 = no weight DMA after the prologue
-               // (timing only, results are garbage); 2 = the 4-wave x 32-row tile at D = 256
+               // (timing only, results are garbage); 2 = the 4-wave x 32-row tile at D = 256;
+               // 4 = the 8-wave x 32-row tile (ffn_fused_rt2_kernel)
 };
 
 thread_local int ffn_debug = 0;   // test-only knob (kinet_ffn_set_debug), per calling thread
@@ -376,6 +377,203 @@ __global__ __launch_bounds__(WAVES * 64) void ffn_fused_kernel(const FfnArgs p, 
     }
 }
 
+// 8 waves x 32 rows (two 16-row tiles per wave; kinet_ffn_set_debug bit 2 = 4): every 1-KiB weight
+// fragment read from the ring feeds two MFMAs -- half the LDS reads per MFMA of the 16-row tile,
+// whose 8 waves saturate the LDS read port.  To stay within 256 VGPRs (two waves
+// per SIMD) the tile's x fragments are loaded at the tile start instead of one tile ahead, phase
+// B of a chunk follows its own phase A (no cross-chunk software pipeline) and the ring holds 3
+// chunks (2 in flight + the one being computed).  Same packed weights, same sums in the same
+// order per output element as ffn_fused_kernel (bit-identical results).
+template <typename T, int D>
+__global__ __launch_bounds__(512) void ffn_fused_rt2_kernel(const FfnArgs p, const int ntiles) {
+    constexpr int RT = 2, WAVES = 8;
+    using G = FfnGeo<D>;
+    constexpr int KS = G::KS, NT = G::NT, FR = G::FR;
+    static_assert(FR % WAVES == 0, "whole DMA rounds per chunk");
+    constexpr int FRW = FR / WAVES;
+    constexpr int ROWS = WAVES * 16 * RT;
+    constexpr int NS = 3;
+    constexpr unsigned OOB = 0x80000000u;
+    constexpr int PAR = (FFN_MAX_F + 3 * D) * 4;
+    __shared__ __attribute__((aligned(16))) char lds[PAR + NS * G::CHUNK];
+    float* const pb1 = reinterpret_cast<float*>(lds);
+    float* const pb2 = pb1 + FFN_MAX_F;
+    float* const pg = pb2 + D;
+    float* const pbe = pg + D;
+    char* const ring = lds + PAR;
+
+    const int P = gridDim.x, bx = blockIdx.x;
+    const int cnt = bx < ntiles ? (ntiles - 1 - bx) / P + 1 : 0;
+    if (cnt == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, c16 = lane & 15;
+    const int nch = p.F / 32;
+    const bool ln = p.ln_g != nullptr;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, p.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, (short)0, p.w_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(p.Y, (short)0, p.y_bytes, 0x00020000);
+
+    for (int i = threadIdx.x; i < p.F; i += WAVES * 64) pb1[i] = p.b1[i];
+    for (int i = threadIdx.x; i < D; i += WAVES * 64) {
+        pb2[i] = p.b2[i];
+        pg[i] = ln ? p.ln_g[i] : 1.f;
+        pbe[i] = ln ? p.ln_b[i] : 0.f;
+    }
+    auto dma_chunk = [&](int q, int c) {
+        char* dst = ring + (q % NS) * G::CHUNK;
+        const unsigned src = (unsigned)c * (unsigned)G::CHUNK + (unsigned)lane * 16u;
+#pragma unroll
+        for (int k = 0; k < FRW; ++k) {
+            const int f = k * WAVES + wave;
+            dma16(rw, dst + f * 1024, src + (unsigned)f * 1024u);
+        }
+    };
+    const int total = cnt * nch;
+    __syncthreads();   // parameters in LDS
+    dma_chunk(0, 0);
+    if (total > 1) dma_chunk(1, nch > 1 ? 1 : 0);
+
+    u32x4 xr[RT][KS];
+    f32x4 acc[RT][NT];
+    for (int ti = 0; ti < cnt; ++ti) {
+        const int tile = bx + ti * P;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const int r = tile * ROWS + wave * 16 * RT + 16 * rt + c16;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const unsigned off = r < p.M ? ((unsigned)r * (unsigned)p.ldx + (unsigned)(32 * ks + 8 * g)) * 2u : OOB;
+                xr[rt][ks] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+            }
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[rt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < nch; ++c) {
+            const int q = ti * nch + c;
+            // chunk q landed: younger are at most chunk q+1's DMA (plus, at a tile boundary, the
+            // previous tile's stores and this tile's x loads -- then this waits for those too)
+            if (q + 1 < total) ffn_wait_vmcnt<FRW>();
+            else ffn_wait_vmcnt<0>();
+            ffn_lds_barrier();   // chunk q visible; slot (q+2) % NS (chunk q-1) free
+            if (q + 2 < total) {
+                int cn = c + 2;
+                if (cn >= nch) cn -= nch;
+                if (cn >= nch) cn -= nch;
+                dma_chunk(q + 2, cn);
+            }
+            const char* wb = ring + (q % NS) * G::CHUNK;
+            f32x4 h0[RT], h1[RT];
+            {
+                const f32x4 bb0 = *reinterpret_cast<const f32x4*>(pb1 + c * 32 + 4 * g);
+                const f32x4 bb1 = *reinterpret_cast<const f32x4*>(pb1 + c * 32 + 16 + 4 * g);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) {
+                    h0[rt] = bb0;
+                    h1[rt] = bb1;
+                }
+            }
+            // phase A: H^T chunk (32 hidden x 32 rows) = W1c x^T + b1
+            u32x4 fa0 = *reinterpret_cast<const u32x4*>(wb + lane * 16);
+            u32x4 fa1 = *reinterpret_cast<const u32x4*>(wb + lane * 16 + KS * 1024);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                u32x4 na0 = fa0, na1 = fa1;
+                if (ks + 1 < KS) {
+                    na0 = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (ks + 1) * 1024);
+                    na1 = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (KS + ks + 1) * 1024);
+                }
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) {
+                    Mma<T>::run(h0[rt], fa0, xr[rt][ks]);
+                    Mma<T>::run(h1[rt], fa1, xr[rt][ks]);
+                }
+                fa0 = na0;
+                fa1 = na1;
+            }
+            // ReLU + round: the B operand of phase B (hidden order as kinet_ffn_pack permuted W2)
+            u32x4 hb[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                hb[rt][0] = pack2<T>(fmaxf(h0[rt][0], 0.f), fmaxf(h0[rt][1], 0.f));
+                hb[rt][1] = pack2<T>(fmaxf(h0[rt][2], 0.f), fmaxf(h0[rt][3], 0.f));
+                hb[rt][2] = pack2<T>(fmaxf(h1[rt][0], 0.f), fmaxf(h1[rt][1], 0.f));
+                hb[rt][3] = pack2<T>(fmaxf(h1[rt][2], 0.f), fmaxf(h1[rt][3], 0.f));
+            }
+            // phase B: out^T += W2c H^T, each W2 fragment feeding both row tiles
+            u32x4 fw = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (2 * KS) * 1024);
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                u32x4 nw = fw;
+                if (nt + 1 < NT) nw = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (2 * KS + nt + 1) * 1024);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) Mma<T>::run(acc[rt][nt], fw, hb[rt]);
+                fw = nw;
+            }
+        }
+        // ---- tile epilogue (as ffn_fused_kernel): + b2 + residual x, LayerNorm, 16-byte stores ----
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const int r = tile * ROWS + wave * 16 * RT + 16 * rt + c16;
+            float s = 0.f;
+#pragma unroll
+            for (int kp = 0; kp < KS; ++kp) {
+                float x8[8];
+                unpack4<T>(u32x2{xr[rt][kp][0], xr[rt][kp][1]}, x8);
+                unpack4<T>(u32x2{xr[rt][kp][2], xr[rt][kp][3]}, x8 + 4);
+                const f32x4 b2a = *reinterpret_cast<const f32x4*>(pb2 + 32 * kp + 8 * g);
+                const f32x4 b2b = *reinterpret_cast<const f32x4*>(pb2 + 32 * kp + 8 * g + 4);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float v0 = acc[rt][2 * kp][i] + b2a[i] + x8[i];
+                    const float v1 = acc[rt][2 * kp + 1][i] + b2b[i] + x8[4 + i];
+                    acc[rt][2 * kp][i] = v0;
+                    acc[rt][2 * kp + 1][i] = v1;
+                    s += v0 + v1;
+                }
+            }
+            float mean = 0.f, rstd = 1.f;
+            if (ln) {
+                s += __shfl_xor(s, 16);
+                s += __shfl_xor(s, 32);
+                mean = s * (1.f / (float)D);
+                float qv = 0.f;
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float d = acc[rt][nt][i] - mean;
+                        qv += d * d;
+                    }
+                qv += __shfl_xor(qv, 16);
+                qv += __shfl_xor(qv, 32);
+                rstd = rsqrtf(qv * (1.f / (float)D) + p.eps);
+            }
+#pragma unroll
+            for (int kp = 0; kp < KS; ++kp) {
+                const int n0 = 32 * kp + 8 * g;
+                float o[8];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    o[i] = acc[rt][2 * kp][i];
+                    o[4 + i] = acc[rt][2 * kp + 1][i];
+                }
+                if (ln) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[e] = (o[e] - mean) * rstd * pg[n0 + e] + pbe[n0 + e];
+                }
+                u32x4 w;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) w[e] = pack2<T>(o[2 * e], o[2 * e + 1]);
+                const unsigned off = r < p.M ? ((unsigned)r * (unsigned)p.ldy + (unsigned)n0) * 2u : OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), ry, off, 0, 0);
+            }
+        }
+    }
+}
+
 // packed[c][f][lane][j] (see include/kinet_ffn.h): f < 2KS -> W1 fragment (h-tile f / KS,
 // k-step f % KS); else W2 fragment of output tile f - 2KS with the hidden index permuted to
 // the phase-A accumulator order.
@@ -412,6 +610,11 @@ int launch_ffn(const FfnArgs& a, hipStream_t s) {
     if (a.M >= 16384) {
         const int nt = (a.M + 127) / 128;
         if constexpr (FfnGeo<D>::FR % 8 == 0) {
+            if (a.dbg & 4) {   // A/B knob: 8 waves x 32 rows (ffn_fused_rt2_kernel)
+                const int n4 = (a.M + 255) / 256;
+                hipLaunchKernelGGL((ffn_fused_rt2_kernel<T, D>), dim3(n4 < 256 ? n4 : 256), dim3(512), 0, s, a, n4);
+                return KINET_OK;
+            }
             if (a.dbg & 2) {   // A/B knob: 4 waves x 32 rows (half the LDS weight reads per MFMA)
                 const int n2 = (a.M + 127) / 128;
                 hipLaunchKernelGGL((ffn_fused_kernel<T, D, 2, 4>), dim3(n2 < 256 ? n2 : 256), dim3(256), 0, s, a, n2);

@@ -656,3 +656,25 @@ def test_direct_conv3x3_c64_vs_fp32(K, B, H, W, dtype):
     torch.cuda.synchronize()
     r2 = F.conv2d(x.float(), w.float(), padding=1)
     assert ((y2.permute(0, 3, 1, 2).float().cpu() - r2).abs() <= 2 * ulp * r2.abs() + 1e-3).all()
+
+
+@pytest.mark.parametrize('M', [16384, 40007, 355568])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_ffn_fused_tile_variants_bit_identical(K, M, dtype):
+    """The fused FFN's tile variants (kinet_ffn_set_debug: 0 = 8 waves x 16 rows, 2 = 4 waves x
+    32 rows, 4 = 8 waves x 32 rows without the cross-chunk pipeline) sum every output element
+    in the same order: bit-identical outputs, incl. a ragged last tile."""
+    from kinet_amd import _native
+    g = torch.Generator().manual_seed(M)
+    lin1, lin2, norm = torch.nn.Linear(256, 1024).cuda(), torch.nn.Linear(1024, 256).cuda(), torch.nn.LayerNorm(256).cuda()
+    x = torch.randn(M, 256, generator=g).to(dtype).cuda()
+    outs = []
+    try:
+        for knob in (0, 2, 4):
+            _native.lib().kinet_ffn_set_debug(knob)
+            outs.append(K.ffn_fused(x, lin1, lin2, norm))
+    finally:
+        _native.lib().kinet_ffn_set_debug(0)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

@@ -3,9 +3,11 @@
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "records or direct_conv" > gpurun_out/r04c_new.log 2>&1; rc=$?; tail -5 gpurun_out/r04c_new.log; [ $rc -eq 0 ] || exit 99
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "records or direct_conv or tile_variants" > gpurun_out/r04c_new.log 2>&1; rc=$?; tail -5 gpurun_out/r04c_new.log; [ $rc -eq 0 ] || exit 99
 timeout -k 10 200 python -u tools/rec_ab.py > gpurun_out/r04c_rec_ab.log 2>&1 || exit 97
 cat gpurun_out/r04c_rec_ab.log
 timeout -k 10 200 python -u tools/conv_ab.py --iters 20 > gpurun_out/r04c_conv_ab.log 2>&1 || exit 98
 head -12 gpurun_out/r04c_conv_ab.log
+timeout -k 10 120 python -u tools/ffn_probe.py --rows 355568 --iters 10 > gpurun_out/r04c_ffn_probe.log 2>&1 || exit 96
+cat gpurun_out/r04c_ffn_probe.log
 bash tools/gpu_suite.sh r04c
