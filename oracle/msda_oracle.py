@@ -196,21 +196,22 @@ def sample_records(loc, attw, ref, shapes, fb):
     word = (hl.long() << (16 + fb)) | (qh.long() << 16) | (wl.long() << fb) | qw.long()   # (B, Lq, M, L, P)
     word = word.to(torch.int64) & 0xffffffff
     locw = torch.where(word >= 2 ** 31, word - 2 ** 32, word).to(torch.int32)
-    a16 = a.to(torch.float16).view(torch.int16).to(torch.int32) & 0xffff                      # (B, Lq, M, L, P)
-    aw_words = a16[..., 0::2] | (a16[..., 1::2] << 16)                                          # (B, Lq, M, L, 2)
-    rec = torch.cat([locw.reshape(B, Lq, M, L * P), aw_words.reshape(B, Lq, M, L * 2)], -1)   # (B, Lq, M, 24)
+    a16 = (a.to(torch.float16).view(torch.int16).to(torch.int32) & 0xffff).reshape(B, Lq, M, L * P)
+    aw_words = a16[..., 0::2] | (a16[..., 1::2] << 16)                                          # (B, Lq, M, L*P/2)
+    rec = torch.cat([locw.reshape(B, Lq, M, L * P), aw_words], -1)        # (B, Lq, M, 24) for L = P = 4
     return rec.permute(2, 0, 1, 3).contiguous()
 
 
 def decode_records(rec, shapes, fb):
-    """records (M, B, Lq, 24) int32 -> (loc (B, Lq, M, L, P, 2), attw (B, Lq, M, L, P)) float64
+    """records (M, B, Lq, 1.5 L P) int32 (24 for L = P = 4) -> (loc (B, Lq, M, L, P, 2), attw (B, Lq, M, L, P)) float64
     whose reference sampling (cuh:165-237, `fwd`) is exactly what a record asks for: the corner
     (hl, wl) + fractions become the location ((wl + lw + 0.5) / W, (hl + lh + 0.5) / H)."""
     rec = rec.long() & 0xffffffff
-    M, B, Lq, _ = rec.shape
-    L, P = len(shapes), 4
+    M, B, Lq, n = rec.shape
+    L = len(shapes)
+    P = (2 * n) // (3 * L)          # n = L*P locations + L*P/2 weight words
     locw = rec[..., :L * P].reshape(M, B, Lq, L, P)
-    aww = rec[..., L * P:].reshape(M, B, Lq, L, 2)
+    aww = rec[..., L * P:]
     hl = locw >> (16 + fb)
     qh = (locw >> 16) & ((1 << fb) - 1)
     wl = (locw >> fb) & ((1 << (16 - fb)) - 1)
@@ -222,6 +223,6 @@ def decode_records(rec, shapes, fb):
     x = (wl.double() + qw.double() / s + 0.5) / W
     lo = (aww & 0xffff).to(torch.int16)
     hi = ((aww >> 16) & 0xffff).to(torch.int16)
-    a = torch.stack([lo, hi], -1).reshape(M, B, Lq, L, P).view(torch.float16).double()
+    a = torch.stack([lo, hi], -1).reshape(M, B, Lq, L, P).view(torch.float16).double()   # pairs of (l, p)
     loc = torch.stack([x, y], -1).permute(1, 2, 0, 3, 4, 5).contiguous()
     return loc, a.permute(1, 2, 0, 3, 4).contiguous()

@@ -60,3 +60,59 @@ def test_torch_core_restatement_matches_reference(golden_dir, name):
                                    torch.from_numpy(d['loc']), torch.from_numpy(d['attw']))
     atol, rtol = _tol(d)
     np.testing.assert_allclose(out.numpy(), d['out'], atol=atol, rtol=rtol)
+
+
+@pytest.mark.parametrize('name', ['msda_kat_f64.npz', 'msda_mid_d32.npz', 'msda_mid_d36.npz'])
+def test_sampling_records_encode_the_reference_sampling(golden_dir, name):
+    """The encoder's sampling records (oracle.sample_records, the encoding kinet_msda_sample_records
+    writes) on the reference's own fixture locations / weights: sampled through the C oracle,
+    the decoded records reproduce the reference output within the 2^-fb-pixel fixed point and f16
+    weights -- including the samples whose footprints leave the level (folded corners) and the
+    samples outside it (weight 0)."""
+    d = _load(golden_dir, name)
+    shapes = [tuple(int(v) for v in s) for s in d['shapes']]
+    loc = torch.from_numpy(d['loc']).double()
+    attw = torch.from_numpy(d['attw']).double()
+    N, Lq, M, L, P, _ = loc.shape
+    # the query's own pixel (where an outside sample points) from a reference point inside the image
+    ref = torch.full((N, Lq, L, 2), 0.5, dtype=torch.float64)
+    fb = 16 - max(1, (max(max(h, w) for h, w in shapes) - 1).bit_length())
+    fb = min(fb, 10)
+    rec = msda_oracle.sample_records(loc, attw, ref, shapes, fb)
+    assert rec.shape == (M, N, Lq, L * P * 3 // 2) and rec.dtype == torch.int32
+    l2, a2 = msda_oracle.decode_records(rec, shapes, fb)
+    out = msda_oracle.fwd(d['value'].astype(np.float64), d['shapes'], l2.numpy(), a2.numpy())
+    vmax = np.abs(d['value']).max()
+    # per sample: |weight| * (2 corners x 2^-(fb+1) pixel + f16 rounding); summed over L*P samples
+    bound = (attw.abs().sum((-1, -2)).max().item()) * vmax * (2.0 ** -fb + 2.0 ** -10) * 2
+    err = np.abs(out - d['out'].astype(np.float64)).max()
+    assert err <= bound, (err, bound)
+    # what every record asks for exists in the level: corners (hl, wl) inside, fraction < 1
+    locw = rec[..., :L * P].long() & 0xffffffff
+    hl, wl = locw >> (16 + fb), (locw >> fb) & ((1 << (16 - fb)) - 1)
+    H = torch.tensor([h for h, _ in shapes]).repeat_interleave(P)
+    W = torch.tensor([w for _, w in shapes]).repeat_interleave(P)
+    assert (hl < H).all() and (wl < W).all()
+
+
+def test_sampling_records_fold_edges():
+    """Footprints that leave the level: the record keeps only the in-level row / column with the
+    weight scaled by its bilinear factor -- exactly the reference's zero-padded bilinear
+    (cuh:227-233) at the top, bottom, left and right edges and outside."""
+    shapes = [(4, 5)]
+    M, L, P = 1, 1, 4
+    # (x, y) normalised: top edge (h = -0.3), bottom (h = H - 0.8), left (w = -0.6), outside
+    pts = torch.tensor([[0.5, (-0.3 + 0.5) / 4], [0.5, (4 - 0.8 + 0.5) / 4], [(-0.6 + 0.5) / 5, 0.5],
+                        [1.3, 0.5]], dtype=torch.float64)
+    loc = pts.view(1, 1, 1, 1, 4, 2)
+    attw = torch.tensor([0.4, 0.3, 0.2, 0.1], dtype=torch.float64).view(1, 1, 1, 1, 4)
+    ref = torch.full((1, 1, 1, 2), 0.5, dtype=torch.float64)
+    rec = msda_oracle.sample_records(loc, attw, ref, shapes, 8)
+    l2, a2 = msda_oracle.decode_records(rec, shapes, 8)
+    value = np.random.default_rng(0).standard_normal((1, 20, 1, 3))
+    ss = np.array(shapes, dtype=np.int64)
+    want = msda_oracle.fwd(value, ss, loc.numpy(), attw.numpy())
+    got = msda_oracle.fwd(value, ss, l2.numpy(), a2.numpy())
+    np.testing.assert_allclose(got, want, atol=3e-3)
+    assert a2[0, 0, 0, 0, 3].item() == 0.0            # outside: weight 0
+    assert abs(a2[0, 0, 0, 0, 0].item() - 0.4 * 0.7) < 1e-3    # top row -1 folded: a * lh
