@@ -78,6 +78,9 @@ def parse():
                     help='diagnostic kernel-selection flags (kinet_gemm_set_flags, csrc/gemm.hip) for A/B runs; '
                          'per calling thread, so the train leg\'s autograd backward (torch\'s engine thread) '
                          'keeps the default kernels')
+    ap.add_argument('--msda-records', type=int, default=1,
+                    help='1: encoder MSDA calls through the sampling records (kinet_msda_sample_records); '
+                         '0: the f16 offsets / logits path (A/B)')
     ap.add_argument('--cpu-stub', action='store_true',
                     help='tests only: run the launch/timing skeleton with a tiny CPU model over gloo')
     a = ap.parse_args()
@@ -543,6 +546,8 @@ def main():
         _native.lib().kinet_gemm_set_flags(a.gemm_flags)
     if a.ffn_knob:
         _native.lib().kinet_ffn_set_debug(a.ffn_knob)
+    from kinet_amd import kernels as K
+    K.MSDA_RECORDS[0] = bool(a.msda_records)
     elapsed, fam, msda, split, dec_touched = run_workload(a, a.workload, dev, world, rank, a.batch, a.streams,
                                                           a.height, a.width, a.dtype, a.steps, a.warmup)
 

@@ -125,65 +125,75 @@ __device__ __forceinline__ void unpack8(const u32x4& u, float* v, bool f16) {
 //   * location = fixed point u32 (hl << (16+fb)) | (round(lh 2^fb) << 16) | (wl << fb) | round(lw 2^fb)
 //     (a rounded-up fraction carries into the integer part), weight = f16.
 // out: 4 location words, then the 4 weights as 2 packed f16 words.
+// max / sum over the 4 lanes lane ^ {0, 16, 32, 48} (the 4 levels of one row): gfx950's row-swap
+// permutes (v_permlane16_swap / v_permlane32_swap) return {own, partner} in some order, so one
+// op per step combines them -- no LDS round trip as __shfl_xor's ds_bpermute takes
+template <bool MAX>
+__device__ __forceinline__ float level_reduce(float x) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = MAX ? fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1])) : __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return MAX ? fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1])) : __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 __device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_lds, bool qmasked, int rl, int l,
                                              const float (&v)[12], uint32_t* out) {
+    // level constants (lane-dependent level: selects, not an indexed kernel-argument load)
     const int Hl = l == 0 ? p.prep_H[0] : l == 1 ? p.prep_H[1] : l == 2 ? p.prep_H[2] : p.prep_H[3];
     const int Wl = l == 0 ? p.prep_W[0] : l == 1 ? p.prep_W[1] : l == 2 ? p.prep_W[2] : p.prep_W[3];
     const float Hf = (float)Hl, Wf = (float)Wl;
+    const float rH = __builtin_amdgcn_rcpf(Hf), rW = __builtin_amdgcn_rcpf(Wf);
     const int fb = p.prep_fb;
     const float fs = (float)(1 << fb);
-    float mx = fmaxf(fmaxf(v[8], v[9]), fmaxf(v[10], v[11]));
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const int fmask = (1 << fb) - 1;
+    const float mx = level_reduce<true>(fmaxf(fmaxf(v[8], v[9]), fmaxf(v[10], v[11])));
     float e[4], es = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         e[q] = __expf(v[8 + q] - mx);
         es += e[q];
     }
-    es += __shfl_xor(es, 16);
-    es += __shfl_xor(es, 32);
-    const float ra = qmasked ? 0.f : 1.f / es;
-    float rx, ry, rw = 0.f, rh = 0.f;
+    es = level_reduce<false>(es);
+    const float ra = qmasked ? 0.f : __builtin_amdgcn_rcpf(es);
+    float rx, ry, sx, sy;   // reference point and the offset scale of each axis
     if (p.prep_refd == 2) {
         const float2 r = *reinterpret_cast<const float2*>(ref_lds + (rl * 4 + l) * 8);
         rx = r.x;
         ry = r.y;
+        sx = rH;   // :77-79 (offsets / spatial_shapes, (H, W) on (x, y))
+        sy = rW;
     } else {
         const float4 r = *reinterpret_cast<const float4*>(ref_lds + (rl * 4 + l) * 16);
         rx = r.x;
         ry = r.y;
-        rw = r.z;
-        rh = r.w;
+        sx = 0.125f * r.z;   // :80-82 (/ n_points * wh * 0.5, n_points = 4)
+        sy = 0.125f * r.w;
     }
     // the query's own pixel of this level: where a sample outside the level points (weight 0)
     const int hr = min(max((int)floorf(ry * Hf), 0), Hl - 1), wr = min(max((int)floorf(rx * Wf), 0), Wl - 1);
+    const uint32_t own = ((uint32_t)hr << (16 + fb)) | ((uint32_t)wr << fb);
     float aw[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        float x, y;
-        if (p.prep_refd == 2) {
-            x = rx + v[2 * q] / Hf;       // :77-79 (offsets / spatial_shapes, (H, W) on (x, y))
-            y = ry + v[2 * q + 1] / Wf;
-        } else {
-            x = rx + v[2 * q] * 0.125f * rw;   // :80-82 (/ n_points * wh * 0.5, n_points = 4)
-            y = ry + v[2 * q + 1] * 0.125f * rh;
-        }
-        float a = e[q] * ra;
-        const float h = y * Hf - 0.5f, w = x * Wf - 0.5f;
+        const float x = fmaf(v[2 * q], sx, rx), y = fmaf(v[2 * q + 1], sy, ry);
+        const float h = fmaf(y, Hf, -0.5f), w = fmaf(x, Wf, -0.5f);
         const bool valid = h > -1.f && w > -1.f && h < Hf && w < Wf;
         const float hfl = floorf(h), wfl = floorf(w);
-        float lh = h - hfl, lw = w - wfl;
-        int hl = (int)hfl, wl = (int)wfl;
-        if (hl < 0) { a *= lh; hl = 0; lh = 0.f; }
-        else if (hl >= Hl - 1) { a *= 1.f - lh; hl = Hl - 1; lh = 0.f; }
-        if (wl < 0) { a *= lw; wl = 0; lw = 0.f; }
-        else if (wl >= Wl - 1) { a *= 1.f - lw; wl = Wl - 1; lw = 0.f; }
-        int qh = (int)(lh * fs + 0.5f), qw = (int)(lw * fs + 0.5f);
-        if (qh >= (1 << fb)) { qh = 0; ++hl; }
-        if (qw >= (1 << fb)) { qw = 0; ++wl; }
-        if (!valid) { a = 0.f; hl = hr; wl = wr; qh = qw = 0; }
-        out[q] = ((uint32_t)hl << (16 + fb)) | ((uint32_t)qh << 16) | ((uint32_t)wl << fb) | (uint32_t)qw;
+        const float lh = h - hfl, lw = w - wfl;
+        const int hl = (int)hfl, wl = (int)wfl;
+        // out-of-level corner rows / columns folded into the weight, branch-free
+        const bool top = hl < 0, bot = hl >= Hl - 1, lef = wl < 0, rig = wl >= Wl - 1;
+        const float fh = top ? lh : (bot ? 1.f - lh : 1.f);
+        const float fw = lef ? lw : (rig ? 1.f - lw : 1.f);
+        const float a = valid ? e[q] * ra * fh * fw : 0.f;
+        // fixed-point fraction (zero on a folded axis); a rounded-up fraction carries into the corner
+        int qh = (top || bot) ? 0 : (int)fmaf(lh, fs, 0.5f);
+        int qw = (lef || rig) ? 0 : (int)fmaf(lw, fs, 0.5f);
+        const int hc = min(max(hl, 0), Hl - 1) + (qh >> fb), wc = min(max(wl, 0), Wl - 1) + (qw >> fb);
+        qh &= fmask;
+        qw &= fmask;
+        const uint32_t word = ((uint32_t)hc << (16 + fb)) | ((uint32_t)qh << 16) | ((uint32_t)wc << fb) | (uint32_t)qw;
+        out[q] = valid ? word : own;
         aw[q] = a;
     }
     out[4] = (uint32_t)__builtin_bit_cast(uint16_t, (f16_t)aw[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, (f16_t)aw[1]) << 16);
