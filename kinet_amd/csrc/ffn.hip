@@ -43,7 +43,7 @@ struct FfnArgs {
     int x_bytes, w_bytes, y_bytes;
     int dbg;   // diagnostic knobs (kinet_ffn_set_debug): 1 = no weight DMA after the prologue
                // (timing only, results are garbage); 2 = the 4-wave x 32-row tile at D = 256;
-               // 4 = the 8-wave x 32-row tile (ffn_fused_rt2_kernel)
+               // 8 = the 8-wave x 16-row tile (default: 8 waves x 32 rows, ffn_fused_rt2_kernel)
 };
 
 thread_local int ffn_debug = 0;   // test-only knob (kinet_ffn_set_debug), per calling thread
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(WAVES * 64) void ffn_fused_kernel(const FfnArgs p, 
     }
 }
 
-// 8 waves x 32 rows (two 16-row tiles per wave; kinet_ffn_set_debug bit 2 = 4): every 1-KiB weight
+// 8 waves x 32 rows (two 16-row tiles per wave; the default at D = 256): every 1-KiB weight
 // fragment read from the ring feeds two MFMAs -- half the LDS reads per MFMA of the 16-row tile,
 // whose 8 waves saturate the LDS read port.  To stay within 256 VGPRs (two waves
 // per SIMD) the tile's x fragments are loaded at the tile start instead of one tile ahead, phase
@@ -610,18 +610,20 @@ int launch_ffn(const FfnArgs& a, hipStream_t s) {
     if (a.M >= 16384) {
         const int nt = (a.M + 127) / 128;
         if constexpr (FfnGeo<D>::FR % 8 == 0) {
-            if (a.dbg & 4) {   // A/B knob: 8 waves x 32 rows (ffn_fused_rt2_kernel)
-                const int n4 = (a.M + 255) / 256;
-                hipLaunchKernelGGL((ffn_fused_rt2_kernel<T, D>), dim3(n4 < 256 ? n4 : 256), dim3(512), 0, s, a, n4);
-                return KINET_OK;
-            }
-            if (a.dbg & 2) {   // A/B knob: 4 waves x 32 rows (half the LDS weight reads per MFMA)
+            if (a.dbg & 2) {   // A/B knob: 4 waves x 32 rows (one wave per SIMD)
                 const int n2 = (a.M + 127) / 128;
                 hipLaunchKernelGGL((ffn_fused_kernel<T, D, 2, 4>), dim3(n2 < 256 ? n2 : 256), dim3(256), 0, s, a, n2);
                 return KINET_OK;
             }
-            // 8 waves x 16 rows: two waves per SIMD hide each other's LDS / VALU latency
-            hipLaunchKernelGGL((ffn_fused_kernel<T, D, 1, 8>), dim3(nt < 256 ? nt : 256), dim3(512), 0, s, a, nt);
+            if (a.dbg & 8) {   // A/B knob: 8 waves x 16 rows (the round-3 default)
+                hipLaunchKernelGGL((ffn_fused_kernel<T, D, 1, 8>), dim3(nt < 256 ? nt : 256), dim3(512), 0, s, a, nt);
+                return KINET_OK;
+            }
+            // 8 waves x 32 rows: each weight fragment feeds two MFMAs and two waves per SIMD hide
+            // each other's latency (config-2 encoder FFN at batch 16: 419 vs 486 us alone, bench
+            // 1267 vs 1219 frames/s, profiles/r04c_ffn_probe.log, r04c_ab_*.json)
+            const int n4 = (a.M + 255) / 256;
+            hipLaunchKernelGGL((ffn_fused_rt2_kernel<T, D>), dim3(n4 < 256 ? n4 : 256), dim3(512), 0, s, a, n4);
         } else {
             hipLaunchKernelGGL((ffn_fused_kernel<T, D, 2, 4>), dim3(nt < 256 ? nt : 256), dim3(256), 0, s, a, nt);
         }

@@ -661,8 +661,8 @@ def test_direct_conv3x3_c64_vs_fp32(K, B, H, W, dtype):
 @pytest.mark.parametrize('M', [16384, 40007, 355568])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
 def test_ffn_fused_tile_variants_bit_identical(K, M, dtype):
-    """The fused FFN's tile variants (kinet_ffn_set_debug: 0 = 8 waves x 16 rows, 2 = 4 waves x
-    32 rows, 4 = 8 waves x 32 rows without the cross-chunk pipeline) sum every output element
+    """The fused FFN's tile variants (kinet_ffn_set_debug: 0 = 8 waves x 32 rows without the
+    cross-chunk pipeline, 2 = 4 waves x 32 rows, 8 = 8 waves x 16 rows) sum every output element
     in the same order: bit-identical outputs, incl. a ragged last tile."""
     from kinet_amd import _native
     g = torch.Generator().manual_seed(M)
@@ -670,7 +670,7 @@ def test_ffn_fused_tile_variants_bit_identical(K, M, dtype):
     x = torch.randn(M, 256, generator=g).to(dtype).cuda()
     outs = []
     try:
-        for knob in (0, 2, 4):
+        for knob in (0, 2, 8):
             _native.lib().kinet_ffn_set_debug(knob)
             outs.append(K.ffn_fused(x, lin1, lin2, norm))
     finally:

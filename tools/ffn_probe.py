@@ -17,7 +17,7 @@ lin1, lin2, norm = torch.nn.Linear(256, 1024).cuda(), torch.nn.Linear(1024, 256)
 x = torch.randn(a.rows, 256, device='cuda', dtype=torch.bfloat16)
 from kinet_amd import _native as N  # noqa: E402
 ref = None
-for knob in (0, 2, 4):
+for knob in (0, 2, 8):
     N.lib().kinet_ffn_set_debug(knob)
     for _ in range(2):
         y = K.ffn_fused(x, lin1, lin2, norm)

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 timeout -k 10 200 python -u tools/rec_ab.py > gpurun_out/r04d_rec_ab.log 2>&1 || exit 97
 cat gpurun_out/r04d_rec_ab.log
 timeout -k 10 400 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -k "records" > gpurun_out/r04d_new.log 2>&1; rc=$?; tail -6 gpurun_out/r04d_new.log; case $rc in 0|1) ;; *) exit 99;; esac
-for v in "rec1:--msda-records 1" "rec0:--msda-records 0" "rec1f4:--msda-records 1 --ffn-knob 4" "rec0f4:--msda-records 0 --ffn-knob 4" "rec1f4g2:--msda-records 1 --ffn-knob 4 --gemm-flags 2" "rec0f4g2:--msda-records 0 --ffn-knob 4 --gemm-flags 2"; do
+for v in "rec1:--msda-records 1" "rec0:--msda-records 0" "rec1g2:--msda-records 1 --gemm-flags 2" "rec0g2:--msda-records 0 --gemm-flags 2" "rec1f8:--msda-records 1 --ffn-knob 8"; do
   n=${v%%:*}; args=${v#*:}
   timeout -k 10 240 python -u bench.py --steps 30 --warmup 5 --no-train --no-config5 --no-cpu-baseline $args > gpurun_out/r04d_ab_$n.log 2>&1 || exit 95
   python - "$n" gpurun_out/r04d_ab_$n.log <<'PY'
