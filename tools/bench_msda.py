@@ -92,21 +92,20 @@ def main():
                                     query_tile_order=order)
         kind = 'encoder-hm'
     if a.rec and not a.decoder:
-        # records of the same offsets / logits: the records GEMM over x = [offsets | logits | 0]
-        # (K = 256) with an identity weight in the (head, level, 12) row grouping
+        # records from an encoder projection with the reference init (sampling_offsets.bias = the
+        # 8-direction grid, ms_deform_attn.py:34-47) plus a small random weight: the sampling
+        # pattern of the bench workload (grid + spread), written by kinet_msda_sample_records
+        from kinet_amd.msda import MSDeformAttn
         B_, Lq_ = offlog.shape[:2]
-        nol = M * L * P * 3
-        x = torch.zeros(B_, Lq_, 256, dtype=torch.float16, device='cuda')
-        x[..., :nol] = offlog
-        rows = []
-        for h in range(M):
-            for l in range(L):
-                base = (h * L + l) * P
-                rows += [2 * base + i for i in range(2 * P)] + [M * L * P * 2 + base + i for i in range(P)]
-        w = torch.zeros(nol, 256, dtype=torch.float16, device='cuda')
-        w[torch.arange(nol), torch.tensor(rows)] = 1.0
-        shapes = [tuple(s) for s in ss.tolist()]
-        rec, fb = K.msda_sample_records(x, w, torch.zeros(nol, device='cuda'), M, ref, shapes)
+        torch.manual_seed(0)
+        attn = MSDeformAttn(256, L, M, P).cuda()
+        with torch.no_grad():
+            attn.sampling_offsets.weight.normal_(0, 0.01 + 0.01 * a.noise)
+            attn.attention_weights.weight.normal_(0, 0.02)
+            w, bias = attn.packed_records_weights()
+            x = torch.randn(B_, Lq_, 256, device='cuda').half()
+            shapes = [tuple(s) for s in ss.tolist()]
+            rec, fb = K.msda_sample_records(x, w, bias, M, ref, shapes)
         fn = lambda: K.msda_encoder_records(value, shapes, rec, fb, out_dtype=torch.bfloat16,   # noqa: E731
                                             query_tile_order=order)
         kind = 'encoder-records'
