@@ -43,7 +43,8 @@ struct FfnArgs {
     int x_bytes, w_bytes, y_bytes;
     int dbg;   // diagnostic knobs (kinet_ffn_set_debug): 1 = no weight DMA after the prologue
                // (timing only, results are garbage); 2 = the 4-wave x 32-row tile at D = 256;
-               // 8 = the 8-wave x 16-row tile (default: 8 waves x 32 rows, ffn_fused_rt2_kernel)
+               // 8 = the 8-wave x 16-row tile (default: 8 waves x 32 rows, ffn_fused_rt2_kernel);
+               // 16 = kinet_bottleneck_pair at D = 64 on the LDS-ring kernel (bneck_pair_kernel)
 };
 
 thread_local int ffn_debug = 0;   // test-only knob (kinet_ffn_set_debug), per calling thread
@@ -80,6 +81,18 @@ __device__ __forceinline__ void unpack4(u32x2 u, float* v) {
         v[3] = (float)__builtin_bit_cast(f16_t, (uint16_t)(u[1] >> 16));
     }
 }
+
+// 16-byte pieces of an accumulator chunk row: lane group g holds hidden 4g..4g+3 (a, 2 packed
+// words) and 16+4g..16+4g+3 (b).  One v_permlane16_swap per word exchanges between lane groups
+// g and g^1 so that even g hold hidden 4g..4g+7 and odd g hold 4g+12..4g+19 (contiguous 8
+// each: a row's 64 bytes in four 16-byte lanes); chunk_piece_off is that piece's first hidden
+// index.  The swap is its own inverse (residual loads take the same route back).
+__device__ __forceinline__ u32x4 chunk_swap(u32x2 a, u32x2 b) {
+    const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+    return u32x4{s0[0], s1[0], s0[1], s1[1]};
+}
+__device__ __forceinline__ int chunk_piece_off(int g) { return (g & 1) ? 4 * g + 12 : 4 * g; }
 
 template <int N>
 __device__ __forceinline__ void ffn_wait_vmcnt() {
@@ -574,9 +587,388 @@ __global__ __launch_bounds__(512) void ffn_fused_rt2_kernel(const FfnArgs p, con
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// ResNet bottleneck pair: block i's conv3 (1x1, D -> F = 4D, + FrozenBN + residual + ReLU) and
+// block i+1's conv1 (1x1, F -> D, + FrozenBN + ReLU) in one launch (torchvision Bottleneck as
+// instantiated by the reference, backbone.py:94-108).  Same scheme as the FFN: phase A's
+// accumulators (the F-wide block output, chunk by chunk) are phase B's operands, so the block
+// output is written once (it is the next block's residual) and never re-read by the next conv1.
+//  * phase A: H^T(32 x rows) = W3c t2^T + b3 (the BN scales are folded into the packed weight
+//    rows, kinet_bottleneck_pack);  + residual, ReLU, round -> stored to Y (two 8-byte pieces
+//    per lane and row tile) and used as the B operand of phase B;
+//  * the residual slice of each chunk (rows of the tile x 32 channels, 64 B per row) travels
+//    with the chunk's weights by LDS-DMA, two chunks ahead, 16-byte pieces XOR-swizzled by
+//    row so the 8-byte reads are conflict-free;
+//  * phase B: out^T(D x rows) += W1c H^T over the F/32 chunks; epilogue relu(out + b1).
+// Weights: kinet_bottleneck_pack(W3 (F, D), W1 (D, F), s3, s1) -- the FFN fragment layout with
+// W3 rows scaled by s3 and W1 rows by s1 before rounding.  F == 4D (the bottleneck expansion).
+struct PairArgs {
+    const void* X;   // t2 (M, D), row stride ldx
+    const void* R;   // residual (M, F), dense
+    const void* W;   // packed weights (BN scales folded)
+    const float* b3;
+    const float* b1;
+    void* Y;   // block output (M, F), dense
+    void* T;   // next conv1 output (M, D), dense
+    int ldx, M, F;
+    int x_bytes, r_bytes, w_bytes, y_bytes, t_bytes;
+};
+
+template <typename T, int D, int RT, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void bneck_pair_kernel(const PairArgs p, const int ntiles) {
+    using G = FfnGeo<D>;
+    constexpr int KS = G::KS, NT = G::NT, FR = G::FR;
+    static_assert(FR % WAVES == 0, "whole DMA rounds per chunk");
+    constexpr int FRW = FR / WAVES;             // weight LDS-DMA instructions per wave per chunk
+    constexpr int ROWS = WAVES * 16 * RT;
+    constexpr int RES = ROWS * 64;              // residual slice per chunk: 32 channels x 2 B per row
+    constexpr int RESW = RT;                    // residual LDS-DMA instructions per wave per chunk (1 KiB each)
+    constexpr int SLOT = G::CHUNK + RES;
+    constexpr int NS = 3;
+    constexpr int F4 = 4 * D;
+    constexpr int PAR = (F4 + D) * 4;
+    constexpr unsigned OOB = 0x80000000u;
+    __shared__ __attribute__((aligned(16))) char lds[PAR + NS * SLOT];
+    float* const pb3 = reinterpret_cast<float*>(lds);
+    float* const pb1 = pb3 + F4;
+    char* const ring = lds + PAR;
+
+    const int P = gridDim.x, bx = blockIdx.x;
+    const int cnt = bx < ntiles ? (ntiles - 1 - bx) / P + 1 : 0;
+    if (cnt == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, c16 = lane & 15;
+    const int F = p.F, nch = F / 32;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, p.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)p.R, (short)0, p.r_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, (short)0, p.w_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(p.Y, (short)0, p.y_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt_ = __builtin_amdgcn_make_buffer_rsrc(p.T, (short)0, p.t_bytes, 0x00020000);
+
+    for (int i = threadIdx.x; i < F4; i += WAVES * 64) pb3[i] = p.b3[i];
+    for (int i = threadIdx.x; i < D; i += WAVES * 64) pb1[i] = p.b1[i];
+    // chunk q = (tile bx + (q / nch) * P, hidden chunk q % nch): its weights + residual slice.
+    // Residual piece of lane l in instruction k: row (k*WAVES + wave)*16 + l/4, 16-byte piece
+    // (l & 3) ^ ((row >> 2) & 3) of the row's 64 bytes, landing at LDS unit l (row-major).
+    auto dma_chunk = [&](int q) {
+        const int ti = q / nch, c = q - ti * nch;
+        const int tile = bx + ti * P;
+        char* dst = ring + (q % NS) * SLOT;
+        const unsigned src = (unsigned)c * (unsigned)G::CHUNK + (unsigned)lane * 16u;
+#pragma unroll
+        for (int k = 0; k < FRW; ++k) {
+            const int f = k * WAVES + wave;
+            dma16(rw, dst + f * 1024, src + (unsigned)f * 1024u);
+        }
+#pragma unroll
+        for (int k = 0; k < RESW; ++k) {
+            const int rl = (k * WAVES + wave) * 16 + (lane >> 2);
+            const int r = tile * ROWS + rl;
+            const int piece = (lane & 3) ^ ((rl >> 2) & 3);
+            const unsigned off =
+                r < p.M ? ((unsigned)r * (unsigned)F + (unsigned)(32 * c)) * 2u + (unsigned)piece * 16u : OOB;
+            dma16(rr, dst + G::CHUNK + (k * WAVES + wave) * 1024, off);
+        }
+    };
+    const int total = cnt * nch;
+    __syncthreads();   // parameters in LDS
+    dma_chunk(0);
+    if (total > 1) dma_chunk(1);
+
+    u32x4 xr[RT][KS];
+    f32x4 acc[RT][NT];
+    for (int ti = 0; ti < cnt; ++ti) {
+        const int tile = bx + ti * P;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const int r = tile * ROWS + wave * 16 * RT + 16 * rt + c16;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const unsigned off = r < p.M ? ((unsigned)r * (unsigned)p.ldx + (unsigned)(32 * ks + 8 * g)) * 2u : OOB;
+                xr[rt][ks] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+            }
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[rt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < nch; ++c) {
+            const int q = ti * nch + c;
+            // chunk q landed.  Younger vector-memory ops (DMA(q) was issued in iteration q-2):
+            // chunk q-2's Y stores (RT), chunk q+1's DMA (if any), chunk q-1's Y stores (RT); across
+            // a tile start also T stores and x loads (RT*KS >= RT).  At c == 0 only the DMA is
+            // counted (waits longer, and right after the prologue nothing else is younger but x)
+            if (q + 1 >= total) ffn_wait_vmcnt<0>();
+            else if (c == 0) ffn_wait_vmcnt<FRW + RESW>();
+            else ffn_wait_vmcnt<FRW + RESW + 2 * RT>();
+            ffn_lds_barrier();   // chunk q visible; slot (q+2) % NS (chunk q-1) free
+            if (q + 2 < total) dma_chunk(q + 2);
+            const char* wb = ring + (q % NS) * SLOT;
+            const char* rb = wb + G::CHUNK;
+            f32x4 h0[RT], h1[RT];
+            {
+                const f32x4 ba = *reinterpret_cast<const f32x4*>(pb3 + c * 32 + 4 * g);
+                const f32x4 bb = *reinterpret_cast<const f32x4*>(pb3 + c * 32 + 16 + 4 * g);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) {
+                    h0[rt] = ba;
+                    h1[rt] = bb;
+                }
+            }
+            u32x4 fa0 = *reinterpret_cast<const u32x4*>(wb + lane * 16);
+            u32x4 fa1 = *reinterpret_cast<const u32x4*>(wb + lane * 16 + KS * 1024);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                u32x4 na0 = fa0, na1 = fa1;
+                if (ks + 1 < KS) {
+                    na0 = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (ks + 1) * 1024);
+                    na1 = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (KS + ks + 1) * 1024);
+                }
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) {
+                    Mma<T>::run(h0[rt], fa0, xr[rt][ks]);
+                    Mma<T>::run(h1[rt], fa1, xr[rt][ks]);
+                }
+                fa0 = na0;
+                fa1 = na1;
+            }
+            // + residual, ReLU, round: the block output (stored) and phase B's operand
+            u32x4 hb[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const int rl = wave * 16 * RT + 16 * rt + c16;
+                const int sw = (c16 >> 2) & 3;
+                const u32x2 ra = *reinterpret_cast<const u32x2*>(rb + rl * 64 + (((g >> 1) ^ sw) << 4) + (g & 1) * 8);
+                const u32x2 rb2 = *reinterpret_cast<const u32x2*>(rb + rl * 64 + (((2 + (g >> 1)) ^ sw) << 4) + (g & 1) * 8);
+                float r0[4], r1[4];
+                unpack4<T>(ra, r0);
+                unpack4<T>(rb2, r1);
+                float v0[4], v1[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    v0[j] = fmaxf(h0[rt][j] + r0[j], 0.f);
+                    v1[j] = fmaxf(h1[rt][j] + r1[j], 0.f);
+                }
+                hb[rt][0] = pack2<T>(v0[0], v0[1]);
+                hb[rt][1] = pack2<T>(v0[2], v0[3]);
+                hb[rt][2] = pack2<T>(v1[0], v1[1]);
+                hb[rt][3] = pack2<T>(v1[2], v1[3]);
+                const int r = tile * ROWS + rl;
+                const unsigned yo = ((unsigned)r * (unsigned)F + (unsigned)(32 * c + chunk_piece_off(g))) * 2u;
+                __builtin_amdgcn_raw_buffer_store_b128(chunk_swap(u32x2{hb[rt][0], hb[rt][1]}, u32x2{hb[rt][2], hb[rt][3]}),
+                                                       ry, r < p.M ? yo : OOB, 0, 0);
+            }
+            // phase B: out^T += W1c H^T, each W1 fragment feeding the RT row tiles
+            u32x4 fw = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (2 * KS) * 1024);
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                u32x4 nw = fw;
+                if (nt + 1 < NT) nw = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (2 * KS + nt + 1) * 1024);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) Mma<T>::run(acc[rt][nt], fw, hb[rt]);
+                fw = nw;
+            }
+        }
+        // ---- tile epilogue: relu(out + b1), 16-byte stores of 8 consecutive channels ----
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const int r = tile * ROWS + wave * 16 * RT + 16 * rt + c16;
+#pragma unroll
+            for (int kp = 0; kp < KS; ++kp) {
+                const int n0 = 32 * kp + 8 * g;
+                float o[8];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    o[i] = fmaxf(acc[rt][2 * kp][i] + pb1[n0 + i], 0.f);
+                    o[4 + i] = fmaxf(acc[rt][2 * kp + 1][i] + pb1[n0 + 4 + i], 0.f);
+                }
+                u32x4 w;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) w[e] = pack2<T>(o[2 * e], o[2 * e + 1]);
+                const unsigned off = r < p.M ? ((unsigned)r * (unsigned)D + (unsigned)n0) * 2u : OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rt_, off, 0, 0);
+            }
+        }
+    }
+}
+
+// D = 64 (ResNet layer 1): the whole packed weight stream is 64 KiB, so it is loaded into LDS
+// ONCE per workgroup and every wave then runs on its own -- no ring, no barrier in the loop.
+// The pair is HBM-bound here (per row 128 B in + 512 B residual + 512 B out + 128 B out; 16
+// MFMAs of work per 16 rows and chunk), so what matters is bytes in flight: each wave owns a
+// 16-row tile and holds the tile's whole residual (8 chunks x 2 pieces per lane = 32 VGPRs);
+// as chunk c consumes its residual registers, they are refilled with the NEXT tile's chunk c,
+// so every residual load has a whole tile of work to land under, and the next tile's t2 rows
+// load at the tile start into a second register set.  Residual loads and block-output stores
+// move 16 bytes per lane (chunk_swap: a row's 64 chunk bytes in four lanes).
+template <typename T>
+__global__ __launch_bounds__(512, 2) void bneck64_kernel(const PairArgs p, const int ntiles) {
+    constexpr int D = 64, F = 256, KS = 2, NT = 4, FR = 8, NCH = F / 32, WAVES = 8;
+    constexpr unsigned OOB = 0x80000000u;
+    __shared__ __attribute__((aligned(16))) char wl[NCH * FR * 1024];
+    __shared__ float pb3[F], pb1[D];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, c16 = lane & 15;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, p.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)p.R, (short)0, p.r_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, (short)0, p.w_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(p.Y, (short)0, p.y_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt_ = __builtin_amdgcn_make_buffer_rsrc(p.T, (short)0, p.t_bytes, 0x00020000);
+    for (int i = threadIdx.x; i < F; i += WAVES * 64) pb3[i] = p.b3[i];
+    if (threadIdx.x < D) pb1[threadIdx.x] = p.b1[threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < NCH * FR / WAVES; ++k) {
+        const int f = k * WAVES + wave;
+        dma16(rw, wl + f * 1024, (unsigned)f * 1024u + (unsigned)lane * 16u);
+    }
+    ffn_wait_vmcnt<0>();
+    __syncthreads();
+
+    const int nw = gridDim.x * WAVES;
+    int tile = blockIdx.x * WAVES + wave;
+    if (tile >= ntiles) return;
+    auto row_of = [&](int t) { return t * 16 + c16; };
+    auto load_x = [&](int t, u32x4 (&dst)[KS]) {
+        const int r = row_of(t);
+        const bool ok = t < ntiles && r < p.M;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            dst[ks] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    rx, ok ? ((unsigned)r * (unsigned)p.ldx + (unsigned)(32 * ks + 8 * g)) * 2u : OOB, 0, 0));
+    };
+    const int poff = chunk_piece_off(g);
+    auto res_off = [&](int t, int c) -> unsigned {
+        const int r = row_of(t);
+        return (t < ntiles && r < p.M) ? ((unsigned)r * (unsigned)F + (unsigned)(32 * c + poff)) * 2u : OOB;
+    };
+    u32x4 xr[KS], xn[KS];
+    u32x4 res[NCH];   // 16-byte pieces (chunk_swap order)
+    load_x(tile, xr);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+        res[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, res_off(tile, c), 0, 0));
+    // first tile landed (once per wave): otherwise the compiler's wait for these registers at the
+    // loop head, merged with the back edge, drains every residual load of each later tile there
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+    for (; tile < ntiles; tile += nw) {
+        const int next = tile + nw;
+        load_x(next, xn);
+        f32x4 acc[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int r = row_of(tile);
+        const bool rok = r < p.M;
+        // opaque per tile: keeps the 64 weight-fragment reads in the loop (hoisted, they would
+        // take 256 VGPRs)
+        int woff = lane * 16;
+        asm volatile("" : "+v"(woff));
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const char* wb = wl + c * FR * 1024 + woff;
+            f32x4 h0 = *reinterpret_cast<const f32x4*>(pb3 + c * 32 + 4 * g);
+            f32x4 h1 = *reinterpret_cast<const f32x4*>(pb3 + c * 32 + 16 + 4 * g);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                Mma<T>::run(h0, *reinterpret_cast<const u32x4*>(wb + ks * 1024), xr[ks]);
+                Mma<T>::run(h1, *reinterpret_cast<const u32x4*>(wb + (KS + ks) * 1024), xr[ks]);
+            }
+            const u32x4 rq = chunk_swap(u32x2{res[c][0], res[c][1]}, u32x2{res[c][2], res[c][3]});
+            float r0[4], r1[4];
+            unpack4<T>(u32x2{rq[0], rq[1]}, r0);
+            unpack4<T>(u32x2{rq[2], rq[3]}, r1);
+            u32x4 hb;
+            hb[0] = pack2<T>(fmaxf(h0[0] + r0[0], 0.f), fmaxf(h0[1] + r0[1], 0.f));
+            hb[1] = pack2<T>(fmaxf(h0[2] + r0[2], 0.f), fmaxf(h0[3] + r0[3], 0.f));
+            hb[2] = pack2<T>(fmaxf(h1[0] + r1[0], 0.f), fmaxf(h1[1] + r1[1], 0.f));
+            hb[3] = pack2<T>(fmaxf(h1[2] + r1[2], 0.f), fmaxf(h1[3] + r1[3], 0.f));
+            const unsigned yo = ((unsigned)r * (unsigned)F + (unsigned)(32 * c + poff)) * 2u;
+            __builtin_amdgcn_raw_buffer_store_b128(chunk_swap(u32x2{hb[0], hb[1]}, u32x2{hb[2], hb[3]}), ry,
+                                                   rok ? yo : OOB, 0, 0);
+            // this chunk's residual registers now take the next tile's chunk c
+            res[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, res_off(next, c), 0, 0));
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                Mma<T>::run(acc[nt], *reinterpret_cast<const u32x4*>(wb + (2 * KS + nt) * 1024), hb);
+        }
+#pragma unroll
+        for (int kp = 0; kp < KS; ++kp) {
+            const int n0 = 32 * kp + 8 * g;
+            u32x4 w;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                w[e] = pack2<T>(fmaxf(acc[2 * kp][2 * e] + pb1[n0 + 2 * e], 0.f),
+                                fmaxf(acc[2 * kp][2 * e + 1] + pb1[n0 + 2 * e + 1], 0.f));
+                w[2 + e] = pack2<T>(fmaxf(acc[2 * kp + 1][2 * e] + pb1[n0 + 4 + 2 * e], 0.f),
+                                    fmaxf(acc[2 * kp + 1][2 * e + 1] + pb1[n0 + 4 + 2 * e + 1], 0.f));
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rt_,
+                                                   rok ? ((unsigned)r * (unsigned)D + (unsigned)n0) * 2u : OOB, 0, 0);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) xr[ks] = xn[ks];
+    }
+}
+
+template <typename T, int D, int RT, int WAVES, int WG_PER_CU>
+void launch_pair_cfg(const PairArgs& a, hipStream_t s) {
+    constexpr int ROWS = WAVES * 16 * RT;
+    const int nt = (a.M + ROWS - 1) / ROWS;
+    const int cap = 256 * WG_PER_CU;
+    hipLaunchKernelGGL((bneck_pair_kernel<T, D, RT, WAVES>), dim3(nt < cap ? nt : cap), dim3(WAVES * 64), 0, s, a, nt);
+}
+
+template <typename T>
+int launch_pair(const PairArgs& a, int D, hipStream_t s) {
+    switch (D) {
+        case 64:
+            if (ffn_debug & 16) {   // A/B knob: the LDS-ring pair kernel at D = 64 too
+                launch_pair_cfg<T, 64, 2, 8, 2>(a, s);
+            } else {
+                const int nt = (a.M + 15) / 16, nb = (nt + 7) / 8;
+                hipLaunchKernelGGL((bneck64_kernel<T>), dim3(nb < 512 ? nb : 512), dim3(512), 0, s, a, nt);
+            }
+            break;
+        case 128: launch_pair_cfg<T, 128, 2, 8, 1>(a, s); break;
+        case 256: launch_pair_cfg<T, 256, 2, 8, 1>(a, s); break;
+        default: return KINET_ERR_ARG;
+    }
+    return KINET_OK;
+}
+
 // packed[c][f][lane][j] (see include/kinet_ffn.h): f < 2KS -> W1 fragment (h-tile f / KS,
 // k-step f % KS); else W2 fragment of output tile f - 2KS with the hidden index permuted to
 // the phase-A accumulator order.
+// kinet_bottleneck_pack: ffn_pack_kernel's fragment order from f32 weights, W3 row h scaled by
+// s3[h] and W1 row n by s1[n] (FrozenBN folded) before the one rounding to T
+template <typename T>
+__global__ void bneck_pack_kernel(const float* __restrict__ W3, const float* __restrict__ W1,
+                                  const float* __restrict__ s3, const float* __restrict__ s1, T* __restrict__ out,
+                                  int D, int F) {
+    const int KS = D / 32, NT = D / 16, FR = 2 * KS + NT;
+    const long total = 2L * D * F;
+    for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+        const long per_chunk = (long)FR * 512;
+        const int c = (int)(idx / per_chunk);
+        const int rem = (int)(idx - (long)c * per_chunk);
+        const int f = rem >> 9, e = rem & 511;
+        const int lane = e >> 3, j = e & 7, g = lane >> 4, c16 = lane & 15;
+        float v;
+        if (f < 2 * KS) {
+            const int ht = f / KS, ks = f - ht * KS;
+            const int h = 32 * c + 16 * ht + c16;
+            v = W3[(long)h * D + 32 * ks + 8 * g + j] * s3[h];
+        } else {
+            const int nt = f - 2 * KS;
+            const int h = 32 * c + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
+            const int n = ffn_sigma(nt, c16);
+            v = W1[(long)n * F + h] * s1[n];
+        }
+        out[idx] = Cvt<T>::from(v);
+    }
+}
+
 template <typename T>
 __global__ void ffn_pack_kernel(const T* __restrict__ W1, const T* __restrict__ W2, T* __restrict__ out, int D,
                                 int F) {
@@ -691,6 +1083,51 @@ extern "C" int kinet_ffn_fused(const void* X, int ldx, const void* packed, const
     int rc;
     if (dtype == KINET_BF16) rc = D == 256 ? launch_ffn<bf16_t, 256>(a, s) : launch_ffn<bf16_t, 288>(a, s);
     else rc = D == 256 ? launch_ffn<f16_t, 256>(a, s) : launch_ffn<f16_t, 288>(a, s);
+    if (rc) return rc;
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_bottleneck_pack(const float* W3, const float* W1, const float* s3, const float* s1,
+                                     void* packed, int D, int F, int dtype, kinet_stream_t stream) {
+    KINET_CHECK_ARG(D > 0 && D % 32 == 0 && F > 0 && F % 32 == 0, "bottleneck_pack: need D %% 32 == 0 and F %% 32 == 0 (D=%d F=%d)", D, F);
+    KINET_CHECK_ARG(dtype == KINET_BF16 || dtype == KINET_F16, "bottleneck_pack: dtype must be bf16 or f16");
+    KINET_CHECK_ARG(W3 && W1 && s3 && s1 && packed, "bottleneck_pack: null pointer");
+    const long total = 2L * D * F;
+    const int grid = (int)((total + 255) / 256 < kMaxGridStride ? (total + 255) / 256 : kMaxGridStride);
+    if (dtype == KINET_BF16)
+        hipLaunchKernelGGL(bneck_pack_kernel<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, W3, W1, s3, s1,
+                           (bf16_t*)packed, D, F);
+    else
+        hipLaunchKernelGGL(bneck_pack_kernel<f16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, W3, W1, s3, s1,
+                           (f16_t*)packed, D, F);
+    KINET_LAUNCH_CHECK();
+    return KINET_OK;
+}
+
+extern "C" int kinet_bottleneck_pair(const void* X, int ldx, const void* R, const void* packed, const float* b3,
+                                     const float* b1, void* Y, void* T, int M, int D, int F, int dtype,
+                                     kinet_stream_t stream) {
+    KINET_CHECK_ARG(D == 64 || D == 128 || D == 256, "bottleneck_pair: D must be 64, 128 or 256 (got %d)", D);
+    KINET_CHECK_ARG(F == 4 * D, "bottleneck_pair: F must be 4 * D (got D=%d F=%d)", D, F);
+    KINET_CHECK_ARG(M >= 0 && ldx >= D && ldx % 8 == 0, "bottleneck_pair: bad M / ldx");
+    KINET_CHECK_ARG(dtype == KINET_BF16 || dtype == KINET_F16, "bottleneck_pair: dtype must be bf16 or f16");
+    KINET_CHECK_ARG(b3 && b1, "bottleneck_pair: folded BN biases of both convs are required");
+    KINET_CHECK_ARG(al16(X) && al16(R) && al16(packed) && al16(Y) && al16(T) && al16(b3) && al16(b1),
+                    "bottleneck_pair: tensors and BN biases must be 16-byte aligned");
+    if (M == 0) return KINET_OK;
+    const long long xb = ((long long)(M - 1) * ldx + D) * 2, fb = (long long)M * F * 2;
+    KINET_CHECK_ARG(xb < (1LL << 31) && fb < (1LL << 31), "bottleneck_pair: tensors larger than 2 GiB (split the call)");
+    PairArgs a{};
+    a.X = X; a.R = R; a.W = packed; a.b3 = b3; a.b1 = b1; a.Y = Y; a.T = T;
+    a.ldx = ldx; a.M = M; a.F = F;
+    a.x_bytes = (int)xb;
+    a.r_bytes = (int)fb;
+    a.y_bytes = (int)fb;
+    a.w_bytes = (int)(2LL * D * F * 2);
+    a.t_bytes = (int)((long long)M * D * 2);
+    hipStream_t s = (hipStream_t)stream;
+    const int rc = dtype == KINET_BF16 ? launch_pair<bf16_t>(a, D, s) : launch_pair<f16_t>(a, D, s);
     if (rc) return rc;
     KINET_LAUNCH_CHECK();
     return KINET_OK;

@@ -52,6 +52,14 @@ class FrozenBatchNorm2d(nn.Module):
         return x * scale.reshape(1, -1, 1, 1) + bias.reshape(1, -1, 1, 1)
 
 
+# Block i's conv3 and block i+1's conv1 as one launch (kinet_bottleneck_pair) for the stages
+# whose bottleneck width is in FUSE_PAIR_WIDTHS; False runs every conv on its own (A/B:
+# tools/bneck_ab.py).  Layer 1 (64) only: at 128 / 256 the persistent pair kernel's row tiles
+# leave a partial last round at batch 16 and the two-launch path is faster (profiles/r04h_bneck_ab.log)
+FUSE_BOTTLENECK_PAIRS = True
+FUSE_PAIR_WIDTHS = (64,)
+
+
 def conv_bn(x, conv, bn, relu, residual=None, cin_pad=None):
     """NHWC conv + folded BN (+ residual) (+ ReLU) in one kernel launch."""
     w = K.pack_conv_weight(conv.weight, x.dtype, cin_pad)
@@ -95,6 +103,35 @@ class Bottleneck(nn.Module):
         return A.conv_nhwc(out, self.conv3.weight, None, 1, 0, *self.bn3.folded(), relu=True, residual=identity)
 
 
+def forward_layer_nhwc(layer, x):
+    """One ResNet stage over NHWC x.  With FUSE_BOTTLENECK_PAIRS the chain conv3 (+ residual +
+    ReLU) of block i -> conv1 of block i+1 runs as one kinet_bottleneck_pair launch: the block
+    output is written once (the next block's residual) and not re-read by the next conv1.
+    Same math as Bottleneck.forward_nhwc per block (torchvision Bottleneck, backbone.py:102)."""
+    blocks = list(layer)
+    b0 = blocks[0]
+    if not (FUSE_BOTTLENECK_PAIRS and len(blocks) > 1 and b0.conv3.in_channels in FUSE_PAIR_WIDTHS
+            and K.bottleneck_pair_supported(x.dtype, b0.conv3.weight, blocks[1].conv1.weight)):
+        for blk in blocks:
+            x = blk.forward_nhwc(x)
+        return x
+    t1 = conv_bn(x, b0.conv1, b0.bn1, True)
+    identity = x if b0.downsample is None else conv_bn(x, b0.downsample[0], b0.downsample[1], False)
+    for i, blk in enumerate(blocks):
+        t2 = conv_bn(t1, blk.conv2, blk.bn2, True)
+        nxt = blocks[i + 1] if i + 1 < len(blocks) else None
+        if nxt is not None and t2.numel() * 4 * t2.element_size() < 2 ** 31:   # the kernel's 32-bit offsets
+            s3, b3 = blk.bn3.folded()
+            s1, b1 = nxt.bn1.folded()
+            packed = K.bottleneck_pack(blk.conv3.weight, nxt.conv1.weight, s3, s1, t2.dtype)
+            identity, t1 = K.bottleneck_pair(t2, identity, packed, b3, b1)
+        else:
+            identity = conv_bn(t2, blk.conv3, blk.bn3, True, residual=identity)
+            if nxt is not None:
+                t1 = conv_bn(identity, nxt.conv1, nxt.bn1, True)
+    return identity
+
+
 class ResNetBody(nn.Module):
     """torchvision ResNet up to layer4 (what IntermediateLayerGetter keeps, backbone.py:81)."""
 
@@ -130,8 +167,7 @@ class ResNetBody(nn.Module):
         x = self.forward_nhwc_stem_layer1(img_nchw, dtype)
         outs = [x]
         for layer in (self.layer2, self.layer3, self.layer4):
-            for blk in layer:
-                x = blk.forward_nhwc(x)
+            x = forward_layer_nhwc(layer, x)
             outs.append(x)
         return outs
 
@@ -162,9 +198,7 @@ class ResNetBody(nn.Module):
         x = K.conv2d_nhwc(x, K.pack_stem_weight(c1.weight, dtype, cg), (c1.stride[0], 1), (c1.padding[0], 0),
                           scale=scale, bias=bias, relu=True)
         x = K.maxpool_3x3s2(x)
-        for blk in self.layer1:
-            x = blk.forward_nhwc(x)
-        return x
+        return forward_layer_nhwc(self.layer1, x)
 
     def forward(self, x):
         return self.forward_autograd(x)
