@@ -81,6 +81,9 @@ def parse():
     ap.add_argument('--msda-records', type=int, default=1,
                     help='1: encoder MSDA calls through the sampling records (kinet_msda_sample_records); '
                          '0: the f16 offsets / logits path (A/B)')
+    ap.add_argument('--bneck-pairs', type=int, default=1,
+                    help='1: ResNet stage-1 bottleneck pairs (conv3 -> next conv1) as one launch '
+                         '(kinet_bottleneck_pair); 0: every conv on its own (A/B)')
     ap.add_argument('--cpu-stub', action='store_true',
                     help='tests only: run the launch/timing skeleton with a tiny CPU model over gloo')
     a = ap.parse_args()
@@ -548,6 +551,8 @@ def main():
         _native.lib().kinet_ffn_set_debug(a.ffn_knob)
     from kinet_amd import kernels as K
     K.MSDA_RECORDS[0] = bool(a.msda_records)
+    from kinet_amd.models import backbone as BB
+    BB.FUSE_BOTTLENECK_PAIRS = bool(a.bneck_pairs)
     elapsed, fam, msda, split, dec_touched = run_workload(a, a.workload, dev, world, rank, a.batch, a.streams,
                                                           a.height, a.width, a.dtype, a.steps, a.warmup)
 

@@ -37,20 +37,21 @@ int kinet_ffn_fused(const void* X, int ldx, const void* packed, const float* b1,
                     int M, int D, int F, int dtype, kinet_stream_t stream);
 
 /* ResNet bottleneck pair (torchvision Bottleneck as the reference instantiates it,
- * backbone.py:94-108): block i's conv3 + FrozenBN + residual + ReLU and block i+1's conv1 +
+ * backbone.py:94-108): block i's conv3 + FrozenBN + residual + ReLU and the next block's conv1 +
  * FrozenBN + ReLU, both 1x1 stride 1 over NHWC rows, in ONE launch (phase A = conv3, its
  * rounded output chunk is stored to Y and is phase B's operand; phase B = the next conv1):
- *   Y = relu(X (s3 W3)^T + b3 + R)   (M, F)  -- the block output, the next block's residual
- *   T = relu(Y (s1 W1)^T + b1)       (M, D)  -- the next block's conv1 output
- * kinet_bottleneck_pack: f32 W3 (F, D), W1 (D, F), FrozenBN scales s3 (F), s1 (D) -> the FFN
- * fragment stream (2*D*F elements of dtype) with each weight row scaled before rounding.
- * F = 4 D, D in {64, 128, 256}; X rows of stride ldx; R, Y, T dense rows; b3 (F), b1 (D) f32;
- * dtype KINET_BF16 / KINET_F16. */
+ *   Y = relu(X (s3 W3)^T + b3 + R)   (M, F)   -- the block output, the next block's residual
+ *   T = relu(Y (s1 W1)^T + b1)       (M, DB)  -- the next block's conv1 output
+ * kinet_bottleneck_pack: f32 W3 (F, D), W1 (DB, F), FrozenBN scales s3 (F), s1 (DB) -> the FFN
+ * fragment stream ((D + DB) * F elements of dtype) with each weight row scaled before rounding.
+ * F = 4 D, D in {64, 128, 256}; DB = D (inside a stage) or, at D = 64, DB = 128 (stage 1's last
+ * block -> stage 2's first conv1, which is stride 1 in torchvision's v1.5 Bottleneck); X rows of
+ * stride ldx; R, Y, T dense rows; b3 (F), b1 (DB) f32; dtype KINET_BF16 / KINET_F16. */
 int kinet_bottleneck_pack(const float* W3, const float* W1, const float* s3, const float* s1,
-                          void* packed, int D, int F, int dtype, kinet_stream_t stream);
+                          void* packed, int D, int F, int DB, int dtype, kinet_stream_t stream);
 
 int kinet_bottleneck_pair(const void* X, int ldx, const void* R, const void* packed, const float* b3,
-                          const float* b1, void* Y, void* T, int M, int D, int F, int dtype,
+                          const float* b1, void* Y, void* T, int M, int D, int F, int DB, int dtype,
                           kinet_stream_t stream);
 
 #ifdef __cplusplus

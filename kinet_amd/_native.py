@@ -41,8 +41,8 @@ _SIGS = {
     'kinet_ffn_pack': [P, P, P, I, I, I, P],
     'kinet_ffn_set_debug': [I],
     'kinet_ffn_fused': [P, I, P, P, P, P, P, F, P, I, I, I, I, I, P],
-    'kinet_bottleneck_pack': [P, P, P, P, P, I, I, I, P],
-    'kinet_bottleneck_pair': [P, I, P, P, P, P, P, P, I, I, I, I, P],
+    'kinet_bottleneck_pack': [P, P, P, P, P, I, I, I, I, P],
+    'kinet_bottleneck_pair': [P, I, P, P, P, P, P, P, I, I, I, I, I, P],
     'kinet_layernorm': [P] * 5 + [I, I, F, I, I, P],
     'kinet_groupnorm': [P] * 4 + [I] * 5 + [F, I, P, P],
     'kinet_groupnorm_workspace': [I] * 5,

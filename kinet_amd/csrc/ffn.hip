@@ -802,12 +802,15 @@ __global__ __launch_bounds__(WAVES * 64) void bneck_pair_kernel(const PairArgs p
 // so every residual load has a whole tile of work to land under, and the next tile's t2 rows
 // load at the tile start into a second register set.  Residual loads and block-output stores
 // move 16 bytes per lane (chunk_swap: a row's 64 chunk bytes in four lanes).
-template <typename T>
-__global__ __launch_bounds__(512, 2) void bneck64_kernel(const PairArgs p, const int ntiles) {
-    constexpr int D = 64, F = 256, KS = 2, NT = 4, FR = 8, NCH = F / 32, WAVES = 8;
+// DB = the next conv1's output width: 64 inside stage 1, 128 for the pair that ends stage 1
+// (its last conv3 -> stage 2's first conv1, 256 -> 128 channels at stride 1); then the weights
+// take 96 KiB and one 16-wave workgroup runs per CU.
+template <typename T, int DB, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1024 / (WAVES * 64)) void bneck64_kernel(const PairArgs p, const int ntiles) {
+    constexpr int D = 64, F = 256, KS = 2, NT = DB / 16, KSB = DB / 32, FR = 2 * KS + NT, NCH = F / 32;
     constexpr unsigned OOB = 0x80000000u;
     __shared__ __attribute__((aligned(16))) char wl[NCH * FR * 1024];
-    __shared__ float pb3[F], pb1[D];
+    __shared__ float pb3[F], pb1[DB];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4, c16 = lane & 15;
@@ -817,7 +820,8 @@ __global__ __launch_bounds__(512, 2) void bneck64_kernel(const PairArgs p, const
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(p.Y, (short)0, p.y_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rt_ = __builtin_amdgcn_make_buffer_rsrc(p.T, (short)0, p.t_bytes, 0x00020000);
     for (int i = threadIdx.x; i < F; i += WAVES * 64) pb3[i] = p.b3[i];
-    if (threadIdx.x < D) pb1[threadIdx.x] = p.b1[threadIdx.x];
+    if (threadIdx.x < DB) pb1[threadIdx.x] = p.b1[threadIdx.x];
+    static_assert(NCH * FR % WAVES == 0, "whole DMA rounds");
 #pragma unroll
     for (int k = 0; k < NCH * FR / WAVES; ++k) {
         const int f = k * WAVES + wave;
@@ -893,7 +897,7 @@ __global__ __launch_bounds__(512, 2) void bneck64_kernel(const PairArgs p, const
                 Mma<T>::run(acc[nt], *reinterpret_cast<const u32x4*>(wb + (2 * KS + nt) * 1024), hb);
         }
 #pragma unroll
-        for (int kp = 0; kp < KS; ++kp) {
+        for (int kp = 0; kp < KSB; ++kp) {
             const int n0 = 32 * kp + 8 * g;
             u32x4 w;
 #pragma unroll
@@ -904,7 +908,7 @@ __global__ __launch_bounds__(512, 2) void bneck64_kernel(const PairArgs p, const
                                     fmaxf(acc[2 * kp + 1][2 * e + 1] + pb1[n0 + 4 + 2 * e + 1], 0.f));
             }
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rt_,
-                                                   rok ? ((unsigned)r * (unsigned)D + (unsigned)n0) * 2u : OOB, 0, 0);
+                                                   rok ? ((unsigned)r * (unsigned)DB + (unsigned)n0) * 2u : OOB, 0, 0);
         }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) xr[ks] = xn[ks];
@@ -920,14 +924,20 @@ void launch_pair_cfg(const PairArgs& a, hipStream_t s) {
 }
 
 template <typename T>
-int launch_pair(const PairArgs& a, int D, hipStream_t s) {
+int launch_pair(const PairArgs& a, int D, int DB, hipStream_t s) {
+    if (D == 64 && DB == 128) {
+        const int nt = (a.M + 15) / 16, nb = (nt + 15) / 16;
+        hipLaunchKernelGGL((bneck64_kernel<T, 128, 16>), dim3(nb < 256 ? nb : 256), dim3(1024), 0, s, a, nt);
+        return KINET_OK;
+    }
+    if (DB != D) return KINET_ERR_ARG;
     switch (D) {
         case 64:
             if (ffn_debug & 16) {   // A/B knob: the LDS-ring pair kernel at D = 64 too
                 launch_pair_cfg<T, 64, 2, 8, 2>(a, s);
             } else {
                 const int nt = (a.M + 15) / 16, nb = (nt + 7) / 8;
-                hipLaunchKernelGGL((bneck64_kernel<T>), dim3(nb < 512 ? nb : 512), dim3(512), 0, s, a, nt);
+                hipLaunchKernelGGL((bneck64_kernel<T, 64, 8>), dim3(nb < 512 ? nb : 512), dim3(512), 0, s, a, nt);
             }
             break;
         case 128: launch_pair_cfg<T, 128, 2, 8, 1>(a, s); break;
@@ -945,9 +955,9 @@ int launch_pair(const PairArgs& a, int D, hipStream_t s) {
 template <typename T>
 __global__ void bneck_pack_kernel(const float* __restrict__ W3, const float* __restrict__ W1,
                                   const float* __restrict__ s3, const float* __restrict__ s1, T* __restrict__ out,
-                                  int D, int F) {
-    const int KS = D / 32, NT = D / 16, FR = 2 * KS + NT;
-    const long total = 2L * D * F;
+                                  int D, int F, int DB) {
+    const int KS = D / 32, NT = DB / 16, FR = 2 * KS + NT;
+    const long total = (long)(D + DB) * F;
     for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
         const long per_chunk = (long)FR * 512;
         const int c = (int)(idx / per_chunk);
@@ -1089,27 +1099,29 @@ extern "C" int kinet_ffn_fused(const void* X, int ldx, const void* packed, const
 }
 
 extern "C" int kinet_bottleneck_pack(const float* W3, const float* W1, const float* s3, const float* s1,
-                                     void* packed, int D, int F, int dtype, kinet_stream_t stream) {
-    KINET_CHECK_ARG(D > 0 && D % 32 == 0 && F > 0 && F % 32 == 0, "bottleneck_pack: need D %% 32 == 0 and F %% 32 == 0 (D=%d F=%d)", D, F);
+                                     void* packed, int D, int F, int DB, int dtype, kinet_stream_t stream) {
+    KINET_CHECK_ARG(D > 0 && D % 32 == 0 && F > 0 && F % 32 == 0 && DB > 0 && DB % 32 == 0,
+                    "bottleneck_pack: need D, F, DB multiples of 32 (D=%d F=%d DB=%d)", D, F, DB);
     KINET_CHECK_ARG(dtype == KINET_BF16 || dtype == KINET_F16, "bottleneck_pack: dtype must be bf16 or f16");
     KINET_CHECK_ARG(W3 && W1 && s3 && s1 && packed, "bottleneck_pack: null pointer");
-    const long total = 2L * D * F;
+    const long total = (long)(D + DB) * F;
     const int grid = (int)((total + 255) / 256 < kMaxGridStride ? (total + 255) / 256 : kMaxGridStride);
     if (dtype == KINET_BF16)
         hipLaunchKernelGGL(bneck_pack_kernel<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, W3, W1, s3, s1,
-                           (bf16_t*)packed, D, F);
+                           (bf16_t*)packed, D, F, DB);
     else
         hipLaunchKernelGGL(bneck_pack_kernel<f16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, W3, W1, s3, s1,
-                           (f16_t*)packed, D, F);
+                           (f16_t*)packed, D, F, DB);
     KINET_LAUNCH_CHECK();
     return KINET_OK;
 }
 
 extern "C" int kinet_bottleneck_pair(const void* X, int ldx, const void* R, const void* packed, const float* b3,
-                                     const float* b1, void* Y, void* T, int M, int D, int F, int dtype,
+                                     const float* b1, void* Y, void* T, int M, int D, int F, int DB, int dtype,
                                      kinet_stream_t stream) {
     KINET_CHECK_ARG(D == 64 || D == 128 || D == 256, "bottleneck_pair: D must be 64, 128 or 256 (got %d)", D);
     KINET_CHECK_ARG(F == 4 * D, "bottleneck_pair: F must be 4 * D (got D=%d F=%d)", D, F);
+    KINET_CHECK_ARG(DB == D || (D == 64 && DB == 128), "bottleneck_pair: DB must be D, or 128 at D = 64 (got D=%d DB=%d)", D, DB);
     KINET_CHECK_ARG(M >= 0 && ldx >= D && ldx % 8 == 0, "bottleneck_pair: bad M / ldx");
     KINET_CHECK_ARG(dtype == KINET_BF16 || dtype == KINET_F16, "bottleneck_pair: dtype must be bf16 or f16");
     KINET_CHECK_ARG(b3 && b1, "bottleneck_pair: folded BN biases of both convs are required");
@@ -1124,10 +1136,10 @@ extern "C" int kinet_bottleneck_pair(const void* X, int ldx, const void* R, cons
     a.x_bytes = (int)xb;
     a.r_bytes = (int)fb;
     a.y_bytes = (int)fb;
-    a.w_bytes = (int)(2LL * D * F * 2);
-    a.t_bytes = (int)((long long)M * D * 2);
+    a.w_bytes = (int)((long long)(D + DB) * F * 2);
+    a.t_bytes = (int)((long long)M * DB * 2);
     hipStream_t s = (hipStream_t)stream;
-    const int rc = dtype == KINET_BF16 ? launch_pair<bf16_t>(a, D, s) : launch_pair<f16_t>(a, D, s);
+    const int rc = dtype == KINET_BF16 ? launch_pair<bf16_t>(a, D, DB, s) : launch_pair<f16_t>(a, D, DB, s);
     if (rc) return rc;
     KINET_LAUNCH_CHECK();
     return KINET_OK;

@@ -326,14 +326,14 @@ def conv2d_nhwc(x, w_packed, stride, pad, scale=None, bias=None, relu=False, res
 
 
 def bottleneck_pack(w3, w1, s3, s1, dtype):
-    """kinet_bottleneck_pack of conv3 (F, D, 1, 1) and the next block's conv1 (D, F, 1, 1) with
+    """kinet_bottleneck_pack of conv3 (F, D, 1, 1) and the next block's conv1 (DB, F, 1, 1) with
     their FrozenBN scales folded in, cached per parameter version."""
     def make(a, b, sa, sb):
-        F_, D = a.shape[0], a.shape[1]
+        F_, D, DB = a.shape[0], a.shape[1], b.shape[0]
         a32 = a.detach().reshape(F_, D).float().contiguous()
-        b32 = b.detach().reshape(D, F_).float().contiguous()
-        out = torch.empty(2 * D * F_, dtype=dtype, device=a.device)
-        N.call('kinet_bottleneck_pack', N.ptr(a32), N.ptr(b32), N.ptr(f32(sa)), N.ptr(f32(sb)), N.ptr(out), D, F_,
+        b32 = b.detach().reshape(DB, F_).float().contiguous()
+        out = torch.empty((D + DB) * F_, dtype=dtype, device=a.device)
+        N.call('kinet_bottleneck_pack', N.ptr(a32), N.ptr(b32), N.ptr(f32(sa)), N.ptr(f32(sb)), N.ptr(out), D, F_, DB,
                N.dtype_code(dtype), N.stream(a.device))
         return out
     return cached_multi([w3, w1, s3, s1], ('bneck_pack', dtype), make)
@@ -341,30 +341,32 @@ def bottleneck_pack(w3, w1, s3, s1, dtype):
 
 def bottleneck_pair_supported(dtype, w3, w1):
     """The fused pair covers 16-bit NHWC rows with D = planes in {64, 128, 256}, F = 4 D (conv3
-    weight (F, D, 1, 1), the next conv1's (D, F, 1, 1))."""
-    F_, D = w3.shape[0], w3.shape[1]
+    weight (F, D, 1, 1)) and the next conv1 (DB, F, 1, 1) with DB = D, or DB = 128 at D = 64."""
+    F_, D, DB = w3.shape[0], w3.shape[1], w1.shape[0]
     return (dtype in (torch.bfloat16, torch.float16) and D in (64, 128, 256) and F_ == 4 * D
-            and tuple(w3.shape) == (F_, D, 1, 1) and tuple(w1.shape) == (D, F_, 1, 1))
+            and (DB == D or (D == 64 and DB == 128))
+            and tuple(w3.shape) == (F_, D, 1, 1) and tuple(w1.shape) == (DB, F_, 1, 1))
 
 
 def bottleneck_pair(x, residual, packed, b3, b1):
     """ResNet bottleneck pair (kinet_bottleneck_pair): x = block i's conv2 output (B, H, W, D)
     NHWC, residual (B, H, W, F) -> (y, t): y = relu(conv3(x) * s3 + b3 + residual) (the block
     output, F = 4 D channels), t = relu(conv1'(y) * s1 + b1) (the next block's conv1 output,
-    D channels); the BN scales are in `packed` (bottleneck_pack)."""
+    DB = b1.numel() channels); the BN scales are in `packed` (bottleneck_pack)."""
     N.require_gpu(x)
     B, H, W, D = x.shape
     F_ = 4 * D
     if residual.shape != (B, H, W, F_) or not residual.is_contiguous() or residual.dtype != x.dtype:
         raise RuntimeError('bottleneck_pair: residual must be a contiguous (B, H, W, 4D) tensor of the input dtype')
     M = B * H * W
+    DB = b1.numel()
     y = torch.empty((B, H, W, F_), dtype=x.dtype, device=x.device)
-    t = torch.empty((B, H, W, D), dtype=x.dtype, device=x.device)
+    t = torch.empty((B, H, W, DB), dtype=x.dtype, device=x.device)
     e = x.element_size()
-    work = {'family': 'conv', 'flops': 4.0 * M * D * F_, 'shape': ('bneck', M, D, F_),
-            'bytes': (2 * M * D + 2 * M * F_ + 2 * D * F_) * e}
+    work = {'family': 'conv', 'flops': 2.0 * M * F_ * (D + DB), 'shape': ('bneck', M, D, F_, DB),
+            'bytes': (M * D + 2 * M * F_ + M * DB + (D + DB) * F_) * e}
     N.call('kinet_bottleneck_pair', N.ptr(x), D, N.ptr(residual), N.ptr(packed), N.ptr(f32(b3)), N.ptr(f32(b1)),
-           N.ptr(y), N.ptr(t), M, D, F_, N.dtype_code(x.dtype), N.stream(x.device), work=work)
+           N.ptr(y), N.ptr(t), M, D, F_, DB, N.dtype_code(x.dtype), N.stream(x.device), work=work)
     return y, t
 
 

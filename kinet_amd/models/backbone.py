@@ -103,33 +103,42 @@ class Bottleneck(nn.Module):
         return A.conv_nhwc(out, self.conv3.weight, None, 1, 0, *self.bn3.folded(), relu=True, residual=identity)
 
 
-def forward_layer_nhwc(layer, x):
-    """One ResNet stage over NHWC x.  With FUSE_BOTTLENECK_PAIRS the chain conv3 (+ residual +
-    ReLU) of block i -> conv1 of block i+1 runs as one kinet_bottleneck_pair launch: the block
-    output is written once (the next block's residual) and not re-read by the next conv1.
-    Same math as Bottleneck.forward_nhwc per block (torchvision Bottleneck, backbone.py:102)."""
+def _pair_ok(dtype, blk, nxt):
+    return (FUSE_BOTTLENECK_PAIRS and blk.conv3.in_channels in FUSE_PAIR_WIDTHS
+            and K.bottleneck_pair_supported(dtype, blk.conv3.weight, nxt.conv1.weight))
+
+
+def forward_layer_nhwc(layer, x, t1=None, next_block=None):
+    """One ResNet stage over NHWC x -> (stage output, next_block's conv1 output or None).
+    With FUSE_BOTTLENECK_PAIRS the chain conv3 (+ residual + ReLU) of block i -> conv1 of block
+    i+1 runs as one kinet_bottleneck_pair launch: the block output is written once (the next
+    block's residual) and not re-read by the next conv1.  `next_block` (the next stage's first
+    block) extends the chain across the stage boundary where the pair kernel covers it (stage 1
+    -> 2: its conv1 is stride 1); `t1` = this stage's first conv1 output when the previous stage
+    computed it.  Same math as Bottleneck.forward_nhwc per block (torchvision, backbone.py:102)."""
     blocks = list(layer)
     b0 = blocks[0]
-    if not (FUSE_BOTTLENECK_PAIRS and len(blocks) > 1 and b0.conv3.in_channels in FUSE_PAIR_WIDTHS
-            and K.bottleneck_pair_supported(x.dtype, b0.conv3.weight, blocks[1].conv1.weight)):
-        for blk in blocks:
-            x = blk.forward_nhwc(x)
-        return x
-    t1 = conv_bn(x, b0.conv1, b0.bn1, True)
+    if t1 is None:
+        t1 = conv_bn(x, b0.conv1, b0.bn1, True)
     identity = x if b0.downsample is None else conv_bn(x, b0.downsample[0], b0.downsample[1], False)
+    t_next = None
     for i, blk in enumerate(blocks):
         t2 = conv_bn(t1, blk.conv2, blk.bn2, True)
-        nxt = blocks[i + 1] if i + 1 < len(blocks) else None
-        if nxt is not None and t2.numel() * 4 * t2.element_size() < 2 ** 31:   # the kernel's 32-bit offsets
+        last = i + 1 == len(blocks)
+        nxt = next_block if last else blocks[i + 1]
+        if (nxt is not None and nxt.conv1.stride == (1, 1) and _pair_ok(t2.dtype, blk, nxt)
+                and t2.numel() * 4 * t2.element_size() < 2 ** 31):   # the kernel's 32-bit offsets
             s3, b3 = blk.bn3.folded()
             s1, b1 = nxt.bn1.folded()
             packed = K.bottleneck_pack(blk.conv3.weight, nxt.conv1.weight, s3, s1, t2.dtype)
             identity, t1 = K.bottleneck_pair(t2, identity, packed, b3, b1)
+            if last:
+                t_next = t1
         else:
             identity = conv_bn(t2, blk.conv3, blk.bn3, True, residual=identity)
-            if nxt is not None:
+            if not last:
                 t1 = conv_bn(identity, nxt.conv1, nxt.bn1, True)
-    return identity
+    return identity, t_next
 
 
 class ResNetBody(nn.Module):
@@ -164,10 +173,11 @@ class ResNetBody(nn.Module):
         # stem (torchvision conv1 7x7/2 + FrozenBN + ReLU): the 7 horizontal taps are folded
         # into 24 channels while packing the image, so the conv runs as 7x1 with strides
         # (2, 1): K = 7*24 = 168 instead of 7*7*8 = 392 (kinet_pack_image_kwfold)
-        x = self.forward_nhwc_stem_layer1(img_nchw, dtype)
+        x, t1 = self._stem_stage1(img_nchw, dtype, self.layer2[0])
         outs = [x]
-        for layer in (self.layer2, self.layer3, self.layer4):
-            x = forward_layer_nhwc(layer, x)
+        stages = (self.layer2, self.layer3, self.layer4)
+        for k, layer in enumerate(stages):
+            x, t1 = forward_layer_nhwc(layer, x, t1, stages[k + 1][0] if k + 1 < len(stages) else None)
             outs.append(x)
         return outs
 
@@ -190,6 +200,11 @@ class ResNetBody(nn.Module):
         return OrderedDict((str(i), nhwc_as_nchw(o)) for i, o in enumerate(outs))
 
     def forward_nhwc_stem_layer1(self, img_nchw, dtype):
+        return self._stem_stage1(img_nchw, dtype, None)[0]
+
+    def _stem_stage1(self, img_nchw, dtype, next_block):
+        """stem + layer1 -> (layer1 output, next_block's conv1 output when the last stage-1 pair
+        computed it, else None)."""
         c1 = self.conv1
         kh, kw = c1.kernel_size
         cg = (3 * kw + 7) // 8 * 8
@@ -198,7 +213,7 @@ class ResNetBody(nn.Module):
         x = K.conv2d_nhwc(x, K.pack_stem_weight(c1.weight, dtype, cg), (c1.stride[0], 1), (c1.padding[0], 0),
                           scale=scale, bias=bias, relu=True)
         x = K.maxpool_3x3s2(x)
-        return forward_layer_nhwc(self.layer1, x)
+        return forward_layer_nhwc(self.layer1, x, None, next_block)
 
     def forward(self, x):
         return self.forward_autograd(x)

@@ -34,9 +34,9 @@ def main():
     B, dt = a.batch, torch.bfloat16
     torch.manual_seed(0)
     body = BB.ResNetBody([3, 4, 6, 3]).cuda().eval()
-    for D, (H, W) in ((64, (200, 334)), (128, (100, 167)), (256, (50, 84))):
+    for D, DB, (H, W) in ((64, 64, (200, 334)), (64, 128, (200, 334)), (128, 128, (100, 167)), (256, 256, (50, 84))):
         F_ = 4 * D
-        blk, nxt = BB.Bottleneck(F_, D).cuda(), BB.Bottleneck(F_, D).cuda()
+        blk, nxt = BB.Bottleneck(F_, D).cuda(), BB.Bottleneck(F_, DB).cuda()
         x = torch.relu(torch.randn(B, H, W, D, device='cuda')).to(dt)
         res = torch.randn(B, H, W, F_, device='cuda').to(dt)
         s3, b3 = blk.bn3.folded()
@@ -53,8 +53,8 @@ def main():
         for r in range(a.reps):
             tf, tp = time_call(fused, a.iters) * 1e3, time_call(plain, a.iters) * 1e3
             M = B * H * W
-            gb = (2 * M * D + 2 * M * F_) * 2 / 1e9
-            print(f'D={D} M={M}: pair {tf:.1f} us ({gb / tf * 1e3:.2f} TB/s algorithmic) | conv3 + conv1 {tp:.1f} us '
+            gb = (M * D + M * DB + 2 * M * F_) * 2 / 1e9
+            print(f'D={D} DB={DB} M={M}: pair {tf:.1f} us ({gb / tf * 1e3:.2f} TB/s algorithmic) | conv3 + conv1 {tp:.1f} us '
                   f'| saved {tp - tf:.1f} us', flush=True)
     img = torch.randn(B, 3, 800, 1333, device='cuda')
 
