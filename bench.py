@@ -84,6 +84,9 @@ def parse():
     ap.add_argument('--bneck-pairs', type=int, default=1,
                     help='1: ResNet stage-1 bottleneck pairs (conv3 -> next conv1) as one launch '
                          '(kinet_bottleneck_pair); 0: every conv on its own (A/B)')
+    ap.add_argument('--stem-image', type=int, default=1,
+                    help='1: the stem conv reads the f32 image directly (kinet_stem_conv_image); '
+                         '0: pack_image_kwfold + the folded conv (A/B)')
     ap.add_argument('--cpu-stub', action='store_true',
                     help='tests only: run the launch/timing skeleton with a tiny CPU model over gloo')
     a = ap.parse_args()
@@ -553,6 +556,7 @@ def main():
     K.MSDA_RECORDS[0] = bool(a.msda_records)
     from kinet_amd.models import backbone as BB
     BB.FUSE_BOTTLENECK_PAIRS = bool(a.bneck_pairs)
+    BB.STEM_FROM_IMAGE = bool(a.stem_image)
     elapsed, fam, msda, split, dec_touched = run_workload(a, a.workload, dev, world, rank, a.batch, a.streams,
                                                           a.height, a.width, a.dtype, a.steps, a.warmup)
 

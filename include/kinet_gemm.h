@@ -96,12 +96,22 @@ int kinet_conv2d_splitk(const void* X, const void* Wt, void* Y, int batch, int H
                         const float* scale, const float* bias, const void* R, int ldr, int relu, int ldy,
                         float* workspace, int ksplit, kinet_stream_t stream);
 
+/* ResNet stem from the image (torchvision conv1, 7x7 / stride 2 / pad 3, 3 -> 64, + folded
+ * FrozenBN + ReLU; the reference's backbone.py:102 body, IntermediateLayerGetter input): img
+ * f32 NCHW (N, 3, H, W) -> Y NHWC (N, (H-1)/2+1, (W-1)/2+1, 64) in dtype (KINET_BF16 /
+ * KINET_F16).  Replaces kinet_pack_image_kwfold + kinet_conv2d_ex over the folded layout
+ * (same values: the image is rounded to dtype once, the tap-folded rows are built in LDS);
+ * w_packed = the folded stem weights (64, 7, 1, 24) of that path; scale / bias (64) f32. */
+int kinet_stem_conv_image(const float* img, const void* w_packed, const float* scale, const float* bias,
+                          void* Y, int N, int H, int W, int dtype, kinet_stream_t stream);
+
 /* Diagnostic kernel-selection knob (no reference counterpart; used by the kernel
  * benchmarks to A/B GEMM kernels in one process).  bit 1: allow the 512-thread
  * 256x256-tile LDS-DMA kernel for large-M problems; bit 2: never use the
  * resident-weight streaming kernel; bit 8 (256): keep K = 512 problems off it (the
  * tiled kernel, as before round 3); bit 1024: never the direct 3x3 64 -> 64 channel
- * convolution (the implicit GEMM instead).  Returns the previous flags.  Per CALLING THREAD: torch
+ * convolution (the implicit GEMM instead); bit 2048: strided 1x1 convolutions (the stage-2
+ * downsample) on the implicit-GEMM kernel instead of the resident-weight conv-row kernel.  Returns the previous flags.  Per CALLING THREAD: torch
  * runs autograd backward for device tensors on its own engine thread, so flags set here do
  * NOT reach the backward kernels launched through autograd (only forward / direct calls). */
 int kinet_gemm_set_flags(int flags);

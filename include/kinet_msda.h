@@ -62,10 +62,17 @@ int64_t kinet_msda_backward_workspace_bytes(int batch, int spatial_size, int num
  * (image, head) walks passes of consecutive queries and adds each value row the pass touches
  * to global memory once.  0 = automatic for every field; mode -1 always selects the
  * one-atomic-per-corner kernel, mode 1 the on-chip-sum kernel for any call, mode 2 the
- * on-chip-sum kernel with queries in index order instead of 8-pixel-wide blocks (A/B, tests);
+ * on-chip-sum kernel with queries in index order instead of 8-pixel-wide blocks (A/B, tests),
+ * mode 3 the on-chip-sum kernel with four samples' corner loads in flight instead of two;
  * log2_rows = pixel hash size, queries_per_pass (0 = threads / 16). */
 void kinet_msda_backward_tune(int mode, int log2_rows, int queries_per_block, int threads,
                               int queries_per_pass);
+
+/* Timing-only phase knobs of the on-chip-sum backward kernel on the CALLING thread (results
+ * are wrong while set; tools/msda_bwd_probe.py --phases): 1 = skip the value-corner loads of
+ * the location / weight gradients, 2 = skip the per-row global atomics, 4 = skip the row-sum
+ * phase, 8 = skip the pixel-hash inserts.  Returns the previous flags. */
+int kinet_msda_backward_debug(int flags);
 
 /* Fused module path (MSDeformAttn.forward, ms_deform_attn.py:49-88): computes
  *   attw = softmax over L*P of logits            (ms_deform_attn.py:70-71)

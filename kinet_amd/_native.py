@@ -23,6 +23,7 @@ _SIGS = {
     'kinet_msda_backward': [P] * 9 + [I] * 10 + [P],
     'kinet_msda_backward_workspace_bytes': [I] * 5,
     'kinet_msda_backward_tune': [I] * 5,
+    'kinet_msda_backward_debug': [I],
     'kinet_msda_encoder_forward': [P, I64, I64, P, P, P, I, P, P] + [I] * 8 + [P, P],
     'kinet_msda_encoder_plan': [P, I, I, I, P],
     'kinet_msda_sample_records': [P, P, P, P, I, I, I, I, I, P, I, P, P, I, I, I, P, P],
@@ -41,6 +42,7 @@ _SIGS = {
     'kinet_ffn_pack': [P, P, P, I, I, I, P],
     'kinet_ffn_set_debug': [I],
     'kinet_ffn_fused': [P, I, P, P, P, P, P, F, P, I, I, I, I, I, P],
+    'kinet_stem_conv_image': [P, P, P, P, P, I, I, I, I, P],
     'kinet_bottleneck_pack': [P, P, P, P, P, I, I, I, I, P],
     'kinet_bottleneck_pair': [P, I, P, P, P, P, P, P, I, I, I, I, I, P],
     'kinet_layernorm': [P] * 5 + [I, I, F, I, I, P],

@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
                 img = c2 ? img + 1 : img;
                 const int ih = oh * p.stride - p.pad + cr_kh[j];
                 const bool ok = m0 + a_row[j] < M && (unsigned)ih < (unsigned)p.Hin;
-                off = ok ? ((unsigned)((img * p.Hin + ih) * p.Win + ow) * (unsigned)p.Cin + a_lo[j]) * 2u : OOB;
+                off = ok ? ((unsigned)((img * p.Hin + ih) * p.Win + ow * p.stride_w) * (unsigned)p.Cin + a_lo[j]) * 2u : OOB;
             }
             dma16(ra, st + (j * 256 + wave * 64) * 16, off);
             if (HAS_A2) dma16(ra2, st + C_::A_BYTES + (j * 256 + wave * 64) * 16, off);
@@ -645,6 +645,22 @@ bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t strea
 // leaves the call to the tiled kernel.
 bool launch_rw_conv(const GemmArgs& a, int in_dtype, hipStream_t stream) {
     if (in_dtype != KINET_BF16 && in_dtype != KINET_F16) return false;
+    // strided 1x1 (the ResNet downsample of stage 2, 256 -> 512 at stride 2): row m = output
+    // pixel, its A row = input pixel (img, 2 oh, 2 ow) -- the conv-row DMA with a horizontal
+    // stride; weights resident (K = 256), 256-column groups sharing each row tile through L2.
+    // The implicit-GEMM kernel ran it at ~310 TF/s (1.8 TB/s of compulsory bytes)
+    if (a.K == 256 && a.Cin == 256 && a.KW == 1 && a.pad == 0 && a.pad_w == 0 && a.stride > 1 &&
+        a.stride_w == a.stride && a.M >= rw_min_m && a.Wout >= 32 && a.N % 256 == 0 && a.R == nullptr &&
+        a.ln_g == nullptr && a.row_mask == nullptr && a.ldc % 8 == 0 && al16(a.C) && !(kinet_gemm_flags & 2048)) {
+        const long long cb = ((long long)(a.M - 1) * a.ldc + a.N) * 2;
+        if (cb >= (1LL << 31)) return false;
+        GemmArgs ac = a;
+        ac.c_bytes = (int)cb;
+        constexpr int NS = ring_depth<8, 32, false, false, false, 4>();
+        if (in_dtype == KINET_BF16) launch_cfg<bf16_t, bf16_t, 8, 32, NS, false, false, false, 4, true>(ac, stream);
+        else launch_cfg<f16_t, f16_t, 8, 32, NS, false, false, false, 4, true>(ac, stream);
+        return true;
+    }
     if (a.M < rw_min_m || a.K > 256 || a.KW != 1 || a.stride_w != 1 || a.pad_w != 0 || a.Win != a.Wout) return false;
     if (a.Cin % 8 != 0 || a.Wout < 32 || a.N > 128 || a.N % 8 != 0 || a.R != nullptr || a.ln_g != nullptr) return false;
     if (a.ldc % 8 != 0 || !al16(a.C) || a.row_mask != nullptr) return false;

@@ -875,6 +875,12 @@ __global__ __launch_bounds__(kThreads) void msda_bwd_kernel(
 //
 // LDS: LevelInfo | keys[NS] | head[NS] | plist[NS] | npass | cinfo[QP*L*P*4] (weight,
 //      grad_output row) | next[QP*L*P*4] | G[QP][D] f32 | taps[QP*L*P]
+// Where the time goes at the config-4 encoder call (tools/msda_bwd_probe.py --phases, r04q):
+// 1.12 ms in all; without phase 3 (row sums + atomics) 0.56, without its atomics 0.97, without
+// phase 2's value loads 0.95, and 0.43 ms with neither loads, hash inserts nor phase 3 -- the
+// per-workgroup setup (serial level info, hash clear) and phase 2's 12 shuffle reductions per
+// sample.  Packing each entry with its link (one LDS round trip per list step instead of two)
+// measured no change (1.12 ms).
 constexpr int kProbe = 8;
 
 struct HTap {
@@ -902,12 +908,12 @@ __device__ __forceinline__ int hash_slot(int* keys, int* plist, int* npass, int 
     return -1;
 }
 
-template <typename T, typename TL, int VEC, int NJ>
+template <typename T, typename TL, int VEC, int NJ, int SP = 2>
 __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
     const T* __restrict__ value, const int64_t* __restrict__ shapes, const TL* __restrict__ loc,
     const TL* __restrict__ attw, const T* __restrict__ gout, float* __restrict__ gvalue,
     TL* __restrict__ gloc, TL* __restrict__ gattw, int S, int M, int D, int L, int Lq, int P, int QC,
-    int QP, int NA, int log2ns, int blocked) {
+    int QP, int NA, int log2ns, int blocked, int dbg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int blk[kMaxLevels + 1];
     const int NS = 1 << log2ns;
@@ -997,6 +1003,7 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
                     for (int k = 0; k < 4; ++k)
                         if (in[k]) {
                             t.off[k] = pix[k] * MD;
+                            if (dbg & 8) continue;
                             const int slot = hash_slot(keys, plist, npass, pix[k], log2ns);
                             if (slot < 0) {
                                 t.flags |= 2 << k;
@@ -1027,7 +1034,7 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
             auto load = [&](const HTap& t, float (&v)[4][VEC]) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    if (cl && (t.flags & 1) && t.off[k] >= 0) {
+                    if (cl && (t.flags & 1) && t.off[k] >= 0 && !(dbg & 1)) {
                         const VecT<T, VEC> vv = *reinterpret_cast<const VecT<T, VEC>*>(vimg + t.off[k] + m * D + c0);
 #pragma unroll
                         for (int j = 0; j < VEC; ++j) v[k][j] = to_acc(vv.v[j], (float*)nullptr);
@@ -1077,6 +1084,20 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
                 }
             };
             int s = 0;
+            if constexpr (SP == 4) {   // four samples' 16 corner loads in flight together
+                for (; s + 3 < LP; s += 4) {
+                    const HTap t0 = tq[s], t1 = tq[s + 1], t2 = tq[s + 2], t3 = tq[s + 3];
+                    float v0[4][VEC], v1[4][VEC], v2[4][VEC], v3[4][VEC];
+                    load(t0, v0);
+                    load(t1, v1);
+                    load(t2, v2);
+                    load(t3, v3);
+                    consume(t0, v0, s);
+                    consume(t1, v1, s + 1);
+                    consume(t2, v2, s + 2);
+                    consume(t3, v3, s + 3);
+                }
+            }
             for (; s + 1 < LP; s += 2) {
                 const HTap t0 = tq[s], t1 = tq[s + 1];
                 float v0[4][VEC], v1[4][VEC];
@@ -1095,7 +1116,7 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
 
         // phase 3 (reads only what phase 1 wrote, so no barrier before it): lane = (slot,
         // channel), consecutive lanes on consecutive channels of the pass's rows
-        const int n = *npass;
+        const int n = (dbg & 4) ? 0 : *npass;
         for (int i = threadIdx.x; i < n * D; i += nt) {
             const int si = i / D, c = i - si * D;
             const int slot = plist[si];
@@ -1104,7 +1125,7 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
                 const int2 ci = cinfo[cid];
                 acc += __int_as_float(ci.x) * G[ci.y + c];
             }
-            atomicAdd(gimg + (long)keys[slot] * MD + c, acc);
+            if (!(dbg & 2)) atomicAdd(gimg + (long)keys[slot] * MD + c, acc);
         }
         __syncthreads();
         for (int i = threadIdx.x; i < n; i += nt) {
@@ -1194,6 +1215,10 @@ struct BwdTune {
     int mode, log2ns, qc, threads, flush_at;
 };
 thread_local BwdTune bwd_tune = {0, 0, 0, 0, 0};
+// timing-only phase knobs of msda_bwd_list_kernel (kinet_msda_backward_debug; results wrong
+// when set): 1 = phase 2 without its value loads, 2 = phase 3 without its global atomics,
+// 4 = no phase 3, 8 = no hash inserts (and so no phase-3 work)
+thread_local int bwd_dbg = 0;
 
 template <typename T, typename TL>
 int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const void* attw,
@@ -1247,9 +1272,15 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
         const int nq = blocked ? (S + QP - 1) / QP : (Lq + qc - 1) / qc;
         dim3 grid(blocked ? nq + nq / 8 + 2 * L : nq, N, M);
 #define KH(VEC, NJ)                                                                                             \
+    if (tn.mode == 3)                                                                                           \
+        hipLaunchKernelGGL((msda_bwd_list_kernel<T, TL, VEC, NJ, 4>), grid, dim3(threads), lds, stream,         \
+                           (const T*)value, shapes, (const TL*)loc, (const TL*)attw, (const T*)gout,            \
+                           (float*)acc_buf, (TL*)gloc, (TL*)gattw, S, M, D, L, Lq, P, qc, QP, c.lpq, log2ns,    \
+                           blocked, bwd_dbg);                                                                   \
+    else                                                                                                        \
     hipLaunchKernelGGL((msda_bwd_list_kernel<T, TL, VEC, NJ>), grid, dim3(threads), lds, stream, (const T*)value, \
                        shapes, (const TL*)loc, (const TL*)attw, (const T*)gout, (float*)acc_buf, (TL*)gloc,     \
-                       (TL*)gattw, S, M, D, L, Lq, P, qc, QP, c.lpq, log2ns, blocked)
+                       (TL*)gattw, S, M, D, L, Lq, P, qc, QP, c.lpq, log2ns, blocked, bwd_dbg)
 #define KHJ(VEC) switch (nj) { case 1: KH(VEC, 1); break; case 2: KH(VEC, 2); break; case 3: KH(VEC, 3); break; default: KH(VEC, 4); }
         switch (c.vec) {
             case 1: KHJ(1); break;
@@ -1462,6 +1493,12 @@ extern "C" int kinet_msda_backward(const void* value, const int64_t* spatial_sha
 #undef ARGS
     set_error("msda backward: unsupported dtype pair value=%d loc=%d", value_dtype, loc_dtype);
     return KINET_ERR_ARG;
+}
+
+extern "C" int kinet_msda_backward_debug(int flags) {
+    const int old = bwd_dbg;
+    bwd_dbg = flags;
+    return old;
 }
 
 extern "C" void kinet_msda_backward_tune(int mode, int log2_rows, int queries_per_block, int threads, int flush_at) {

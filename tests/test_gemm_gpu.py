@@ -767,3 +767,57 @@ def test_bottleneck_pair64_kernels_bit_identical(K, M):
         _native.lib().kinet_ffn_set_debug(old)
     torch.cuda.synchronize()
     assert torch.equal(y0, y1) and torch.equal(t0, t1)
+
+
+@pytest.mark.parametrize('B,H,W,N', [(16, 200, 334, 512), (2, 67, 81, 256), (1, 64, 64, 512)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_strided_conv1x1_rw_vs_fp32(K, B, H, W, N, dtype):
+    """The strided 1x1 conv (ResNet stage-2 downsample, 256 -> 512 at stride 2) on the
+    resident-weight conv-row kernel against torch fp32 F.conv2d + folded BN, at the config-2 size
+    and ragged sizes (odd H / W, partial row tiles); and against the implicit-GEMM kernel
+    (kinet_gemm_set_flags 2048) on the same inputs."""
+    from kinet_amd import _native
+    g = torch.Generator().manual_seed(H * W + N)
+    x = torch.relu(torch.randn(B, 256, H, W, generator=g)).to(dtype)
+    w = (torch.randn(N, 256, 1, 1, generator=g) * (1.0 / 256) ** 0.5).to(dtype)
+    scale = torch.rand(N, generator=g) + 0.5
+    bias = torch.randn(N, generator=g) * 0.1
+    xn = x.permute(0, 2, 3, 1).contiguous().cuda()
+    wp = K.pack_conv_weight(w.cuda(), dtype)
+    y = K.conv2d_nhwc(xn, wp, 2, 0, scale=scale.cuda(), bias=bias.cuda())
+    old = _native.lib().kinet_gemm_set_flags(2048)
+    try:
+        y_gemm = K.conv2d_nhwc(xn, wp, 2, 0, scale=scale.cuda(), bias=bias.cuda())
+    finally:
+        _native.lib().kinet_gemm_set_flags(old)
+    torch.cuda.synchronize()
+    ref = (F.conv2d(x.float().cuda(), w.float().cuda(), stride=2) * scale.cuda()[None, :, None, None]
+           + bias.cuda()[None, :, None, None])
+    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    err = (y.permute(0, 3, 1, 2).float() - ref).abs()
+    assert (err <= 2 * ulp * ref.abs() + 1e-3).all(), err.max().item()
+    d = (y.float() - y_gemm.float()).abs()
+    assert (d <= 2 * ulp * y_gemm.float().abs() + 1e-3).all(), d.max().item()
+
+
+@pytest.mark.parametrize('B,H,W', [(2, 50, 66), (1, 37, 41), (2, 800, 1333), (1, 1080, 1920), (1, 9, 7)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_stem_conv_image_equals_folded_path(K, B, H, W, dtype):
+    """kinet_stem_conv_image (folded rows built in LDS from the f32 image) is bit-identical to
+    pack_image_kwfold + the folded stem conv (same rounded inputs, same MFMA order), incl. ragged
+    tiles and an image smaller than one tile; and both match torch fp32 conv1 + BN + ReLU."""
+    g = torch.Generator().manual_seed(H * W + B)
+    img = torch.randn(B, 3, H, W, generator=g)
+    w = torch.randn(64, 3, 7, 7, generator=g) * 0.1
+    scale = torch.rand(64, generator=g) + 0.5
+    bias = torch.randn(64, generator=g) * 0.1
+    wp = K.pack_stem_weight(w.cuda(), dtype, 24)
+    xp = K.pack_image_kwfold(img.cuda(), dtype, 7, 2, 3, 24)
+    y0 = K.conv2d_nhwc(xp, wp, (2, 1), (3, 0), scale=scale.cuda(), bias=bias.cuda(), relu=True)
+    y1 = K.stem_conv_image(img.cuda(), wp, scale.cuda(), bias.cuda(), dtype)
+    torch.cuda.synchronize()
+    assert y1.shape == y0.shape
+    assert torch.equal(y0, y1)
+    if H * W < 10 ** 6:
+        ref = F.relu(F.conv2d(img, w, stride=2, padding=3) * scale[None, :, None, None] + bias[None, :, None, None])
+        assert _rel(y1.permute(0, 3, 1, 2), ref) < 2e-2

@@ -8,7 +8,11 @@ have random reference points.  Offsets: the reference init (8-direction grid, po
 radius i+1 pixels) + N(0, noise) pixels.  Times the direct-atomic kernel (tune mode -1) and the
 LDS-table kernel at the given table shapes, and checks they agree.
 
-    python tools/msda_bwd_probe.py [--iters 10] [--noise 0.5] [--sweep]
+    python tools/msda_bwd_probe.py [--iters 10] [--noise 0.5] [--sweep] [--phases]
+
+--phases: the on-chip-sum kernel with each timing-only phase knob (kinet_msda_backward_debug:
+1 no value loads in the location / weight gradients, 2 no row atomics, 4 no row-sum phase,
+8 no hash inserts) -- where the time goes.
 """
 import argparse
 import math
@@ -50,14 +54,16 @@ def main():
     ap.add_argument('--noise', type=float, default=0.5)
     ap.add_argument('--sweep', action='store_true')
     ap.add_argument('--case', default='encoder,decoder')
+    ap.add_argument('--phases', action='store_true')
     a = ap.parse_args()
     from kinet_amd import _native
     from kinet_amd.MultiScaleDeformableAttention import ms_deform_attn_backward
     tune = _native.lib().kinet_msda_backward_tune
+    dbg = _native.lib().kinet_msda_backward_debug
     lv = [(100, 167), (50, 84), (25, 42), (13, 21)]
     cases = {'encoder': (2, lv, 22223, True), 'decoder': (2, lv + lv, 520, False)}
     # (mode, log2 hash rows, queries per block, threads, queries per pass)
-    cfgs = [(-1, 0, 0, 0, 0), (0, 0, 0, 0, 0), (2, 0, 0, 0, 0)]
+    cfgs = [(-1, 0, 0, 0, 0), (0, 0, 0, 0, 0), (2, 0, 0, 0, 0), (3, 0, 0, 0, 0)]
     if a.sweep:
         cfgs += [(0, l2, 0, th, qp) for l2 in (9, 10, 11) for th in (256, 512) for qp in (16, 32, 64)
                  if qp >= th // 32]
@@ -66,15 +72,21 @@ def main():
             continue
         v, ss, loc, attw, gout = inputs(B, shapes, Lq, encoder=enc, noise=a.noise)
         ref = None
-        for cfg in cfgs:
+        runs = [(c, 0) for c in cfgs]
+        if a.phases:
+            runs += [((0, 0, 0, 0, 0), f) for f in (1, 2, 4, 8, 1 | 4, 1 | 8)]
+        for cfg, flags in runs:
             tune(*cfg)
+            dbg(flags)
             try:
                 out = ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
             except RuntimeError as ex:
                 print(f'{name:8s} cfg {cfg}: {ex}', flush=True)
                 continue
             torch.cuda.synchronize()
-            if ref is None:
+            if flags:
+                pass
+            elif ref is None:
                 ref = [t.clone() for t in out]
                 err = 0.0
             else:
@@ -85,6 +97,11 @@ def main():
                 ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
             e.record()
             torch.cuda.synchronize()
+            dbg(0)
+            if flags:
+                print(f'{name:8s} noise {a.noise} cfg {cfg} phase knob {flags}: {s.elapsed_time(e) / a.iters:8.3f} ms',
+                      flush=True)
+                continue
             print(f'{name:8s} noise {a.noise} cfg {cfg}: {s.elapsed_time(e) / a.iters:8.3f} ms  '
                   f'max rel diff vs direct {err:.2e}', flush=True)
     tune(0, 0, 0, 0, 0)
