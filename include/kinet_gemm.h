@@ -105,6 +105,12 @@ int kinet_conv2d_splitk(const void* X, const void* Wt, void* Y, int batch, int H
 int kinet_stem_conv_image(const float* img, const void* w_packed, const float* scale, const float* bias,
                           void* Y, int N, int H, int W, int dtype, kinet_stream_t stream);
 
+/* kinet_stem_conv_image followed by torchvision's maxpool (3x3, stride 2, pad 1) in ONE launch:
+ * Y NHWC (N, (Ho-1)/2+1, (Wo-1)/2+1, 64) with (Ho, Wo) the conv output; the conv map is never
+ * written (bit-identical to kinet_stem_conv_image + kinet_maxpool2d_3x3s2). */
+int kinet_stem_pool_image(const float* img, const void* w_packed, const float* scale, const float* bias,
+                          void* Y, int N, int H, int W, int dtype, kinet_stream_t stream);
+
 /* Diagnostic kernel-selection knob (no reference counterpart; used by the kernel
  * benchmarks to A/B GEMM kernels in one process).  bit 1: allow the 512-thread
  * 256x256-tile LDS-DMA kernel for large-M problems; bit 2: never use the

@@ -343,6 +343,24 @@ def stem_conv_image(img, w_packed, scale, bias, dtype):
     return y
 
 
+def stem_pool_image(img, w_packed, scale, bias, dtype):
+    """ResNet stem + max-pool in one launch from the f32 NCHW image (kinet_stem_pool_image):
+    (B, 3, H, W) -> (B, Hp, Wp, 64) NHWC, Hp = ((H-1)//2)//2 + 1, the conv map never stored."""
+    img = img.float().contiguous()
+    N.require_gpu(img)
+    B, C, H, W = img.shape
+    if C != 3:
+        raise RuntimeError('stem_pool_image expects 3-channel images')
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    Hp, Wp = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
+    y = torch.empty((B, Hp, Wp, 64), dtype=dtype, device=img.device)
+    work = {'family': 'conv', 'flops': 2.0 * B * Ho * Wo * 64 * 147, 'shape': ('stem_pool', B, H, W),
+            'bytes': B * 3 * H * W * 4 + B * Hp * Wp * 64 * y.element_size()}
+    N.call('kinet_stem_pool_image', N.ptr(img), N.ptr(w_packed), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(y),
+           B, H, W, N.dtype_code(dtype), N.stream(img.device), work=work)
+    return y
+
+
 def bottleneck_pack(w3, w1, s3, s1, dtype):
     """kinet_bottleneck_pack of conv3 (F, D, 1, 1) and the next block's conv1 (DB, F, 1, 1) with
     their FrozenBN scales folded in, cached per parameter version."""

@@ -61,6 +61,8 @@ FUSE_PAIR_WIDTHS = (64,)
 # 16-bit stem straight from the f32 image (kinet_stem_conv_image); False: pack_image_kwfold +
 # the folded conv (A/B: bench.py --stem-image 0)
 STEM_FROM_IMAGE = True
+# ... and the max-pool fused into it (kinet_stem_pool_image; A/B: bench.py --stem-pool 0)
+STEM_POOL = False
 
 
 def conv_bn(x, conv, bn, relu, residual=None, cin_pad=None):
@@ -212,14 +214,18 @@ class ResNetBody(nn.Module):
         kh, kw = c1.kernel_size
         cg = (3 * kw + 7) // 8 * 8
         scale, bias = self.bn1.folded()
-        if STEM_FROM_IMAGE and dtype in (torch.bfloat16, torch.float16):
-            # the folded rows built in LDS from the f32 image (no packed copy of the image)
-            x = K.stem_conv_image(img_nchw, K.pack_stem_weight(c1.weight, dtype, cg), scale, bias, dtype)
+        if STEM_FROM_IMAGE and STEM_POOL and dtype in (torch.bfloat16, torch.float16):
+            # conv1 + bn1 + relu + maxpool in one launch from the f32 image (conv map never stored)
+            x = K.stem_pool_image(img_nchw, K.pack_stem_weight(c1.weight, dtype, cg), scale, bias, dtype)
         else:
-            x = K.pack_image_kwfold(img_nchw, dtype, kw, c1.stride[1], c1.padding[1], cg)
-            x = K.conv2d_nhwc(x, K.pack_stem_weight(c1.weight, dtype, cg), (c1.stride[0], 1), (c1.padding[0], 0),
-                              scale=scale, bias=bias, relu=True)
-        x = K.maxpool_3x3s2(x)
+            if STEM_FROM_IMAGE and dtype in (torch.bfloat16, torch.float16):
+                # the folded rows built in LDS from the f32 image (no packed copy of the image)
+                x = K.stem_conv_image(img_nchw, K.pack_stem_weight(c1.weight, dtype, cg), scale, bias, dtype)
+            else:
+                x = K.pack_image_kwfold(img_nchw, dtype, kw, c1.stride[1], c1.padding[1], cg)
+                x = K.conv2d_nhwc(x, K.pack_stem_weight(c1.weight, dtype, cg), (c1.stride[0], 1),
+                                  (c1.padding[0], 0), scale=scale, bias=bias, relu=True)
+            x = K.maxpool_3x3s2(x)
         return forward_layer_nhwc(self.layer1, x, None, next_block)
 
     def forward(self, x):

@@ -821,3 +821,22 @@ def test_stem_conv_image_equals_folded_path(K, B, H, W, dtype):
     if H * W < 10 ** 6:
         ref = F.relu(F.conv2d(img, w, stride=2, padding=3) * scale[None, :, None, None] + bias[None, :, None, None])
         assert _rel(y1.permute(0, 3, 1, 2), ref) < 2e-2
+
+
+@pytest.mark.parametrize('B,H,W', [(2, 50, 66), (1, 37, 41), (2, 800, 1333), (1, 1080, 1920), (1, 9, 7), (1, 3, 130)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_stem_pool_image_equals_separate(K, B, H, W, dtype):
+    """kinet_stem_pool_image (conv1 + BN + ReLU + maxpool 3x3/2 in one launch; the conv map is
+    recomputed on tile halos and never stored) is bit-identical to kinet_stem_conv_image +
+    kinet_maxpool2d_3x3s2, incl. ragged pooled tiles and images smaller than one tile."""
+    g = torch.Generator().manual_seed(H * W + B + 7)
+    img = torch.randn(B, 3, H, W, generator=g)
+    w = torch.randn(64, 3, 7, 7, generator=g) * 0.1
+    scale = torch.rand(64, generator=g) + 0.5
+    bias = torch.randn(64, generator=g) * 0.1
+    wp = K.pack_stem_weight(w.cuda(), dtype, 24)
+    sep = K.maxpool_3x3s2(K.stem_conv_image(img.cuda(), wp, scale.cuda(), bias.cuda(), dtype))
+    fused = K.stem_pool_image(img.cuda(), wp, scale.cuda(), bias.cuda(), dtype)
+    torch.cuda.synchronize()
+    assert fused.shape == sep.shape
+    assert torch.equal(fused, sep)
