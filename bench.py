@@ -87,8 +87,12 @@ def parse():
     ap.add_argument('--stem-image', type=int, default=1,
                     help='1: the stem conv reads the f32 image directly (kinet_stem_conv_image); '
                          '0: pack_image_kwfold + the folded conv (A/B)')
-    ap.add_argument('--stem-pool', type=int, default=1,
-                    help='1: stem conv + max-pool in one launch (kinet_stem_pool_image); 0: separate (A/B)')
+    ap.add_argument('--stem-pool', type=int, default=0,
+                    help='1: stem conv + max-pool in one launch (kinet_stem_pool_image; measured slower, '
+                         'DESIGN.md §4); 0: separate')
+    ap.add_argument('--pool-pair', type=int, default=0,
+                    help='1: max-pool + layer1[0].conv1 + downsample in one launch (kinet_pool_conv1x1_pair; '
+                         'measured slower, DESIGN.md §4); 0: separate')
     ap.add_argument('--cpu-stub', action='store_true',
                     help='tests only: run the launch/timing skeleton with a tiny CPU model over gloo')
     a = ap.parse_args()
@@ -560,6 +564,7 @@ def main():
     BB.FUSE_BOTTLENECK_PAIRS = bool(a.bneck_pairs)
     BB.STEM_FROM_IMAGE = bool(a.stem_image)
     BB.STEM_POOL = bool(a.stem_pool)
+    BB.POOL_PAIR = bool(a.pool_pair)
     elapsed, fam, msda, split, dec_touched = run_workload(a, a.workload, dev, world, rank, a.batch, a.streams,
                                                           a.height, a.width, a.dtype, a.steps, a.warmup)
 

@@ -111,6 +111,15 @@ int kinet_stem_conv_image(const float* img, const void* w_packed, const float* s
 int kinet_stem_pool_image(const float* img, const void* w_packed, const float* scale, const float* bias,
                           void* Y, int N, int H, int W, int dtype, kinet_stream_t stream);
 
+/* ResNet stage-1 entry (torchvision resnet50 / 101 as backbone.py:102 builds it): maxpool
+ * (3x3 / 2, pad 1) of the stem output X (N, Ho, Wo, 64) NHWC, then layer1[0].conv1 (64 -> 64,
+ * + folded bn1, + ReLU) -> T1 (N, Hp, Wp, 64) and layer1[0].downsample (64 -> 256, + folded BN)
+ * -> ID (N, Hp, Wp, 256), in ONE launch (the pooled map is not written).  W (320, 64) = conv1
+ * weight rows then downsample weight rows (dtype); scale / bias (320) f32 = bn1 then the
+ * downsample BN, folded.  dtype KINET_BF16 / KINET_F16. */
+int kinet_pool_conv1x1_pair(const void* X, const void* W, const float* scale, const float* bias, void* T1,
+                            void* ID, int N, int Ho, int Wo, int dtype, kinet_stream_t stream);
+
 /* Diagnostic kernel-selection knob (no reference counterpart; used by the kernel
  * benchmarks to A/B GEMM kernels in one process).  bit 1: allow the 512-thread
  * 256x256-tile LDS-DMA kernel for large-M problems; bit 2: never use the

@@ -44,6 +44,7 @@ _SIGS = {
     'kinet_ffn_fused': [P, I, P, P, P, P, P, F, P, I, I, I, I, I, P],
     'kinet_stem_conv_image': [P, P, P, P, P, I, I, I, I, P],
     'kinet_stem_pool_image': [P, P, P, P, P, I, I, I, I, P],
+    'kinet_pool_conv1x1_pair': [P, P, P, P, P, P, I, I, I, I, P],
     'kinet_bottleneck_pack': [P, P, P, P, P, I, I, I, I, P],
     'kinet_bottleneck_pair': [P, I, P, P, P, P, P, P, I, I, I, I, I, P],
     'kinet_layernorm': [P] * 5 + [I, I, F, I, I, P],

@@ -361,6 +361,30 @@ def stem_pool_image(img, w_packed, scale, bias, dtype):
     return y
 
 
+def pool_conv1x1_pair(x, w1, s1, b1, wds, sds, bds):
+    """maxpool 3x3/2 of the stem output x (B, Ho, Wo, 64) NHWC, then layer1[0].conv1 (w1 (64, 64,
+    1, 1), folded bn1 s1/b1, ReLU) and layer1[0].downsample (wds (256, 64, 1, 1), folded BN) in one
+    launch (kinet_pool_conv1x1_pair) -> (t1 (B, Hp, Wp, 64), identity (B, Hp, Wp, 256))."""
+    N.require_gpu(x)
+    B, Ho, Wo, C = x.shape
+    if C != 64 or not x.is_contiguous():
+        raise RuntimeError('pool_conv1x1_pair: x must be a contiguous (B, Ho, Wo, 64) tensor')
+    Hp, Wp = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
+    wcat = cached_multi([w1, wds], ('pool_pair_w', x.dtype),
+                        lambda a, b: torch.cat([a.detach().reshape(64, 64), b.detach().reshape(256, 64)]).to(x.dtype).contiguous())
+    sc = cached_multi([s1, sds], ('pool_pair_s',), lambda a, b: torch.cat([f32(a), f32(b)]).contiguous())
+    bi = cached_multi([b1, bds], ('pool_pair_b',), lambda a, b: torch.cat([f32(a), f32(b)]).contiguous())
+    t1 = torch.empty((B, Hp, Wp, 64), dtype=x.dtype, device=x.device)
+    idn = torch.empty((B, Hp, Wp, 256), dtype=x.dtype, device=x.device)
+    M = B * Hp * Wp
+    e = x.element_size()
+    work = {'family': 'conv', 'flops': 2.0 * M * 320 * 64, 'shape': ('pool_pair', M),
+            'bytes': (B * Ho * Wo * 64 + M * 320) * e}
+    N.call('kinet_pool_conv1x1_pair', N.ptr(x), N.ptr(wcat), N.ptr(sc), N.ptr(bi), N.ptr(t1), N.ptr(idn), B, Ho, Wo,
+           N.dtype_code(x.dtype), N.stream(x.device), work=work)
+    return t1, idn
+
+
 def bottleneck_pack(w3, w1, s3, s1, dtype):
     """kinet_bottleneck_pack of conv3 (F, D, 1, 1) and the next block's conv1 (DB, F, 1, 1) with
     their FrozenBN scales folded in, cached per parameter version."""

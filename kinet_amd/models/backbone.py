@@ -63,6 +63,9 @@ FUSE_PAIR_WIDTHS = (64,)
 STEM_FROM_IMAGE = True
 # ... and the max-pool fused into it (kinet_stem_pool_image; A/B: bench.py --stem-pool 0)
 STEM_POOL = False
+# max-pool + layer1[0].conv1 + layer1[0].downsample in one launch (kinet_pool_conv1x1_pair):
+# measured 1.4 % slower than the three kernels in the bench, off by default
+POOL_PAIR = False
 
 
 def conv_bn(x, conv, bn, relu, residual=None, cin_pad=None):
@@ -113,19 +116,23 @@ def _pair_ok(dtype, blk, nxt):
             and K.bottleneck_pair_supported(dtype, blk.conv3.weight, nxt.conv1.weight))
 
 
-def forward_layer_nhwc(layer, x, t1=None, next_block=None):
+def forward_layer_nhwc(layer, x, t1=None, next_block=None, identity0=None):
     """One ResNet stage over NHWC x -> (stage output, next_block's conv1 output or None).
     With FUSE_BOTTLENECK_PAIRS the chain conv3 (+ residual + ReLU) of block i -> conv1 of block
     i+1 runs as one kinet_bottleneck_pair launch: the block output is written once (the next
     block's residual) and not re-read by the next conv1.  `next_block` (the next stage's first
     block) extends the chain across the stage boundary where the pair kernel covers it (stage 1
     -> 2: its conv1 is stride 1); `t1` = this stage's first conv1 output when the previous stage
-    computed it.  Same math as Bottleneck.forward_nhwc per block (torchvision, backbone.py:102)."""
+    computed it, `identity0` its first block's downsample output (then x is not read).  Same
+    math as Bottleneck.forward_nhwc per block (torchvision, backbone.py:102)."""
     blocks = list(layer)
     b0 = blocks[0]
     if t1 is None:
         t1 = conv_bn(x, b0.conv1, b0.bn1, True)
-    identity = x if b0.downsample is None else conv_bn(x, b0.downsample[0], b0.downsample[1], False)
+    if identity0 is not None:
+        identity = identity0
+    else:
+        identity = x if b0.downsample is None else conv_bn(x, b0.downsample[0], b0.downsample[1], False)
     t_next = None
     for i, blk in enumerate(blocks):
         t2 = conv_bn(t1, blk.conv2, blk.bn2, True)
@@ -225,6 +232,15 @@ class ResNetBody(nn.Module):
                 x = K.pack_image_kwfold(img_nchw, dtype, kw, c1.stride[1], c1.padding[1], cg)
                 x = K.conv2d_nhwc(x, K.pack_stem_weight(c1.weight, dtype, cg), (c1.stride[0], 1),
                                   (c1.padding[0], 0), scale=scale, bias=bias, relu=True)
+            b0 = self.layer1[0]
+            if (POOL_PAIR and dtype in (torch.bfloat16, torch.float16) and b0.downsample is not None
+                    and tuple(b0.conv1.weight.shape) == (64, 64, 1, 1)
+                    and tuple(b0.downsample[0].weight.shape) == (256, 64, 1, 1) and b0.downsample[0].stride == (1, 1)):
+                # maxpool + layer1[0].conv1 + layer1[0].downsample in one launch (pooled map not stored)
+                s1, bb1 = b0.bn1.folded()
+                sd, bd = b0.downsample[1].folded()
+                t1, idn = K.pool_conv1x1_pair(x, b0.conv1.weight, s1, bb1, b0.downsample[0].weight, sd, bd)
+                return forward_layer_nhwc(self.layer1, None, t1, next_block, identity0=idn)
             x = K.maxpool_3x3s2(x)
         return forward_layer_nhwc(self.layer1, x, None, next_block)
 

@@ -840,3 +840,34 @@ def test_stem_pool_image_equals_separate(K, B, H, W, dtype):
     torch.cuda.synchronize()
     assert fused.shape == sep.shape
     assert torch.equal(fused, sep)
+
+
+@pytest.mark.parametrize('B,Ho,Wo', [(2, 400, 667), (1, 37, 53), (2, 5, 3), (1, 540, 960)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_pool_conv1x1_pair_vs_separate(K, B, Ho, Wo, dtype):
+    """kinet_pool_conv1x1_pair (maxpool 3x3/2 + layer1[0].conv1 + bn1 + ReLU and the 64 -> 256
+    downsample + BN in one launch) against maxpool_3x3s2 followed by the two convs: the pooled
+    map is the same (max is exact), the 1x1 convs agree to one output rounding; and against
+    torch fp32 on the rounded pooled map."""
+    g = torch.Generator().manual_seed(Ho * Wo + B)
+    x = torch.relu(torch.randn(B, Ho, Wo, 64, generator=g)).to(dtype).cuda()
+    w1 = (torch.randn(64, 64, 1, 1, generator=g) * 0.15).cuda()
+    wd = (torch.randn(256, 64, 1, 1, generator=g) * 0.15).cuda()
+    s1, b1 = (torch.rand(64, generator=g) + 0.5).cuda(), (torch.randn(64, generator=g) * 0.1).cuda()
+    sd, bd = (torch.rand(256, generator=g) + 0.5).cuda(), (torch.randn(256, generator=g) * 0.1).cuda()
+    t1, idn = K.pool_conv1x1_pair(x, w1, s1, b1, wd, sd, bd)
+    xp = K.maxpool_3x3s2(x)
+    t1r = K.conv2d_nhwc(xp, K.pack_conv_weight(w1, dtype), 1, 0, scale=s1, bias=b1, relu=True)
+    idr = K.conv2d_nhwc(xp, K.pack_conv_weight(wd, dtype), 1, 0, scale=sd, bias=bd)
+    torch.cuda.synchronize()
+    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    for got, ref in ((t1, t1r), (idn, idr)):
+        assert got.shape == ref.shape
+        d = (got.float() - ref.float()).abs()
+        assert (d <= 2 * ulp * ref.float().abs() + 1e-3).all(), d.max().item()
+    xf = xp.float().reshape(-1, 64)
+    f1 = torch.relu(xf @ (w1.reshape(64, 64).to(dtype).float()).T * s1 + b1)
+    fd = xf @ (wd.reshape(256, 64).to(dtype).float()).T * sd + bd
+    for got, ref in ((t1, f1), (idn, fd)):
+        d = (got.float().reshape(ref.shape) - ref).abs()
+        assert (d <= 2 * ulp * ref.abs() + 1e-3).all(), d.max().item()
