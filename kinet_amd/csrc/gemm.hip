@@ -601,6 +601,13 @@ int dispatch(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t s) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;
     }
+    // opt-in only: the direct 128-channel kernel measured slower than the implicit GEMM (186-193 vs
+    // 118-134 us at batch 16, profiles/r04v_time.log: one MFMA per LDS fragment read, all 8 waves
+    // reading every fragment -- LDS-bound)
+    if (CONV && (kinet_gemm_flags & 4096) && out_dtype == in_dtype && launch_conv3x3_c128(a, in_dtype, s)) {
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
     if (CONV && !(kinet_gemm_flags & 32) && out_dtype == in_dtype && launch_stem_conv(a, in_dtype, s)) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;

@@ -871,3 +871,35 @@ def test_pool_conv1x1_pair_vs_separate(K, B, Ho, Wo, dtype):
     for got, ref in ((t1, f1), (idn, fd)):
         d = (got.float().reshape(ref.shape) - ref).abs()
         assert (d <= 2 * ulp * ref.abs() + 1e-3).all(), d.max().item()
+
+
+@pytest.mark.parametrize('B,H,W', [(16, 100, 167), (2, 37, 53), (1, 3, 5), (3, 9, 70)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_direct_conv3x3_c128_vs_fp32(K, B, H, W, dtype):
+    """The direct 3x3 / stride 1 / pad 1, 128 -> 128 conv (csrc/conv3x3.hip conv3x3_c128_kernel,
+    opt-in through kinet_gemm_set_flags 4096: weights resident in VGPRs, 4 x 32 tiles with LDS
+    halos) and the default implicit GEMM, both against torch fp32 F.conv2d + folded BN + ReLU at
+    the config-2 stage-2 size and ragged sizes, and against each other."""
+    from kinet_amd import _native
+    g = torch.Generator().manual_seed(H * W + B + 128)
+    x = torch.relu(torch.randn(B, 128, H, W, generator=g)).to(dtype)
+    w = (torch.randn(128, 128, 3, 3, generator=g) * (2.0 / 1152) ** 0.5).to(dtype)
+    scale = torch.rand(128, generator=g) + 0.5
+    bias = torch.randn(128, generator=g) * 0.1
+    xn = x.permute(0, 2, 3, 1).contiguous().cuda()
+    wp = K.pack_conv_weight(w.cuda(), dtype)
+    y = K.conv2d_nhwc(xn, wp, 1, 1, scale=scale.cuda(), bias=bias.cuda(), relu=True)
+    old = _native.lib().kinet_gemm_set_flags(4096)
+    try:
+        y_gemm = K.conv2d_nhwc(xn, wp, 1, 1, scale=scale.cuda(), bias=bias.cuda(), relu=True)
+    finally:
+        _native.lib().kinet_gemm_set_flags(old)
+    torch.cuda.synchronize()
+    ref = F.relu(F.conv2d(x.float().cuda(), w.float().cuda(), padding=1) * scale.cuda()[None, :, None, None]
+                 + bias.cuda()[None, :, None, None])
+    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    for out in (y, y_gemm):
+        err = (out.permute(0, 3, 1, 2).float() - ref).abs()
+        assert (err <= 2 * ulp * ref.abs() + 1e-3).all(), err.max().item()
+    d = (y.float() - y_gemm.float()).abs()
+    assert (d <= 2 * ulp * y_gemm.float().abs() + 1e-3).all(), d.max().item()
