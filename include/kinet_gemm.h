@@ -128,7 +128,9 @@ int kinet_pool_conv1x1_pair(const void* X, const void* W, const float* scale, co
  * convolution (the implicit GEMM instead); bit 2048: strided 1x1 convolutions (the stage-2
  * downsample) on the implicit-GEMM kernel instead of the resident-weight conv-row kernel; bit 4096:
  * the direct 3x3 128 -> 128 channel convolution for stage 2's conv2 (opt-in: measured slower than
- * the implicit GEMM).  Returns the previous flags.  Per CALLING THREAD: torch
+ * the implicit GEMM); bit 8192: the encoder sampling-records GEMM (kinet_msda_sample_records with
+ * x_add) at two workgroups per CU with a 4-slot ring instead of three with a 2-slot ring.
+ * Returns the previous flags.  Per CALLING THREAD: torch
  * runs autograd backward for device tensors on its own engine thread, so flags set here do
  * NOT reach the backward kernels launched through autograd (only forward / direct calls). */
 int kinet_gemm_set_flags(int flags);

@@ -205,8 +205,8 @@ __device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_
 // pack_image_kwfold_kernel): K = KH*Cin, logical chunk q of the row = 8 channels of tap
 // kh = q / (Cin/8) read from input row oh*stride - pad + kh (zeros outside the image and past K)
 template <typename T, typename TO, int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2, bool CR,
-          bool PREP = false>
-__global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const int n_mtiles) {
+          bool PREP = false, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, const int n_mtiles) {
     using C_ = RwCfg<KC, NT, BMR, NS, HAS_R, LN, HAS_A2, PREP>;
     constexpr int TMR = BMR / 16;             // 16-row MFMA tiles per row tile
     constexpr int GW = C_::GW;
@@ -539,7 +539,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rw_kernel(const GemmArgs p, const
 }
 
 template <typename T, typename TO, int KC, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2 = false, int NT = 4,
-          bool CR = false, bool PREP = false>
+          bool CR = false, bool PREP = false, int OCC = 2>
 void launch_cfg(const GemmArgs& a, hipStream_t stream) {
     constexpr int GW = 4 * NT * 16;
     const int n_mtiles = (a.M + BMR - 1) / BMR;
@@ -547,10 +547,12 @@ void launch_cfg(const GemmArgs& a, hipStream_t stream) {
     // 2 resident workgroups per CU over all groups: never more than the 512 slots (a second
     // round of workgroups would double the launch), and a multiple of 8 so the column groups
     // of one row tile land on one XCD (linear id bx + y*P) and share its L2 copy of the tile
-    int P = 512 / ng >= 8 ? 512 / ng / 8 * 8 : 512 / ng;
+    // (OCC resident workgroups per CU: 256 * OCC slots)
+    const int slots = 256 * OCC;
+    int P = slots / ng >= 8 ? slots / ng / 8 * 8 : slots / ng;
     if (P > n_mtiles) P = n_mtiles;
     dim3 grid(P, ng), block(256);
-    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR, PREP>), grid, block, 0, stream,
+    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR, PREP, OCC>), grid, block, 0, stream,
                        a, n_mtiles);
 }
 
@@ -722,6 +724,18 @@ extern "C" int kinet_msda_sample_records(const void* A, const void* A2, const vo
     hipStream_t s = (hipStream_t)stream;
     constexpr int NS2 = ring_depth<8, 16, false, false, true, 3, true>();
     constexpr int NS1 = ring_depth<8, 16, false, false, false, 3, true>();
+    // three workgroups per CU (159 VGPRs, a 2-slot ring: 39 KiB of LDS each) when the tile adds
+    // A2: alone the call is ~4 % slower than two workgroups with a 4-slot ring (228 vs 220 us),
+    // but under the bench's three batches in flight the whole step is 0.9 % faster (1311 / 1316
+    // vs 1304 / 1299 frames/s, profiles/r04z_occ_ab.log) -- the smaller LDS footprint leaves room
+    // for the other streams' workgroups.  Four per CU (128 VGPRs) spills and loses 7 %.  Flag
+    // 8192: the two-workgroup ring.
+    if (!(kinet_gemm_flags & 8192) && A2) {
+        if (in_dtype == KINET_BF16) launch_cfg<bf16_t, f16_t, 8, 16, 2, false, false, true, 3, false, true, 3>(a, s);
+        else launch_cfg<f16_t, f16_t, 8, 16, 2, false, false, true, 3, false, true, 3>(a, s);
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
     if (in_dtype == KINET_BF16) {
         if (A2) launch_cfg<bf16_t, f16_t, 8, 16, NS2, false, false, true, 3, false, true>(a, s);
         else launch_cfg<bf16_t, f16_t, 8, 16, NS1, false, false, false, 3, false, true>(a, s);

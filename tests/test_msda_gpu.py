@@ -657,3 +657,26 @@ def test_encoder_records_path_matches_offlog_path():
     vmax = value.float().abs().max().item()
     assert (d <= o_off.float().abs() * 2.0 ** -6 + 2.0 ** -6 * vmax).all(), d.max().item()
     assert d.mean().item() <= 2e-3, d.mean().item()
+
+
+@pytest.mark.parametrize('masked', [False, True])
+def test_sample_records_occupancy_variants_bit_identical(masked):
+    """The records GEMM at three workgroups per CU (the default: 2-slot ring, <= 168 VGPRs) runs
+    the same per-row arithmetic as two per CU with a 4-slot ring (kinet_gemm_set_flags 8192):
+    bit-identical records, incl. the ragged last tile."""
+    from kinet_amd import _native
+    from kinet_amd import kernels as K
+    shapes = ((100, 167), (50, 84), (25, 42), (13, 21))
+    x, pos, w, bias, ref, qmask, raw = _record_problem(shapes, 2, 3.0, 77, 2, masked)
+    args = (x.cuda(), w.cuda(), bias.cuda(), 8, ref.cuda(), shapes)
+    kw = dict(x_add=pos.cuda(), query_attn_mask=qmask.cuda() if qmask is not None else None)
+    r0, fb0 = K.msda_sample_records(*args, **kw)
+    old = _native.lib().kinet_gemm_set_flags(8192)
+    try:
+        r1, fb1 = K.msda_sample_records(*args, **kw)
+    finally:
+        _native.lib().kinet_gemm_set_flags(old)
+    torch.cuda.synchronize()
+    assert fb0 == fb1
+    d = (r0 != r1)
+    assert not d.any(), (int(d.sum()), d.reshape(-1, r0.shape[-1]).sum(0).tolist())
