@@ -1,5 +1,5 @@
-"""Records GEMM (kinet_msda_sample_records, batch-16 encoder shape) at 2 / 3 / 4 workgroups per
-CU (kinet_gemm_set_flags 0 / 8192 / 32768); run under rocprofv3 --kernel-trace --stats for
+"""Records GEMM (kinet_msda_sample_records, batch-16 encoder shape) at 3 / 2 workgroups per
+CU (kinet_gemm_set_flags 0 = three per CU, 8192 = two); run under rocprofv3 --kernel-trace --stats for
 device times."""
 import os
 import sys
@@ -20,7 +20,7 @@ w = (torch.randn(384, 256, generator=g) / 16).cuda()
 bias = torch.randn(384, generator=g).cuda()
 ref = torch.rand(B, S, 4, 2, generator=g).cuda()
 lib = _native.lib()
-for flags in (0, 8192, 32768, 0):
+for flags in (0, 8192, 0, 8192):
     lib.kinet_gemm_set_flags(flags)
     for _ in range(3):
         K.msda_sample_records(x, w, bias, 8, ref, shapes, x_add=pos)
