@@ -69,7 +69,15 @@ class HungarianMatcher(nn.Module):
         sizes = [len(v["boxes"]) for v in targets]
         offsets = np.cumsum([0] + sizes[:-1])
         tq = [i for i, t in enumerate(targets) if 'track_query_match_ids' in t]
-        costs = torch.stack([self.cost_matrix(o, targets) for o in outputs_list])
+        shapes = {(tuple(o["pred_logits"].shape), tuple(o["pred_boxes"].shape)) for o in outputs_list}
+        if len(outputs_list) > 1 and len(shapes) == 1:
+            # every set in one cost computation (the same element-wise ops and per-pair L1 /
+            # GIoU, S x fewer launches): rows (set, image, query)
+            S, (bsz, nq) = len(outputs_list), outputs_list[0]["pred_logits"].shape[:2]
+            both = {k: torch.cat([o[k] for o in outputs_list]) for k in ("pred_logits", "pred_boxes")}
+            costs = self.cost_matrix(both, targets).view(S, bsz, nq, -1)
+        else:
+            costs = torch.stack([self.cost_matrix(o, targets) for o in outputs_list])
         extra = []
         if tq:
             masks = torch.stack([torch.stack([targets[i]['track_queries_fal_pos_mask'],
