@@ -14,7 +14,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 from torch import nn
 
-from kinet_amd.models.misc import box_cxcywh_to_xyxy, generalized_box_iou
+from kinet_amd.models.misc import box_cxcywh_to_xyxy, generalized_box_iou, host_to_device
 
 
 def sigmoid_focal_loss(inputs, targets, num_boxes, alpha: float = 0.25, gamma: float = 2):
@@ -119,7 +119,7 @@ class SetCriterion(nn.Module):
         """detr.py:705-717."""
         pred_logits = outputs['pred_logits']
         device = pred_logits.device
-        tgt_lengths = torch.as_tensor([len(v["labels"]) for v in targets], device=device)
+        tgt_lengths = host_to_device([len(v["labels"]) for v in targets], torch.long, device)
         card_pred = (pred_logits.argmax(-1) != pred_logits.shape[-1] - 1).sum(1)
         return {'cardinality_error': F.l1_loss(card_pred.float(), tgt_lengths.float())}
 

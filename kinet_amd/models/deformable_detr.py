@@ -341,8 +341,14 @@ class DeformableDETR(nn.Module):
                     src_list.append(src)
                     mask_list.append(m)
                     pos_list.append(pos_l[:, frame] if three_d else pos_l)
+        # padding known from the host-side image sizes (nested_tensor_from_tensor_list pads to the
+        # largest image, so equal sizes mean all-False masks): no device -> host mask check
+        size_sets = [getattr(samples, 'sizes', None)]
+        if self.multi_frame_attention:
+            size_sets.append(getattr(prev_features[0], 'sizes', None))
+        padded = None if any(z is None for z in size_sets) else any(len(set(z)) > 1 for z in size_sets)
         hs, memory, init_reference, inter_references, _, _ = self.transformer(
-            src_list, mask_list, pos_list, self.query_embed.weight, targets)
+            src_list, mask_list, pos_list, self.query_embed.weight, targets, padded=padded)
         outputs_classes, outputs_coords = [], []
         for lvl in range(hs.shape[0]):
             reference = init_reference if lvl == 0 else inter_references[lvl - 1]

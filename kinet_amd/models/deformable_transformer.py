@@ -30,7 +30,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 
 from kinet_amd import autograd as A
 from kinet_amd import kernels as K
-from kinet_amd.models.misc import inverse_sigmoid
+from kinet_amd.models.misc import host_to_device, inverse_sigmoid
 from kinet_amd.msda import MSDeformAttn, value_dtype_for
 
 
@@ -154,7 +154,7 @@ class DeformableTransformerEncoder(nn.Module):
             shapes_host = shapes_host or [tuple(int(v) for v in s) for s in shapes]
             reference_points = self.get_reference_points(shapes, valid_ratios, device=src.device)
         if not torch.is_tensor(spatial_shapes):
-            spatial_shapes = torch.as_tensor(spatial_shapes, dtype=torch.long, device=src.device)
+            spatial_shapes = host_to_device(spatial_shapes, torch.long, src.device)
         for layer in self.layers:
             output = layer(output, pos, reference_points, spatial_shapes, padding_mask, query_order=query_order,
                            shapes_host=shapes_host)
@@ -385,22 +385,29 @@ class DeformableTransformer(nn.Module):
         valid_ratios = torch.stack([self.get_valid_ratio(m) for m in masks], 1)
         return src_flatten, mask_flatten, lvl_pos_embed_flatten, spatial_shapes, valid_ratios
 
-    def forward(self, srcs, masks, pos_embeds, query_embed=None, targets=None):
+    def forward(self, srcs, masks, pos_embeds, query_embed=None, targets=None, padded=None):
         src_flatten, mask_flatten, lvl_pos, shapes, valid_ratios = self.prepare_inputs(srcs, masks, pos_embeds)
         if fast_path(self):
             dt = srcs[0].dtype
             src_flatten = src_flatten.to(dt).contiguous()
             lvl_pos = lvl_pos.to(dt).contiguous()
-        geo = self.geometry(shapes, valid_ratios, mask_flatten, src_flatten.device)
+        geo = self.geometry(shapes, valid_ratios, mask_flatten, src_flatten.device, padded)
         return self.forward_flat(src_flatten, lvl_pos, geo, query_embed, targets)
 
-    def geometry(self, shapes, valid_ratios, mask_flatten, device):
-        """Everything that depends only on the level shapes and padding masks."""
+    def geometry(self, shapes, valid_ratios, mask_flatten, device, padded=None):
+        """Everything that depends only on the level shapes and padding masks.  padded: whether
+        any frame is padded when the caller knows it from the host-side image sizes (None: ask
+        the mask, one device -> host sync)."""
         L = len(shapes)
         geo = {'shapes': [tuple(int(v) for v in s) for s in shapes], 'valid_ratios': valid_ratios}
-        geo['spatial_shapes'] = torch.as_tensor(geo['shapes'], dtype=torch.long, device=device)
+        geo['spatial_shapes'] = host_to_device(geo['shapes'], torch.long, device)
         geo['mask_flatten'] = mask_flatten
-        geo['pad_mask'] = mask_flatten if (mask_flatten is not None and bool(mask_flatten.any())) else None
+        if mask_flatten is None or padded is False:
+            geo['pad_mask'] = None
+        elif padded:
+            geo['pad_mask'] = mask_flatten
+        else:
+            geo['pad_mask'] = mask_flatten if bool(mask_flatten.any()) else None
         if self.multi_frame_attention_separate_encoder:
             half = L // 2
             s_half = sum(h * w for h, w in geo['shapes'][:half])

@@ -77,6 +77,16 @@ def nested_tensor_from_tensor_list(tensor_list: List[Tensor]):
     return NestedTensor(tensor, mask, sizes)
 
 
+def host_to_device(values, dtype, device):
+    """A small host list / array as a device tensor without a host-side wait: a plain
+    torch.as_tensor(..., device=cuda) copies from pageable memory and synchronises the stream,
+    which drains the queue the host is running ahead of."""
+    t = torch.as_tensor(values, dtype=dtype)
+    if torch.device(device).type != 'cuda':
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def inverse_sigmoid(x, eps=1e-5):
     if x.is_cuda and x.dtype == torch.float32:
         # one HIP kernel each way (csrc/train_ops.hip) instead of 6 / 8 torch launches
