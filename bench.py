@@ -488,10 +488,12 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
     # roofline pass: HIP events around every launch of 3 more steps, one stream (the traced
     # kernel durations must not overlap)
     _native.trace_begin()
-    for _ in range(3):
-        with torch.no_grad():
-            model(samples, *extra[0])
-    trace = _native.trace_end()
+    try:
+        for _ in range(3):
+            with torch.no_grad():
+                model(samples, *extra[0])
+    finally:
+        trace = _native.trace_end()
     torch.cuda.synchronize()
     fam, msda = summarize_trace(trace, 3)
     dec_touched = decoder_touched_bytes(model, samples, extra[0]) if name == 'config2' else None

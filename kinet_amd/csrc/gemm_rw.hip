@@ -49,14 +49,16 @@ struct RwCfg {
     static constexpr int R_OFF = A_BYTES + A2_BYTES;
     static constexpr int MASK_OFF = R_OFF + R_BYTES;
     static constexpr int REF_OFF = MASK_OFF + 1024;         // PREP: the tile's reference points
-    static constexpr int STAGE = REF_OFF + (PREP ? 1024 : 0);   // + one DMA of row-mask bytes (+ refs)
+    static constexpr int REF_OPS = PREP ? BMR / 16 : 0;     // 1 KiB DMAs: BMR rows x 4 levels x <= 16 B
+    static constexpr int STAGE = REF_OFF + REF_OPS * 1024;  // + one DMA of row-mask bytes (+ refs)
     static constexpr int PAR = 4 * GW * 4;                  // scale, bias, gamma, beta (f32)
     static constexpr int LNS = LN ? 2 * BMR * 4 * 4 : 0;    // [2][BMR][4 waves] partial sums
     static constexpr int BYTES = PAR + LNS + NS * STAGE;
     static constexpr int A_OPS = A_BYTES / 4096;            // DMA instructions per thread per tile
     static constexpr int R_OPS = R_BYTES / 4096;
-    static constexpr int D = A_OPS * (HAS_A2 ? 2 : 1) + R_OPS + 1 + (PREP ? 1 : 0);
-    static_assert(!PREP || (NT == 3 && BMR == 16 && !HAS_R && !LN), "sampling records: 12 columns per lane, 16-row tiles");
+    static constexpr int D = A_OPS * (HAS_A2 ? 2 : 1) + R_OPS + 1 + REF_OPS;
+    static_assert(!PREP || (NT == 3 && (BMR == 16 || BMR == 32) && !HAS_R && !LN),
+                  "sampling records: 12 columns per lane, 16- or 32-row tiles");
     static_assert(A_BYTES % 4096 == 0 && R_BYTES % 4096 == 0, "whole DMA rounds per tile");
     static_assert((CPR & (CPR - 1)) == 0 && (!HAS_R || (R_CPR & (R_CPR - 1)) == 0), "power-of-two rows");
     static_assert(BMR / 16 <= 64, "mask DMA lanes");
@@ -205,7 +207,7 @@ __device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_
 // pack_image_kwfold_kernel): K = KH*Cin, logical chunk q of the row = 8 channels of tap
 // kh = q / (Cin/8) read from input row oh*stride - pad + kh (zeros outside the image and past K)
 template <typename T, typename TO, int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2, bool CR,
-          bool PREP = false, int OCC = 2>
+          bool PREP = false, int OCC = 2, int DIAG = 0>
 __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, const int n_mtiles) {
     using C_ = RwCfg<KC, NT, BMR, NS, HAS_R, LN, HAS_A2, PREP>;
     constexpr int TMR = BMR / 16;             // 16-row MFMA tiles per row tile
@@ -334,8 +336,11 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
         // wave writes the same bytes, rows past M read 0)
         if constexpr (PREP) {
             const unsigned rbytes = (unsigned)(BMR * 16 * p.prep_refd);
-            dma16(rf, st + C_::REF_OFF, (unsigned)lane * 16u < rbytes ? (unsigned)m0 * 16u * (unsigned)p.prep_refd +
-                                                                         (unsigned)lane * 16u : OOB);
+#pragma unroll
+            for (int j = 0; j < C_::REF_OPS; ++j) {
+                const unsigned o = (unsigned)(j * 1024 + lane * 16);
+                dma16(rf, st + C_::REF_OFF + j * 1024, o < rbytes ? (unsigned)m0 * 16u * (unsigned)p.prep_refd + o : OOB);
+            }
         }
     };
 
@@ -452,6 +457,14 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
                 for (int a = 0; a < NT; ++a) Mma<T>::run(acc[a][t], wf[a][c], xf);
             }
 
+        if constexpr (DIAG == 1) {   // diagnostic: 32 idle wait states between the MFMAs and the epilogue
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+        } else if constexpr (DIAG == 2) {   // diagnostic: every wave's memory traffic retired first
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
         // ---- epilogue (registers) ----
         float v[TMR][NC];
         if constexpr (PREP) {
@@ -539,7 +552,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
 }
 
 template <typename T, typename TO, int KC, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2 = false, int NT = 4,
-          bool CR = false, bool PREP = false, int OCC = 2>
+          bool CR = false, bool PREP = false, int OCC = 2, int DIAG = 0>
 void launch_cfg(const GemmArgs& a, hipStream_t stream) {
     constexpr int GW = 4 * NT * 16;
     const int n_mtiles = (a.M + BMR - 1) / BMR;
@@ -552,7 +565,7 @@ void launch_cfg(const GemmArgs& a, hipStream_t stream) {
     int P = slots / ng >= 8 ? slots / ng / 8 * 8 : slots / ng;
     if (P > n_mtiles) P = n_mtiles;
     dim3 grid(P, ng), block(256);
-    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR, PREP, OCC>), grid, block, 0, stream,
+    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR, PREP, OCC, DIAG>), grid, block, 0, stream,
                        a, n_mtiles);
 }
 
@@ -730,6 +743,15 @@ extern "C" int kinet_msda_sample_records(const void* A, const void* A2, const vo
     // vs 1304 / 1299 frames/s, profiles/r04z_occ_ab.log) -- the smaller LDS footprint leaves room
     // for the other streams' workgroups.  Four per CU (128 VGPRs) spills and loses 7 %.  Flag
     // 8192: the two-workgroup ring.
+    // diagnostic (round 5): the 32-row records tile that differed from the 16-row tile in round 4
+    // (flag 16384; + 32768: idle wait states before the epilogue; + 65536: traffic drained first)
+    if ((kinet_gemm_flags & 16384) && A2 && in_dtype == KINET_BF16) {
+        if (kinet_gemm_flags & 32768) launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2, 1>(a, s);
+        else if (kinet_gemm_flags & 65536) launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2, 2>(a, s);
+        else launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2>(a, s);
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
     if (!(kinet_gemm_flags & 8192) && A2) {
         if (in_dtype == KINET_BF16) launch_cfg<bf16_t, f16_t, 8, 16, 2, false, false, true, 3, false, true, 3>(a, s);
         else launch_cfg<f16_t, f16_t, 8, 16, 2, false, false, true, 3, false, true, 3>(a, s);

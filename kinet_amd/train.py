@@ -205,19 +205,24 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # every step timed on its own (device synchronised on both sides; the step already syncs
-    # with the host 3 times for the matcher / sampler copies): the median over >= 10 steps is
-    # the reported rate, so one slow step (allocator growth, a host hiccup) cannot move it
-    per_step = []
+    # the reported rate: K steps back to back (no extra synchronisation between them, so host
+    # work of step i+1 overlaps the device tail of step i as in a real training loop), elapsed
+    # time max over ranks -> value = frames / elapsed
     t0 = time.perf_counter()
     for _ in range(steps):
-        ts = time.perf_counter()
         loss = step()
-        torch.cuda.synchronize()
-        per_step.append(time.perf_counter() - ts)
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # a separate pass with every step timed on its own (device synchronised on both sides): the
+    # median / min / max describe the spread; they are not the reported value
+    per_step = []
+    for _ in range(steps):
+        ts = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        per_step.append(time.perf_counter() - ts)
     if world > 1:
         t = torch.tensor([el] + per_step, device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -236,8 +241,10 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
     # backward rooflines: HIP events around every kinet launch of one more step (one stream)
     from kinet_amd import _native
     _native.trace_begin()
-    step()
-    trace = _native.trace_end()
+    try:
+        step()
+    finally:
+        trace = _native.trace_end()
     torch.cuda.synchronize()
     rooflines = train_rooflines(trace)
     frames = batch * steps * world
@@ -254,10 +261,12 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
             pg += ' (RCCL all-reduce)'
     return {'metric': 'train frames/sec (config 4: mot17 deformable multi_frame tracking, 3x%dx%d pairs)'
                       % (height, width),
-            'value': fpstep / med, 'unit': 'frames/s', 'images_per_s': 2 * fpstep / med, 'n_gpus': world,
-            'steps': steps, 'warmup': warmup, 's_per_step': med, 's_per_step_median': med,
-            's_per_step_mean': el / steps, 's_per_step_min': min(per_step), 's_per_step_max': max(per_step),
-            'frames_per_s_mean': frames / el, 'rate_basis': 'median of the per-step times (max over ranks)',
+            'value': frames / el, 'unit': 'frames/s', 'images_per_s': 2 * frames / el, 'n_gpus': world,
+            'steps': steps, 'warmup': warmup, 's_per_step': el / steps, 's_per_step_mean': el / steps,
+            's_per_step_median_synced': med, 's_per_step_min_synced': min(per_step),
+            's_per_step_max_synced': max(per_step), 'frames_per_s_median_synced': fpstep / med,
+            'rate_basis': 'frames of all ranks / elapsed time of K back-to-back steps (max over ranks); the '
+                          '*_synced fields come from a second pass with each step synchronised and timed alone',
             'loss': float(loss), 'scaling': 'weak',
             'host_glue': {'ms_per_step': glue['glue_s'] / 2 * 1e3,
                           'device_wait_ms_per_step': glue['sync_wait_s'] / 2 * 1e3,

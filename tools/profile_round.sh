@@ -3,7 +3,8 @@
 #   1. rocprofv3 --kernel-trace --stats of the default bench command (config 2 headline +
 #      config-5 sub-run + config-4 train leg) -> gpurun_out/<tag>_kernel_stats.csv
 #   2. per workload (config2, config5) two PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs,
-#      no trace domains beside --pmc) of that workload ALONE (--no-train --no-config5)
+#      --pmc with --kernel-trace only: no sys / runtime / hip / hsa / memory-copy trace domains)
+#      of that workload ALONE (--no-train --no-config5)
 #      -> gpurun_out/<tag>_<wl>_pmc_{fetch,write}.json -> per-launch HBM bytes merged into
 #      gpurun_out/pmc_traffic.json under '<wl>:<kernel>' (also copied to profiles/ of this
 #      snapshot so step 3 reads it)
