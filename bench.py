@@ -7,7 +7,7 @@ iterative box refinement, 91 focal logits) on synthetic 3x800x1333 frames, bf16 
 all kernels hand-written HIP (kinet_amd).  One step = one detection forward over a batch
 of `--batch` frames per GPU whose pixels are already resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload config2|config5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload config2|config3|config5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (driver)
 
 `--workload config5` (BASELINE.json configs[4], cfgs/train_full_res.yaml): ResNet-101,
@@ -41,11 +41,19 @@ MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'f16': 2500.0, 'f32': 157.3}   # dense
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command
 # (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950 per MI355X_MICROARCH.md "HBM")
 PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
+# MFMA-pipe utilisation per kernel group from a rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE
+# pass over the config-2 forward (tools/pmc_mfma.py)
+PMC_MFMA = os.path.join(HERE, 'profiles', 'pmc_mfma.json')
 
 WORKLOADS = {
     'config2': dict(cfgs=('train_deformable',), over={}, h=800, w=1333, batch=16, streams=3, dtype='bf16',
                     K=0, desc='config2 cfgs/train_deformable.yaml: R-50 Deformable-DETR inference forward, '
                               'd=256, 4 levels, 6/6 layers, 300 queries, box refine'),
+    'config3': dict(cfgs=('train_deformable', 'train_multi_frame', 'train_tracking'), over=dict(dataset='mot'),
+                    h=800, w=1333, batch=8, streams=2, dtype='bf16', K=40,
+                    desc='config3 tracking forward (cfgs/train_tracking.yaml on the multi-frame d=288 stack): R-50, '
+                         '500 object + 40 track queries, separate per-frame encoders (L=4), 8-level decoder, '
+                         'prev-frame features resident, 800x1333 frame pairs'),
     'config5': dict(cfgs=('train_deformable', 'train_multi_frame', 'train_tracking', 'train_full_res'),
                     over=dict(dataset='mot', backbone='resnet101'), h=1080, w=1920, batch=4, streams=2, dtype='f16',
                     K=20, desc='config5 cfgs/train_full_res.yaml: R-101 multi-frame tracking forward, d=288, '
@@ -69,7 +77,9 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-train', action='store_true', help='skip the config-4 training sub-benchmark')
     ap.add_argument('--no-config5', action='store_true', help='skip the config-5 sub-benchmark of the default line')
+    ap.add_argument('--no-config3', action='store_true', help='skip the config-3 sub-benchmark of the default line')
     ap.add_argument('--config5-steps', type=int, default=8)
+    ap.add_argument('--config3-steps', type=int, default=8)
     ap.add_argument('--train-steps', type=int, default=10)
     ap.add_argument('--cpu-seconds', type=float, default=20.0, help='bound on the CPU baseline sample')
     ap.add_argument('--ffn-knob', type=int, default=0,
@@ -334,6 +344,19 @@ def pmc_traffic(key):
         return None, None
 
 
+def pmc_mfma_util():
+    """Counter-measured MFMA busy fraction of the committed pass (groups + provenance), or None."""
+    try:
+        with open(PMC_MFMA) as f:
+            d = json.load(f)
+        return {'groups': d['groups'], 'source': d.get('source'),
+                'definition': 'SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) over the group\'s '
+                              'dispatches: the fraction of matrix-core cycles kept busy (1.0 = the dense peak '
+                              'at the clock the kernels ran)'}
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_model():
     try:
         with open('/proc/cpuinfo') as f:
@@ -585,6 +608,20 @@ def main():
               'roofline_gemm_conv_split': split5,
               'device_ms_per_step_by_family': {k: round(v['ms'], 4) for k, v in fam5.items()}}
 
+    # config 3 (BASELINE configs[2], the tracking forward on the d=288 stack at 800x1333) the same way
+    c3 = None
+    if a.workload == 'config2' and not a.no_config3:
+        w3 = WORKLOADS['config3']
+        el3, fam3, msda3, split3, _ = run_workload(a, 'config3', dev, world, rank, w3['batch'], w3['streams'],
+                                                   w3['h'], w3['w'], w3['dtype'], a.config3_steps, 2)
+        c3 = {'workload': w3['desc'], 'value': w3['batch'] * a.config3_steps * world / el3, 'unit': 'frames/s',
+              'frames_per_gpu_per_step': w3['batch'], 'in_flight_batches': w3['streams'],
+              'frame': [3, w3['h'], w3['w']], 'dtype': w3['dtype'], 'steps': a.config3_steps, 'warmup': 2,
+              'ms_per_step': el3 / a.config3_steps * 1e3,
+              'roofline': msda_roofline('config3', msda3, None),
+              'roofline_gemm_conv_split': split3,
+              'device_ms_per_step_by_family': {k: round(v['ms'], 4) for k, v in fam3.items()}}
+
     # config-4 training step (BASELINE configs[3]): every rank runs the DDP step, gradients
     # all-reduced over RCCL -- the path whose 1 -> 8 GPU scaling north_star targets
     train = None
@@ -613,7 +650,8 @@ def main():
                      'achieved': mfma_ach, 'peak': MFMA_PEAK_TFLOPS[dt_name], 'unit': 'TFLOP/s',
                      'frac': mfma_ach / MFMA_PEAK_TFLOPS[dt_name], 'traffic': None,
                      'algorithmic_flops_per_frame': mfma_flops / a.batch,
-                     'device_ms_per_step': mfma_ms}
+                     'device_ms_per_step': mfma_ms,
+                     'pmc_mfma_util': pmc_mfma_util() if a.workload == 'config2' else None}
         roofline = msda_roof or mfma_roof
         line = {
             'metric': 'frames/sec (3x800x1333, 300 obj+track queries) at 1/2/4/8 GPUs; MSDeformAttn ms/call',
@@ -631,6 +669,7 @@ def main():
             'roofline_gemm_conv_split': split,
             'msda_ms_per_call': {'encoder': msda_enc_ms, 'decoder': msda_dec_ms},
             'device_ms_per_step_by_family': {k: round(v['ms'], 4) for k, v in fam.items()},
+            'config3': c3,
             'config5': c5,
             'cpu_baseline': cpu,
             'train': train,

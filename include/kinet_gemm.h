@@ -82,6 +82,17 @@ int kinet_gemm_headmajor_ex(const void* A, const void* A2, const void* B, void* 
                             const uint8_t* row_mask, int rows_per_batch, int head_dim,
                             kinet_stream_t stream);
 
+/* Split head-major store (round 5, the head_dim-36 MSDA value of configs 3-5): the weight rows
+ * are ordered [every head's first head_dim channels | every head's last tail_dim channels];
+ * columns [0, split_cols) go head-major (split_cols/head_dim, B, S, head_dim) to C and columns
+ * [split_cols, N) head-major (heads, B, S, tail_dim) right after that plane, at
+ * C + split_cols*M elements.  kinet_msda_encoder_forward_split reads the two planes.  Replaces
+ * the value_proj + view of ms_deform_attn.py:64-66 for that kernel. */
+int kinet_gemm_headmajor_split(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                               int in_dtype, int out_dtype, const float* bias, const uint8_t* row_mask,
+                               int rows_per_batch, int head_dim, int split_cols, int tail_dim,
+                               kinet_stream_t stream);
+
 /* Split-K forms for small-M / long-K problems (few output tiles): K is cut into `ksplit`
  * slices (rounded to whole 64-element K-steps) whose f32 partial tiles go to `workspace`
  * (ksplit * M * N floats, caller-allocated), then one finalize pass sums the slices and

@@ -178,6 +178,33 @@ int kinet_msda_encoder_forward_records(const void* value, int64_t value_sb, int6
                                        int num_levels, int num_query, int num_point, int output_dtype,
                                        const int32_t* query_tile_order, kinet_stream_t stream);
 
+/* Which kernel the calling thread's last kinet_msda_backward launched: 1 = msda_bwd_list_kernel
+ * (grad_value rows summed on chip), 0 = msda_bwd_kernel (per-corner atomics), -1 = none (an
+ * empty call, or no call yet).  Host-side bookkeeping for the rooflines; no GPU call. */
+int kinet_msda_backward_last_kernel(void);
+
+/* Head_dim-36 encoder calls (configs 3-5, d = 288: cfgs/train_multi_frame.yaml:2) on the strip
+ * kernel: the value in TWO head-major planes written by kinet_gemm_headmajor_split --
+ * value_main (M, N, S, 32) f16 (channels 0-31 of each head; strides as value_sb / value_sm of
+ * kinet_msda_encoder_forward) and value_tail (M, N, S, 4) f16 (channels 32-35, 8 bytes per
+ * pixel; tail_sb / tail_sm in elements) -- so the 32-channel part runs the D = 32 sampling
+ * unchanged and each quad of lanes adds the 4 tail channels (one 8-byte corner read per lane
+ * per sample, tail map staged in LDS beside the main map).  channels must be 36; offsets /
+ * logits head-major as kinet_msda_encoder_forward; output (N, Lq, M*36).  Same sampling as
+ * ms_deform_im2col_cuda.cuh:165-237 for any channel count. */
+int kinet_msda_encoder_forward_split(const void* value_main, int64_t main_sb, int64_t main_sm,
+                                     const void* value_tail, int64_t tail_sb, int64_t tail_sm,
+                                     const int64_t* spatial_shapes_host, const void* offsets_logits_hm,
+                                     const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
+                                     void* output, int batch, int spatial_size, int num_heads, int channels,
+                                     int num_levels, int num_query, int num_point, int output_dtype,
+                                     const int32_t* query_tile_order, kinet_stream_t stream);
+
+/* kinet_msda_encoder_plan for head_dim `channels` (32, or 36: the split kernel, whose LDS map
+ * holds 72 bytes per staged pixel). */
+int kinet_msda_encoder_plan_ex(const int64_t* spatial_shapes_host, int batch, int num_heads, int num_query,
+                               int channels, int32_t* plan_out);
+
 #ifdef __cplusplus
 }
 #endif

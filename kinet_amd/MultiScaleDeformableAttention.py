@@ -72,15 +72,15 @@ def ms_deform_attn_backward(value, spatial_shapes, sampling_loc, attn_weight, gr
     grad_attw = torch.empty_like(attn_weight)
     ws_bytes = _n.lib().kinet_msda_backward_workspace_bytes(N, S, M, D, _n.dtype_code(value.dtype))
     ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=value.device) if ws_bytes else None
+    work = {'family': 'msda_bwd', 'Lq': Lq, 'S': S,
+            # SURVEY 8(d) B_bwd: value + grad_out + loc/attw + f32 grad_value + grad loc/attw
+            'bytes': (N * S * M * D * value.element_size() + N * Lq * M * D * grad_output.element_size()
+                      + 12 * N * Lq * M * L * P + 4 * N * S * M * D + 12 * N * Lq * M * L * P)}
     _n.call('kinet_msda_backward', _n.ptr(value), _n.ptr(spatial_shapes), _n.ptr(sampling_loc),
             _n.ptr(attn_weight), _n.ptr(grad_output), _n.ptr(grad_value), _n.ptr(grad_loc),
             _n.ptr(grad_attw), _n.ptr(ws), N, S, M, D, L, Lq, P, int(im2col_step),
-            _n.dtype_code(value.dtype), _n.dtype_code(sampling_loc.dtype), _n.stream(value.device),
-            work={'family': 'msda_bwd', 'Lq': Lq, 'S': S,
-                  # the launcher's choice (csrc/msda.hip): encoder calls (Lq == S) sum grad_value
-                  # rows on chip, the others scatter per corner
-                  'kernel': 'msda_bwd_list_kernel' if Lq == S else 'msda_bwd_kernel',
-                  # SURVEY 8(d) B_bwd: value + grad_out + loc/attw + f32 grad_value + grad loc/attw
-                  'bytes': (N * S * M * D * value.element_size() + N * Lq * M * D * grad_output.element_size()
-                            + 12 * N * Lq * M * L * P + 4 * N * S * M * D + 12 * N * Lq * M * L * P)})
+            _n.dtype_code(value.dtype), _n.dtype_code(sampling_loc.dtype), _n.stream(value.device), work=work)
+    # the launcher's own choice (csrc/msda.hip): the list kernel sums grad_value rows on chip
+    work['kernel'] = {1: 'msda_bwd_list_kernel', 0: 'msda_bwd_kernel'}.get(
+        _n.lib().kinet_msda_backward_last_kernel(), 'none')
     return [grad_value, grad_loc, grad_attw]

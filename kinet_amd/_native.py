@@ -24,8 +24,11 @@ _SIGS = {
     'kinet_msda_backward_workspace_bytes': [I] * 5,
     'kinet_msda_backward_tune': [I] * 5,
     'kinet_msda_backward_debug': [I],
+    'kinet_msda_backward_last_kernel': [],
     'kinet_msda_encoder_forward': [P, I64, I64, P, P, P, I, P, P] + [I] * 8 + [P, P],
     'kinet_msda_encoder_plan': [P, I, I, I, P],
+    'kinet_msda_encoder_plan_ex': [P, I, I, I, I, P],
+    'kinet_msda_encoder_forward_split': [P, I64, I64, P, I64, I64, P, P, P, I, P, P] + [I] * 8 + [P, P],
     'kinet_msda_sample_records': [P, P, P, P, I, I, I, I, I, P, I, P, P, I, I, I, P, P],
     'kinet_msda_encoder_forward_records': [P, I64, I64, P, P, I, P] + [I] * 8 + [P, P],
     'kinet_msda_fused_forward': [P, I64, I64, I64, P, P, I, P, I, P, P, P, P] + [I] * 10 + [P, P],
@@ -33,6 +36,7 @@ _SIGS = {
     'kinet_gemm_force_tile': [I, I],
     'kinet_gemm_headmajor': [P, P, P] + [I] * 7 + [P, P, I, I, P],
     'kinet_gemm_headmajor_ex': [P, P, P, P] + [I] * 7 + [P, P, I, I, P],
+    'kinet_gemm_headmajor_split': [P, P, P] + [I] * 7 + [P, P, I, I, I, I, P],
     'kinet_gemm': [P, P, P] + [I] * 7 + [P, P, P, I, I, I, P, I, P],
     'kinet_gemm_ex': [P, P, P, P] + [I] * 7 + [P, P, P, I, I, P, P, F, I, P, P],
     'kinet_conv2d': [P, P, P] + [I] * 12 + [P, P, P, I, I, I, P],

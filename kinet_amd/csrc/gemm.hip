@@ -209,8 +209,14 @@ __device__ __forceinline__ void epilogue_rows(const GemmArgs& p, const float* ep
             TO* dst;
             if (p.hm_rows) {
                 const int bb = m / p.hm_rows, ss = m - bb * p.hm_rows;
-                const int g = n / p.hm_d, dd = n - g * p.hm_d;
-                dst = C + (((long)g * p.hm_batch + bb) * p.hm_rows + ss) * p.hm_d + dd;
+                if (p.hm_split && n >= p.hm_split) {   // the tail plane (4-column groups never straddle)
+                    const int n2 = n - p.hm_split, g = n2 / p.hm_d2, dd = n2 - g * p.hm_d2;
+                    dst = C + (long)p.hm_split * p.hm_batch * p.hm_rows +
+                          (((long)g * p.hm_batch + bb) * p.hm_rows + ss) * p.hm_d2 + dd;
+                } else {
+                    const int g = n / p.hm_d, dd = n - g * p.hm_d;
+                    dst = C + (((long)g * p.hm_batch + bb) * p.hm_rows + ss) * p.hm_d + dd;
+                }
             } else {
                 dst = C + (long)m * p.ldc + n;
             }
@@ -487,7 +493,9 @@ int launch(const GemmArgs& a, hipStream_t stream) {
     // gains (DESIGN.md "GEMM / conv kernel"), so those keep the 4-wave tiles.  Flag 2 forces
     // them wherever eligible.
     int bm8 = 0, bn8 = 0;
-    if (sizeof(T) == 2 && a.A2 == nullptr && a.kchunk == 0 && a.M >= 4096 && a.N >= 128 && (!ln || a.N <= 256)) {
+    // (not for head-major stores: only gemm_kernel's epilogue writes them)
+    if (sizeof(T) == 2 && a.A2 == nullptr && a.kchunk == 0 && a.hm_rows == 0 && a.M >= 4096 && a.N >= 128 &&
+        (!ln || a.N <= 256)) {
         const int tn = (a.N > 128 || ln) ? 256 : 128;
         const long t = (long)((a.M + 255) / 256) * ((a.N + tn - 1) / tn);
         const double eff = (double)a.M * a.N / ((double)((t + 255) / 256) * 256.0 * 256.0 * tn);
@@ -798,6 +806,35 @@ extern "C" int kinet_gemm_headmajor_ex(const void* A, const void* A2, const void
     KINET_CHECK_ARG(ab < (1LL << 31) && bb < (1LL << 31), "gemm_headmajor: operand larger than 2 GiB");
     a.a_bytes = (int)ab;
     a.b_bytes = (int)bb;
+    return dispatch<false>(a, in_dtype, out_dtype, (hipStream_t)stream);
+}
+
+extern "C" int kinet_gemm_headmajor_split(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                                          int in_dtype, int out_dtype, const float* bias, const uint8_t* row_mask,
+                                          int rows_per_batch, int head_dim, int split_cols, int tail_dim,
+                                          kinet_stream_t stream) {
+    KINET_CHECK_ARG(out_dtype == in_dtype || (in_dtype == KINET_BF16 && out_dtype == KINET_F16),
+                    "gemm_headmajor_split: out_dtype must equal in_dtype (or f16 from bf16)");
+    KINET_CHECK_ARG(M >= 0 && N > 0 && K > 0, "gemm_headmajor_split: invalid sizes");
+    KINET_CHECK_ARG(rows_per_batch > 0 && M % rows_per_batch == 0, "gemm_headmajor_split: M must be batch*rows_per_batch");
+    KINET_CHECK_ARG(head_dim > 0 && head_dim % 4 == 0 && tail_dim > 0 && tail_dim % 4 == 0 && split_cols > 0 &&
+                        split_cols % head_dim == 0 && split_cols < N && (N - split_cols) % tail_dim == 0 &&
+                        split_cols / head_dim == (N - split_cols) / tail_dim,
+                    "gemm_headmajor_split: N = heads*head_dim + heads*tail_dim, dims multiples of 4");
+    KINET_CHECK_ARG(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K, "gemm_headmajor_split: bad K/lda/ldb");
+    KINET_CHECK_ARG(aligned16(A) && aligned16(B), "gemm_headmajor_split: A and B must be 16-byte aligned");
+    GemmArgs a{};
+    a.A = A; a.B = B; a.C = C; a.bias = bias; a.row_mask = row_mask;
+    a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = N;
+    a.hm_rows = rows_per_batch; a.hm_d = head_dim; a.hm_batch = M / rows_per_batch;
+    a.hm_split = split_cols; a.hm_d2 = tail_dim;
+    const long long es = (long long)dtype_size(in_dtype);
+    const long long ab = M > 0 ? ((long long)(M - 1) * lda + K) * es : 0;
+    const long long bb = ((long long)(N - 1) * ldb + K) * es;
+    KINET_CHECK_ARG(ab < (1LL << 31) && bb < (1LL << 31), "gemm_headmajor_split: operand larger than 2 GiB");
+    a.a_bytes = (int)ab;
+    a.b_bytes = (int)bb;
+    if (M == 0) return KINET_OK;
     return dispatch<false>(a, in_dtype, out_dtype, (hipStream_t)stream);
 }
 

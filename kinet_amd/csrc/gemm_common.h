@@ -28,6 +28,10 @@ struct GemmArgs {
     // head-major store (hm_rows > 0): row r = b*hm_rows + s, column n = g*hm_d + d goes to
     // C[((g*hm_batch + b)*hm_rows + s)*hm_d + d]  -- the MSDA value layout (heads, B, S, D)
     int hm_rows, hm_d, hm_batch;
+    // split head-major store (hm_split > 0): columns n >= hm_split go to a second plane after the
+    // first, C + hm_split*hm_batch*hm_rows, as ((g*hm_batch + b)*hm_rows + s)*hm_d2 + d with
+    // n - hm_split = g*hm_d2 + d -- the head_dim-36 MSDA value as a 32-channel plane + a 4-channel plane
+    int hm_split, hm_d2;
     int M, N, K, lda, ldb, ldc, ldr, relu;
     // split-K (gemm_kernel only): blockIdx.y = K slice of kchunk elements, whose f32 partial
     // tile goes to C + blockIdx.y * c_slice (no epilogue; splitk_finalize applies it)

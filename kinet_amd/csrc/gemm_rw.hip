@@ -587,6 +587,15 @@ void launch_ring(const GemmArgs& a, hipStream_t stream) {
     constexpr int BMR = (KC == 2 || (KC <= 8 && !HAS_R && !LN && !HAS_A2)) ? 32 : 16;
     constexpr int NS = ring_depth<KC, BMR, HAS_R, LN, HAS_A2, NT>();
     static_assert(NS >= 2, "LDS budget");
+    if constexpr (BMR == 32 && KC >= 4) {
+        // flag 131072 (tests): the same problem on 16-row tiles -- the 32-row tiles' two MFMA row
+        // tiles per wave (TMR = 2) must give the 16-row tiles' results bit for bit
+        if (kinet_gemm_flags & 131072) {
+            constexpr int NS16 = ring_depth<KC, 16, HAS_R, LN, HAS_A2, NT>();
+            launch_cfg<T, TO, KC, 16, NS16, HAS_R, LN, HAS_A2, NT>(a, stream);
+            return;
+        }
+    }
     launch_cfg<T, TO, KC, BMR, NS, HAS_R, LN, HAS_A2, NT>(a, stream);
 }
 
@@ -635,7 +644,7 @@ bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t strea
     if (!o16 && !o32) return false;
     if (o16 ? (a.ldc % 8 != 0) : (a.ldc % 4 != 0)) return false;
     if (!al16(a.C) || (a.R != nullptr && (!o16 || a.ldr % 8 != 0 || !al16(a.R)))) return false;
-    if (a.hm_rows && a.hm_d % 8 != 0) return false;
+    if (a.hm_rows && (a.hm_d % 8 != 0 || a.hm_split)) return false;
     // output descriptor extent (buffer stores; offsets must stay below 2^31)
     const long long osz = out_dtype == KINET_F32 ? 4 : 2;
     const long long cb = a.hm_rows ? (long long)a.M * a.N * osz
@@ -672,6 +681,12 @@ bool launch_rw_conv(const GemmArgs& a, int in_dtype, hipStream_t stream) {
         GemmArgs ac = a;
         ac.c_bytes = (int)cb;
         constexpr int NS = ring_depth<8, 32, false, false, false, 4>();
+        constexpr int NS16 = ring_depth<8, 16, false, false, false, 4>();
+        if (kinet_gemm_flags & 131072) {   // tests: 16-row tiles (bit-identical to the 32-row ones)
+            if (in_dtype == KINET_BF16) launch_cfg<bf16_t, bf16_t, 8, 16, NS16, false, false, false, 4, true>(ac, stream);
+            else launch_cfg<f16_t, f16_t, 8, 16, NS16, false, false, false, 4, true>(ac, stream);
+            return true;
+        }
         if (in_dtype == KINET_BF16) launch_cfg<bf16_t, bf16_t, 8, 32, NS, false, false, false, 4, true>(ac, stream);
         else launch_cfg<f16_t, f16_t, 8, 32, NS, false, false, false, 4, true>(ac, stream);
         return true;
@@ -684,6 +699,12 @@ bool launch_rw_conv(const GemmArgs& a, int in_dtype, hipStream_t stream) {
     GemmArgs ac = a;
     ac.c_bytes = (int)cb;
     constexpr int NS = ring_depth<8, 32, false, false, false>();
+    constexpr int NS16 = ring_depth<8, 16, false, false, false>();
+    if (kinet_gemm_flags & 131072) {   // tests: 16-row tiles (bit-identical to the 32-row ones)
+        if (in_dtype == KINET_BF16) launch_cfg<bf16_t, bf16_t, 8, 16, NS16, false, false, false, 2, true>(ac, stream);
+        else launch_cfg<f16_t, f16_t, 8, 16, NS16, false, false, false, 2, true>(ac, stream);
+        return true;
+    }
     if (in_dtype == KINET_BF16) launch_cfg<bf16_t, bf16_t, 8, 32, NS, false, false, false, 2, true>(ac, stream);
     else launch_cfg<f16_t, f16_t, 8, 32, NS, false, false, false, 2, true>(ac, stream);
     return true;

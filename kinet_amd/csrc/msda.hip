@@ -1219,6 +1219,9 @@ thread_local BwdTune bwd_tune = {0, 0, 0, 0, 0};
 // when set): 1 = phase 2 without its value loads, 2 = phase 3 without its global atomics,
 // 4 = no phase 3, 8 = no hash inserts (and so no phase-3 work)
 thread_local int bwd_dbg = 0;
+// the kernel the calling thread's last kinet_msda_backward launched (kinet_msda_backward_last_kernel):
+// 1 = msda_bwd_list_kernel (rows summed on chip), 0 = msda_bwd_kernel (per-corner atomics), -1 = none
+thread_local int bwd_last = -1;
 
 template <typename T, typename TL>
 int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const void* attw,
@@ -1293,6 +1296,7 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
         KINET_LAUNCH_CHECK();
     }
     }
+    bwd_last = hashed ? 1 : (N > 0 && Lq > 0 ? 0 : -1);
     if (hashed) {
     } else if (N > 0 && Lq > 0) {
         // groups padded to a power of two (reductions by shuffles instead of LDS atomics)
@@ -1494,6 +1498,8 @@ extern "C" int kinet_msda_backward(const void* value, const int64_t* spatial_sha
     set_error("msda backward: unsupported dtype pair value=%d loc=%d", value_dtype, loc_dtype);
     return KINET_ERR_ARG;
 }
+
+extern "C" int kinet_msda_backward_last_kernel(void) { return bwd_last; }
 
 extern "C" int kinet_msda_backward_debug(int flags) {
     const int old = bwd_dbg;

@@ -45,6 +45,12 @@ namespace {
 constexpr int EW = 16;             // waves per workgroup (one workgroup per CU)
 constexpr int EQT = 16;            // queries per wave tile
 constexpr int EMAP_PIX = 2544;     // LDS map pixels of 64 B (162,816 B; the level table fits beside)
+// head_dim 36 (TAIL): the value as a 32-channel plane + a 4-channel TAIL plane (8 B per pixel,
+// kinet_gemm_headmajor_split); the LDS map holds both, 72 B per pixel: 2261 main pixels, then the
+// tail map (pixel x at ETB + 8x, the same pixel indexing as the main map)
+constexpr int EMAP_T = 2261;
+constexpr int ETB = EMAP_T * 64;
+constexpr int EWT = 12;   // TAIL: waves per workgroup (3 per SIMD: the tail's registers need > 128 VGPRs)
 constexpr int EL = 4, EP = 4;      // levels, points (the configs' values; host-checked)
 constexpr int EREC = EL * EP * 3;  // head-major offsets/logits per query and head (48)
 constexpr int EHALO = 4;           // rows staged beyond a strip's query rows on each side
@@ -78,6 +84,10 @@ struct EncArgs {
     const f16_t* value;    // head map (b, m) at value + b*vsb + m*vsm, pixel rows of 32 f16
     long vsb, vsm;
     int head_bytes;        // bytes addressable from a head map's base (buffer range)
+    const f16_t* tail;     // TAIL: the 4-channel plane, head map (b, m) at tail + b*tsb + m*tsm
+    long tsb, tsm;
+    int tail_bytes;
+    int od;                // output channels per head (32, or 36 with the tail)
     int H[EL], W[EL];      // level shapes (host copy of spatial_shapes)
     int cap[EL], base[EL]; // the plan's LDS regions
     const f16_t* offlog;   // (M, B, Lq, 48) head-major
@@ -373,7 +383,30 @@ __device__ __forceinline__ void strip_rows(const EncArgs& a, const EncLevels& lv
     }
 }
 
-template <typename TO, int FL, int REFD, bool QM, bool REC>
+// TAIL (head_dim 36): the 4 tail channels of a query are summed by its quad too -- lane l1 takes
+// corner (row l1 >> 1, column l1 & 1) of every footprint: one 8-byte read of that pixel's 4 tail
+// channels per sample (vs four 16-byte main reads), two packed-f16 MACs with that corner's
+// weight, per-level f16 pair sums widened into 4 f32 accumulators; at the tile's end the quad's 4
+// corners are summed by two DPP steps and lane 0 of the quad stores the 4 channels
+__device__ __forceinline__ void tail_flush(float (&t)[4], const uint32_t (&th)[2]) {
+    constexpr uint32_t one = 0x3c003c00u;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        t[2 * j] = fma_mix16_lo_lo(t[2 * j], th[j], one);
+        t[2 * j + 1] = fma_mix16_hi_lo(t[2 * j + 1], th[j], one);
+    }
+}
+// the f16 weight of this lane's corner (row tr, column tc) in the low half
+__device__ __forceinline__ uint32_t tail_w(uint32_t w01, uint32_t w23, int tr, int tc) {
+    const uint32_t w = tr ? w23 : w01;
+    return __builtin_amdgcn_alignbyte(w, w, (uint32_t)tc * 2u);
+}
+__device__ __forceinline__ void tail_mac(uint32_t (&th)[2], uint2 v, uint32_t wq, bool first) {
+    th[0] = first ? pk_mul_lo(v.x, wq) : pk_fma_lo(th[0], v.x, wq);
+    th[1] = first ? pk_mul_lo(v.y, wq) : pk_fma_lo(th[1], v.y, wq);
+}
+
+template <typename TO, int FL, int REFD, bool QM, bool REC, bool TAIL, int NW>
 __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4v* vmap, int b, int m, int strip,
                                           int wave, int lane) {
     constexpr int NGL = FL;            // levels gathered through the texture path
@@ -393,9 +426,15 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
         __builtin_amdgcn_make_buffer_rsrc((void*)a.ref, (short)0, a.B * Lq * EL * REFD * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rq =
         __builtin_amdgcn_make_buffer_rsrc((void*)a.qmask, (short)0, a.qmask ? a.B * Lq : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, a.B * Lq * a.M * 64, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, a.B * Lq * a.M * a.od * 2, 0x00020000);
+    const char* tmap = TAIL ? reinterpret_cast<const char*>(a.tail + (long)b * a.tsb + (long)m * a.tsm) : hmap;
+    const __amdgpu_buffer_rsrc_t rt =
+        __builtin_amdgcn_make_buffer_rsrc((void*)tmap, (short)0, TAIL ? a.tail_bytes : 0, 0x00020000);
+    const int tr = l1 >> 1, tc = l1 & 1;   // TAIL: this lane's footprint corner
 
     const char* vm = reinterpret_cast<const char*>(vmap) + cb;
+    const char* vmb = reinterpret_cast<const char*>(vmap);
     RecK rk;
     if constexpr (REC) {
         const uint32_t fb = (uint32_t)a.fb;
@@ -421,12 +460,20 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
     int q0 = has ? tile_q0(t) : 0;
     uint32_t rec_o[EP], rec_w01[EP], rec_w23[EP];
     u32x4v g[EP][4];
+    uint2 gt[EP];   // TAIL: the gathered level's tail corner of each point
     // gathered level LV: its 4 points' records from quad lane LV, 16 corner loads in flight
     auto issue = [&](auto lvc) {
         constexpr int LV = decltype(lvc)::value;
 #pragma unroll
         for (int p = 0; p < EP; ++p) {
-            const uint32_t o = quad_bcast<LV>(rec_o[p]) + cb;
+            const uint32_t ob = quad_bcast<LV>(rec_o[p]);
+            const uint32_t o = ob + cb;
+            if constexpr (TAIL) {
+                // head-map offset / 8 = tail-plane offset of (hl, wl); an invalid sample's TAF
+                // offset lands past the tail plane's range (reads 0)
+                const uint32_t tco = (tr ? (uint32_t)wb[LV] >> 3 : 0u) + (uint32_t)tc * 8u;
+                gt[p] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rt, (ob >> 3) + tco, 0, 0));
+            }
             const uint32_t o1 = o + (uint32_t)wb[LV];
             g[p][0] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o, 0, 0));
             g[p][1] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o + 64u, 0, 0));
@@ -479,7 +526,7 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
     // outside the image: the range check's zeros) ----
     {
         const int npiece = (a.used + 15) >> 4;
-        for (int j = wave; j < npiece; j += EW) {
+        for (int j = wave; j < npiece; j += NW) {
             const int x = j * 16 + (lane >> 2);
             uint32_t off = TAF;
 #pragma unroll
@@ -493,6 +540,27 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(vmap + j * 64), 16,
                                                      off, 0, 0, 0);
         }
+        if constexpr (TAIL) {
+            // the tail map: dword pieces (one dword = half a pixel's 4 channels), 256 B per
+            // wave-instruction, the same pixel indexing and zero fill as the main map
+            const int ndw = (a.used * 2 + 63) >> 6;
+            for (int j = wave; j < ndw; j += NW) {
+                const int dw = j * 64 + lane;
+                const int x = dw >> 1;
+                uint32_t off = TAF;
+#pragma unroll
+                for (int l = FL; l < EL; ++l) {
+                    const int W = a.W[l];
+                    const int k = x - a.base[l] - 1;
+                    const int rel = ra_[l] * W + k;
+                    const bool in = k >= -1 && k <= a.cap[l] * W && rel >= 0 && rel < a.H[l] * W;
+                    off = in ? (uint32_t)(lv.start[l] + rel) * 8u + (uint32_t)(dw & 1) * 4u : off;
+                }
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rt, (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(vmap) + ETB + j * 256), 4, off,
+                    0, 0, 0);
+            }
+        }
     }
 
     if (has) {
@@ -504,7 +572,7 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (!has) return;
-    const int stride = EW;
+    const int stride = NW;
 #pragma unroll 1
     for (;;) {
         const int tn = t + stride;
@@ -516,6 +584,7 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
             load_tile<REFD, QM, REC>(in, ro, rr, rq, b, Lq, qn0 + (li >> 2), li & 3);
         }
         f32x2 acc[4] = {};
+        float tacc[4] = {0.f, 0.f, 0.f, 0.f};   // TAIL: this lane's corner of every sample
         // the gathered level: weights fetched from the quad again (registers are the limit)
         auto consume = [&](auto lvc) {
             constexpr int LV = decltype(lvc)::value;
@@ -527,6 +596,12 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
             }
             level_sum16(h, g, w01, w23);
             flush16<!LDS_FIRST && LV == 0>(acc, h);
+            if constexpr (TAIL) {
+                uint32_t th[2];
+#pragma unroll
+                for (int p = 0; p < EP; ++p) tail_mac(th, gt[p], tail_w(w01[p], w23[p], tr, tc), p == 0);
+                tail_flush(tacc, th);
+            }
         };
         // LDS level LV, one point at a time (8 VGPRs of corner data beside the gathers).  A
         // footprint outside the staged rows (record flag TAF) is gathered from the head map:
@@ -535,7 +610,7 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
         // branch, so the common path keeps its gathers in flight and holds no extra registers)
         // the level's f16 sums into h; the flush into acc follows the FAR / common branch merge,
         // so only h (not the 8 accumulators) crosses it
-        auto lds_level = [&](auto lvc, auto farc, uint32_t (&h)[4]) {
+        auto lds_level = [&](auto lvc, auto farc, uint32_t (&h)[4], uint32_t (&th)[2]) {
             constexpr int LV = decltype(lvc)::value;
             constexpr bool FAR = decltype(farc)::value;
 #pragma unroll
@@ -577,18 +652,34 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
                     h[j] = pk_fma_lo(h[j], v2[j], w23);
                     h[j] = pk_fma_hi(h[j], v3[j], w23);
                 }
+                if constexpr (TAIL) {
+                    // this lane's corner from the tail map (a far sample: from the tail plane)
+                    const uint32_t tco = (tr ? wrow >> 3 : 0u) + (uint32_t)tc * 8u;
+                    uint2 tv = *reinterpret_cast<const uint2*>(vmb + ETB + (lo >> 3) + tco);
+                    if (FAR && any_far) {
+                        if (far) {
+                            const uint32_t go = ((o & ~TAF) >> 3) - ((wrow >> 3) + 8u) + tco;
+                            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)"
+                                         : "+v"(tv)
+                                         : "v"(go), "s"(rt)
+                                         : "memory");
+                        }
+                    }
+                    tail_mac(th, tv, tail_w(w01, w23, tr, tc), p == 0);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
         auto lds_level_any = [&](auto lvc) {
             constexpr int LV = decltype(lvc)::value;
             const uint32_t f = quad_bcast<LV>(rec_o[0] | rec_o[1] | rec_o[2] | rec_o[3]);
-            uint32_t h[4];
+            uint32_t h[4], th[2];
             if (__builtin_amdgcn_ballot_w64((f & TAF) != 0u) != 0)
-                lds_level(lvc, std::true_type{}, h);
+                lds_level(lvc, std::true_type{}, h, th);
             else
-                lds_level(lvc, std::false_type{}, h);
+                lds_level(lvc, std::false_type{}, h, th);
             flush16<LDS_FIRST && LV == FL>(acc, h);
+            if constexpr (TAIL) tail_flush(tacc, th);
         };
         // LDS levels interleaved between the gathered levels' consumes (slot s: LDS levels
         // FL + [s*NLL/NST, (s+1)*NLL/NST))
@@ -602,6 +693,14 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
         });
         const int lis = lane_id_here();
         const int q = q0 + (lis >> 2);
+        if constexpr (TAIL) {
+            // the quad's 4 corners: two DPP steps (every lane active)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                tacc[i] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(tacc[i]), 0xB1, 0xf, 0xf, false));
+                tacc[i] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(tacc[i]), 0x4E, 0xf, 0xf, false));
+            }
+        }
         if (q < Lq) {
             VecT<TO, 8> o;
 #pragma unroll
@@ -609,8 +708,19 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
                 o.v[2 * j] = Cvt<TO>::from(acc[j][0]);
                 o.v[2 * j + 1] = Cvt<TO>::from(acc[j][1]);
             }
-            const uint32_t oo = ((uint32_t)(b * Lq + q) * (uint32_t)a.M * 32u + (uint32_t)m * 32u + (uint32_t)(lis & 3) * 8u) * 2u;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, o), rw, oo, 0, 0);
+            const uint32_t od = (uint32_t)a.od;
+            const uint32_t ob = ((uint32_t)(b * Lq + q) * (uint32_t)a.M + (uint32_t)m) * od;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, o), rw, (ob + (uint32_t)(lis & 3) * 8u) * 2u,
+                                                   0, 0);
+            if constexpr (TAIL) {
+                if ((lis & 3) == 0) {
+                    VecT<TO, 4> t;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) t.v[i] = Cvt<TO>::from(tacc[i]);
+                    typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_, t), rw, (ob + 32u) * 2u, 0, 0);
+                }
+            }
         }
         if (!more) break;
         t = tn;
@@ -624,8 +734,8 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
     }
 }
 
-template <typename TO, int FL, int REFD, bool QM, bool REC = false>
-__global__ __launch_bounds__(EW * 64) void msda_enc_kernel(const EncArgs a) {
+template <typename TO, int FL, int REFD, bool QM, bool REC = false, bool TAIL = false, int NW = EW>
+__global__ __launch_bounds__(NW * 64) void msda_enc_kernel(const EncArgs a) {
     __shared__ EncLevels lv;
     __shared__ u32x4v vmap[EMAP_PIX * 4];
     // XCD-aware remap (cdna_hip_programming.md T1): the strips of one (frame, head) map run
@@ -661,12 +771,12 @@ __global__ __launch_bounds__(EW * 64) void msda_enc_kernel(const EncArgs a) {
     }
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    enc_tiles<TO, FL, REFD, QM, REC>(a, lv, vmap, b, m, strip, wave, lane);
+    enc_tiles<TO, FL, REFD, QM, REC, TAIL, NW>(a, lv, vmap, b, m, strip, wave, lane);
 }
 
 // LDS regions for strips of 1/n of the image: rows ceil(H/n) + 3 (pixel centres, the +1 corner
 // row, a tile spilling into the next row) + 2*EHALO, at most the whole level + the two zero rows
-bool plan_layout(const int64_t* shapes, int fl, int n, EncPlan& pl) {
+bool plan_layout(const int64_t* shapes, int fl, int n, EncPlan& pl, int budget = EMAP_PIX) {
     int wmax = 0;
     for (int l = fl; l < EL; ++l) wmax = std::max<int>(wmax, (int)shapes[2 * l + 1]);
     long long pos = ((long long)wmax + 2 + 15) / 16 * 16;   // zero margin: a whole 2x2 footprint of any level
@@ -678,7 +788,7 @@ bool plan_layout(const int64_t* shapes, int fl, int n, EncPlan& pl) {
         pl.cap[l] = (int)cap;
         pl.base[l] = (int)pos;
         pos += (cap * W + 2 + 15) / 16 * 16;
-        if (pos > EMAP_PIX) return false;
+        if (pos > budget) return false;
     }
     pl.used = (int)pos;
     pl.fl = fl;
@@ -688,7 +798,8 @@ bool plan_layout(const int64_t* shapes, int fl, int n, EncPlan& pl) {
 
 // the fewest gathered levels whose staged levels fit with strips of at least 16 tiles, then the
 // fewest strips (>= what fits) whose workgroups fill >= 90 % of their last round of one per CU
-bool enc_plan(const int64_t* shapes, int batch, int heads, int num_query, EncPlan& pl) {
+bool enc_plan(const int64_t* shapes, int batch, int heads, int num_query, EncPlan& pl, bool tail = false) {
+    const int budget = tail ? EMAP_T : EMAP_PIX;
     const int cus = cu_count();
     const int maps = batch * heads;
     const int ntile = (num_query + EQT - 1) / EQT;
@@ -696,7 +807,7 @@ bool enc_plan(const int64_t* shapes, int batch, int heads, int num_query, EncPla
     for (int fl = 0; fl < EL; ++fl) {
         int nmin = 0;
         for (int n = 1; n <= nmax && n <= 64; ++n)
-            if (plan_layout(shapes, fl, n, pl)) {
+            if (plan_layout(shapes, fl, n, pl, budget)) {
                 nmin = n;
                 break;
             }
@@ -709,7 +820,7 @@ bool enc_plan(const int64_t* shapes, int batch, int heads, int num_query, EncPla
                 break;
             }
         }
-        return plan_layout(shapes, fl, n, pl);
+        return plan_layout(shapes, fl, n, pl, budget);
     }
     return false;
 }
@@ -746,10 +857,15 @@ int encoder_forward(const void* value, int64_t value_sb, int64_t value_sm, const
                     const void* offlog, const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
                     int frac_bits, bool rec, void* output, int batch, int spatial_size, int num_heads, int channels,
                     int num_levels, int num_query, int num_point, int output_dtype, const int32_t* query_tile_order,
-                    kinet_stream_t stream) {
+                    kinet_stream_t stream, const void* tail = nullptr, int64_t tail_sb = 0, int64_t tail_sm = 0) {
     KINET_CHECK_ARG(batch >= 0 && spatial_size > 0 && num_heads > 0 && num_query >= 0, "msda encoder: bad sizes");
-    KINET_CHECK_ARG(channels == 32 && num_levels == EL && num_point == EP,
-                    "msda encoder: head_dim 32, 4 levels, 4 points (got %d, %d, %d)", channels, num_levels, num_point);
+    const bool has_tail = tail != nullptr;
+    KINET_CHECK_ARG(channels == (has_tail ? 36 : 32) && num_levels == EL && num_point == EP,
+                    "msda encoder: head_dim %d, 4 levels, 4 points (got %d, %d, %d)", has_tail ? 36 : 32, channels,
+                    num_levels, num_point);
+    KINET_CHECK_ARG(!has_tail || (!rec && ((uintptr_t)tail % 16) == 0 && tail_sb % 8 == 0 && tail_sm % 8 == 0 &&
+                                  tail_sb >= (int64_t)spatial_size * 4 && tail_sm >= tail_sb),
+                    "msda encoder: tail plane must be 16-byte aligned (M, B, S, 4) with offsets/logits input");
     if (!rec)
         KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.",
                         ref_dim);
@@ -775,9 +891,11 @@ int encoder_forward(const void* value, int64_t value_sb, int64_t value_sm, const
                     spatial_size);
     if (batch == 0 || num_query == 0) return KINET_OK;
     EncPlan pl{};
-    KINET_CHECK_ARG(enc_plan(spatial_shapes_host, batch, num_heads, num_query, pl),
+    KINET_CHECK_ARG(enc_plan(spatial_shapes_host, batch, num_heads, num_query, pl, has_tail),
                     "msda encoder: no strip plan fits the LDS map (use kinet_msda_fused_forward)");
     const long long head_bytes = (long long)spatial_size * 64;
+    // the tail plane's range stays below TAF >> 3 (an invalid gathered sample's offset)
+    KINET_CHECK_ARG(!has_tail || (long long)spatial_size * 8 < (1LL << 28), "msda encoder: tail plane too large");
     long long wmax = 0;
     for (int l = 0; l < EL; ++l) wmax = std::max<long long>(wmax, spatial_shapes_host[2 * l + 1]);
     const int rd = rec ? 2 : ref_dim;
@@ -785,13 +903,18 @@ int encoder_forward(const void* value, int64_t value_sb, int64_t value_sm, const
     KINET_CHECK_ARG((spatial_size + wmax + 2) * 64 < (1LL << 31) && (long long)num_query * EREC * 2 < (1LL << 31) &&
                         (long long)batch * num_query < (1LL << 24) &&
                         (long long)batch * num_query * EL * rd * 4 < (1LL << 31) &&
-                        (long long)batch * num_query * num_heads * 64 < (1LL << 31),
+                        (long long)batch * num_query * num_heads * channels * 2 < (1LL << 31),
                     "msda encoder: problem too large for 32-bit buffer offsets");
     EncArgs a{};
     a.value = (const f16_t*)value;
     a.vsb = (long)value_sb;
     a.vsm = (long)value_sm;
     a.head_bytes = (int)head_bytes;
+    a.tail = (const f16_t*)tail;
+    a.tsb = (long)tail_sb;
+    a.tsm = (long)tail_sm;
+    a.tail_bytes = has_tail ? spatial_size * 8 : 0;
+    a.od = channels;
     for (int l = 0; l < EL; ++l) {
         a.H[l] = (int)spatial_shapes_host[2 * l];
         a.W[l] = (int)spatial_shapes_host[2 * l + 1];
@@ -815,6 +938,30 @@ int encoder_forward(const void* value, int64_t value_sb, int64_t value_sm, const
     KINET_CHECK_ARG(maps * pl.nstrip < (1LL << 31), "msda encoder: grid too large");
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)(maps * pl.nstrip)), block(EW * 64);
+    if (has_tail) {
+        const dim3 tblock(EWT * 64);
+#define TK(TO_, FL_, RD_, QM_) hipLaunchKernelGGL((msda_enc_kernel<TO_, FL_, RD_, QM_, false, true, EWT>), grid, tblock, 0, s, a)
+#define TK_QM(TO_, FL_, RD_) if (query_attn_mask) TK(TO_, FL_, RD_, true); else TK(TO_, FL_, RD_, false)
+#define TK_RD(TO_, FL_) if (ref_dim == 2) { TK_QM(TO_, FL_, 2); } else { TK_QM(TO_, FL_, 4); }
+#define TK_FL(TO_)                        \
+    switch (pl.fl) {                      \
+        case 0: TK_RD(TO_, 0) break;      \
+        case 1: TK_RD(TO_, 1) break;      \
+        case 2: TK_RD(TO_, 2) break;      \
+        default: TK_RD(TO_, 3) break;     \
+    }
+        if (output_dtype == KINET_BF16) {
+            TK_FL(bf16_t)
+        } else {
+            TK_FL(f16_t)
+        }
+#undef TK_FL
+#undef TK_RD
+#undef TK_QM
+#undef TK
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
 #define EK(TO_, FL_, RD_, QM_) hipLaunchKernelGGL((msda_enc_kernel<TO_, FL_, RD_, QM_>), grid, block, 0, s, a)
 #define EK_QM(TO_, FL_, RD_) if (query_attn_mask) EK(TO_, FL_, RD_, true); else EK(TO_, FL_, RD_, false)
 #define EK_RD(TO_, FL_)                                                                                  \
@@ -850,6 +997,36 @@ extern "C" int kinet_msda_encoder_forward(const void* value, int64_t value_sb, i
     return encoder_forward(value, value_sb, value_sm, spatial_shapes_host, offsets_logits_hm, ref_points, ref_dim,
                            query_attn_mask, 0, false, output, batch, spatial_size, num_heads, channels, num_levels,
                            num_query, num_point, output_dtype, query_tile_order, stream);
+}
+
+extern "C" int kinet_msda_encoder_forward_split(const void* value_main, int64_t main_sb, int64_t main_sm,
+                                                const void* value_tail, int64_t tail_sb, int64_t tail_sm,
+                                                const int64_t* spatial_shapes_host, const void* offsets_logits_hm,
+                                                const float* ref_points, int ref_dim, const uint8_t* query_attn_mask,
+                                                void* output, int batch, int spatial_size, int num_heads, int channels,
+                                                int num_levels, int num_query, int num_point, int output_dtype,
+                                                const int32_t* query_tile_order, kinet_stream_t stream) {
+    KINET_CHECK_ARG(value_tail != nullptr, "msda encoder split: value_tail is NULL");
+    return encoder_forward(value_main, main_sb, main_sm, spatial_shapes_host, offsets_logits_hm, ref_points, ref_dim,
+                           query_attn_mask, 0, false, output, batch, spatial_size, num_heads, channels, num_levels,
+                           num_query, num_point, output_dtype, query_tile_order, stream, value_tail, tail_sb, tail_sm);
+}
+
+extern "C" int kinet_msda_encoder_plan_ex(const int64_t* spatial_shapes_host, int batch, int num_heads, int num_query,
+                                          int channels, int32_t* plan_out) {
+    KINET_CHECK_ARG(channels == 32 || channels == 36, "msda encoder plan: head_dim 32 or 36 (got %d)", channels);
+    KINET_CHECK_ARG(spatial_shapes_host != nullptr && batch > 0 && num_heads > 0 && num_query > 0,
+                    "msda encoder plan: bad arguments");
+    EncPlan pl{};
+    KINET_CHECK_ARG(enc_plan(spatial_shapes_host, batch, num_heads, num_query, pl, channels == 36),
+                    "msda encoder: no strip plan fits the LDS map (use kinet_msda_fused_forward)");
+    if (plan_out) {
+        plan_out[0] = pl.fl;
+        plan_out[1] = pl.nstrip;
+        plan_out[2] = pl.used;
+        plan_out[3] = batch * num_heads * pl.nstrip;
+    }
+    return KINET_OK;
 }
 
 extern "C" int kinet_msda_encoder_forward_records(const void* value, int64_t value_sb, int64_t value_sm,

@@ -264,6 +264,73 @@ def value_proj_headmajor(x, weight, bias, head_dim, row_mask=None, out_dtype=Non
     return out
 
 
+class SplitValue:
+    """A head_dim-36 MSDA value in the two head-major planes of kinet_gemm_headmajor_split:
+    main (M, B, S, 32) and tail (M, B, S, 4), views of one buffer."""
+    __slots__ = ('main', 'tail')
+
+    def __init__(self, main, tail):
+        self.main, self.tail = main, tail
+
+    @property
+    def shape(self):
+        M_, B, S, _ = self.main.shape
+        return (M_, B, S, 36)
+
+    @property
+    def dtype(self):
+        return self.main.dtype
+
+    @property
+    def device(self):
+        return self.main.device
+
+    def dim(self):
+        return 4
+
+    def merged(self):
+        """(M, B, S, 36) head-major copy (tests / the generic kernel)."""
+        return torch.cat([self.main, self.tail], -1)
+
+
+def split_value_weights(weight, bias, heads):
+    """value_proj rows reordered [every head's channels 0-31 | every head's channels 32-35] (the
+    split GEMM's column order), cached per parameter version."""
+    D = weight.shape[0] // heads
+
+    def perm(t):
+        t = t.detach().view(heads, D, *t.shape[1:])
+        return torch.cat([t[:, :32].reshape(heads * 32, *t.shape[2:]), t[:, 32:].reshape(heads * (D - 32), *t.shape[2:])],
+                         0).contiguous()
+    return cached(weight, 'split_w', perm), cached(bias, 'split_b', lambda b: perm(b).float().contiguous())
+
+
+def value_proj_headmajor_split(x, weight_split, bias_split, heads, row_mask=None, out_dtype=None):
+    """MSDA value projection of a head_dim-36 layer into the two planes the split encoder
+    kernel reads (kinet_gemm_headmajor_split): x (B, S, K), weight/bias from split_value_weights
+    -> SplitValue(main (heads, B, S, 32), tail (heads, B, S, 4)); padding rows zeroed
+    (ms_deform_attn.py:64-67)."""
+    N.require_gpu(x)
+    B, S, K = x.shape
+    x2 = x.reshape(B * S, K)
+    if x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    w = weight_as(weight_split, x.dtype)
+    Nout = w.shape[0]
+    od = out_dtype or x.dtype
+    buf = torch.empty(B * S * Nout, dtype=od, device=x.device)
+    main = buf[:heads * B * S * 32].view(heads, B, S, 32)
+    tail = buf[heads * B * S * 32:].view(heads, B, S, Nout // heads - 32)
+    mask = row_mask.reshape(-1).to(torch.uint8).contiguous() if row_mask is not None else None
+    e = x.element_size()
+    N.call('kinet_gemm_headmajor_split', N.ptr(x2), N.ptr(w), N.ptr(buf), B * S, Nout, K, x2.stride(0), K,
+           N.dtype_code(x.dtype), N.dtype_code(od), N.ptr(f32(bias_split)), N.ptr(mask), S, 32, heads * 32,
+           Nout // heads - 32, N.stream(x.device),
+           work={'family': 'gemm', 'flops': 2.0 * B * S * Nout * K, 'shape': (B * S, Nout, K),
+                 'bytes': (B * S * K + Nout * K + B * S * Nout) * e})
+    return SplitValue(main, tail)
+
+
 # ----------------------------------------------------------------------------------- conv
 def pack_conv_weight(w, dtype, cin_pad=None):
     """OIHW -> OHWI (Cin fastest), optional zero channel padding, cast."""
@@ -644,18 +711,72 @@ _enc_plans = {}
 _KT = {torch.bfloat16: 'kinet::bf16_t', torch.float16: 'kinet::f16_t', torch.float32: 'float', torch.float64: 'double'}
 
 
-def msda_encoder_plan(shapes, batch, n_heads, Lq):
-    """kinet_msda_encoder_plan for host level shapes: (levels gathered from HBM, strips per head
+def msda_encoder_plan(shapes, batch, n_heads, Lq, channels=32):
+    """kinet_msda_encoder_plan_ex for host level shapes: (levels gathered from HBM, strips per head
     map, LDS map pixels used, workgroups), or None when no strip plan fits the LDS map.  Cached."""
-    key = (tuple(tuple(int(v) for v in s) for s in shapes), int(batch), int(n_heads), int(Lq))
+    key = (tuple(tuple(int(v) for v in s) for s in shapes), int(batch), int(n_heads), int(Lq), int(channels))
     if key not in _enc_plans:
         import ctypes
         hs = (ctypes.c_int64 * 8)(*[v for s in key[0] for v in s])
         out = (ctypes.c_int32 * 4)()
-        rc = N.lib().kinet_msda_encoder_plan(ctypes.cast(hs, ctypes.c_void_p), key[1], key[2], key[3],
-                                             ctypes.cast(out, ctypes.c_void_p))
+        rc = N.lib().kinet_msda_encoder_plan_ex(ctypes.cast(hs, ctypes.c_void_p), key[1], key[2], key[3], key[4],
+                                                ctypes.cast(out, ctypes.c_void_p))
         _enc_plans[key] = tuple(out) if rc == 0 else None
     return _enc_plans[key]
+
+
+# head_dim-36 encoder calls through the split value planes + kinet_msda_encoder_forward_split
+# when eligible; False keeps the generic fused kernel on the (M, B, S, 36) value (A/B and tests)
+MSDA_SPLIT = [True]
+
+
+def msda_split_supported(dtype, head_dim, shapes, Lq, n_heads, n_levels, n_points, batch):
+    """True when a head_dim-36 encoder call runs on the strip kernel with the split value planes:
+    16-bit compute, 4 levels x 4 points, >= 2048 queries per frame, a strip plan for 72-byte
+    pixels and a tail plane below 2^28 bytes."""
+    if not MSDA_SPLIT[0] or dtype not in (torch.bfloat16, torch.float16) or head_dim != 36:
+        return False
+    if n_levels != 4 or n_points != 4 or Lq < 2048 or shapes is None or len(shapes) != 4:
+        return False
+    S = sum(int(h) * int(w) for h, w in shapes)
+    if batch * Lq >= (1 << 24) or S * 8 >= (1 << 28):
+        return False
+    return msda_encoder_plan(shapes, batch, n_heads, Lq, 36) is not None
+
+
+def msda_encoder_split(value, shapes, offlog_hm, reference_points, n_heads, query_attn_mask=None, out_dtype=None,
+                       query_tile_order=None):
+    """Head_dim-36 encoder sampling (kinet_msda_encoder_forward_split): value a SplitValue from
+    value_proj_headmajor_split, offlog_hm (M, B, Lq, 48) f16, reference_points (B, Lq, 4, 2|4) f32
+    -> (B, Lq, M*36)."""
+    main, tail = value.main, value.tail
+    M_, B, S, _ = main.shape
+    D = 36
+    Lq = offlog_hm.shape[2]
+    key = tuple(tuple(int(v) for v in s) for s in shapes)
+    hs = _host_shapes.get(key)
+    if hs is None:
+        hs = _host_shapes[key] = torch.tensor(key, dtype=torch.int64)
+    ref = reference_points.float().contiguous()
+    od = out_dtype or torch.bfloat16
+    out = torch.empty((B, Lq, M_ * D), dtype=od, device=main.device)
+    qm = query_attn_mask.to(torch.uint8).contiguous() if query_attn_mask is not None else None
+    if query_tile_order is not None and (query_tile_order.dtype != torch.int32 or
+                                         query_tile_order.numel() != (Lq + 15) // 16):
+        raise RuntimeError('msda_encoder_split: query_tile_order must be int32 with ceil(Lq/16) entries')
+    offlog_hm = offlog_hm.contiguous()
+    nsamp = B * Lq * M_ * 16
+    plan = msda_encoder_plan(key, B, M_, Lq, 36)
+    kname = 'msda_enc_kernel<%s, %d, %d, %s, false, true, 12>' % (_KT[od], plan[0] if plan else -1, ref.shape[-1],
+                                                                  'true' if qm is not None else 'false')
+    N.call('kinet_msda_encoder_forward_split', N.ptr(main), main.stride(1), main.stride(0), N.ptr(tail),
+           tail.stride(1), tail.stride(0), N.ptr(hs), N.ptr(offlog_hm), N.ptr(ref), ref.shape[-1], N.ptr(qm),
+           N.ptr(out), B, S, M_, D, 4, Lq, 4, N.dtype_code(od), N.ptr(query_tile_order), N.stream(main.device),
+           work={'family': 'msda', 'flops': 10.0 * nsamp * D, 'Lq': Lq, 'S': S, 'kernel': kname,
+                 # compulsory bytes: both value planes once, f16 offsets + logits, refs, output once
+                 'bytes': B * S * M_ * D * 2 + offlog_hm.numel() * 2 + ref.numel() * 4
+                 + out.numel() * out.element_size()})
+    return out
 
 
 def msda_encoder_supported(value, shapes, Lq, n_heads, n_levels, n_points, batch):

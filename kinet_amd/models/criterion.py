@@ -129,7 +129,8 @@ class SetCriterion(nn.Module):
         src_boxes = outputs['pred_boxes'][idx]
         target_boxes = torch.cat([t['boxes'][i] for t, (_, i) in zip(targets, indices)], dim=0).to(src_boxes.device)
         loss_bbox = F.l1_loss(src_boxes, target_boxes, reduction='none')
-        loss_giou = 1 - torch.diag(generalized_box_iou(box_cxcywh_to_xyxy(src_boxes), box_cxcywh_to_xyxy(target_boxes)))
+        loss_giou = 1 - torch.diag(generalized_box_iou(box_cxcywh_to_xyxy(src_boxes), box_cxcywh_to_xyxy(target_boxes),
+                                                       self.deferred_checks if src_boxes.is_cuda else None))
         return {'loss_bbox': loss_bbox.sum() / num_boxes, 'loss_giou': loss_giou.sum() / num_boxes}
 
     def get_loss(self, loss, outputs, targets, indices, num_boxes, **kwargs):
@@ -170,7 +171,17 @@ class SetCriterion(nn.Module):
         it = iter(dev)
         return [[(next(it), next(it)) for _ in per_set] for per_set in host]
 
+    deferred_checks = None
+
+    def pop_deferred_checks(self):
+        """The GIoU degenerate-box flags of the last forward as one device bool (None if none):
+        the training step asserts it at its loss-finiteness sync instead of two syncs per
+        loss_boxes call (util/box_ops.py:44-45)."""
+        c, self.deferred_checks = self.deferred_checks, None
+        return torch.stack(c).all() if c else None
+
     def forward(self, outputs, targets):
+        self.deferred_checks = []
         outputs_without_aux = {k: v for k, v in outputs.items() if k != 'aux_outputs'}
         aux = list(outputs.get('aux_outputs', []))
         all_indices = self.match([outputs_without_aux] + aux, targets)

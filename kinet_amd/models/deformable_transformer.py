@@ -114,7 +114,7 @@ class DeformableTransformerEncoderLayer(nn.Module):
                      shapes_host=None):
         # deformable_transformer.py:290-299, one kernel per step
         a = self.self_attn
-        value = a.project_value(src, padding_mask)                                     # head-major
+        value = a.project_value(src, padding_mask, encoder_shapes=shapes_host)         # head-major
         samp = a.sample(src, reference_points, value, spatial_shapes, query_add=pos,   # (src+pos) @ W
                         query_order=query_order, shapes_host=shapes_host)
         n1, n2 = self.norm1, self.norm2

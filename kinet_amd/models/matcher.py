@@ -34,9 +34,9 @@ class HungarianMatcher(nn.Module):
         assert cost_class != 0 or cost_bbox != 0 or cost_giou != 0, "all costs cant be 0"
 
     @torch.no_grad()
-    def cost_matrix(self, outputs, targets):
+    def cost_matrix(self, outputs, targets, checks=None):
         """(batch, num_queries, sum_targets) f32 cost on the predictions' device
-        (matcher.py:135-171)."""
+        (matcher.py:135-171).  checks: see misc.generalized_box_iou."""
         batch_size, num_queries = outputs["pred_logits"].shape[:2]
         logits = outputs["pred_logits"].flatten(0, 1).float()
         out_prob = logits.sigmoid() if self.focal_loss else logits.softmax(-1)
@@ -51,7 +51,7 @@ class HungarianMatcher(nn.Module):
         else:
             cost_class = -out_prob[:, tgt_ids]
         cost_bbox = torch.cdist(out_bbox, tgt_bbox, p=1)
-        cost_giou = -generalized_box_iou(box_cxcywh_to_xyxy(out_bbox), box_cxcywh_to_xyxy(tgt_bbox))
+        cost_giou = -generalized_box_iou(box_cxcywh_to_xyxy(out_bbox), box_cxcywh_to_xyxy(tgt_bbox), checks)
         c = self.cost_bbox * cost_bbox + self.cost_class * cost_class + self.cost_giou * cost_giou
         return c.view(batch_size, num_queries, -1)
 
@@ -70,24 +70,33 @@ class HungarianMatcher(nn.Module):
         offsets = np.cumsum([0] + sizes[:-1])
         tq = [i for i, t in enumerate(targets) if 'track_query_match_ids' in t]
         shapes = {(tuple(o["pred_logits"].shape), tuple(o["pred_boxes"].shape)) for o in outputs_list}
+        # the GIoU degenerate-box asserts (util/box_ops.py:44-45) ride on the cost matrix's one host
+        # copy instead of synchronising twice per generalized_box_iou call
+        checks = []
         if len(outputs_list) > 1 and len(shapes) == 1:
             # every set in one cost computation (the same element-wise ops and per-pair L1 /
             # GIoU, S x fewer launches): rows (set, image, query)
             S, (bsz, nq) = len(outputs_list), outputs_list[0]["pred_logits"].shape[:2]
             both = {k: torch.cat([o[k] for o in outputs_list]) for k in ("pred_logits", "pred_boxes")}
-            costs = self.cost_matrix(both, targets).view(S, bsz, nq, -1)
+            costs = self.cost_matrix(both, targets, checks).view(S, bsz, nq, -1)
         else:
-            costs = torch.stack([self.cost_matrix(o, targets) for o in outputs_list])
-        extra = []
+            costs = torch.stack([self.cost_matrix(o, targets, checks) for o in outputs_list])
+        has_chk = bool(checks) and costs.is_cuda
+        extra = [torch.stack(checks)] if has_chk else []
         if tq:
             masks = torch.stack([torch.stack([targets[i]['track_queries_fal_pos_mask'],
                                               targets[i]['track_queries_mask']]).to(costs.device) for i in tq])
             ids = [targets[i]['track_query_match_ids'] for i in tq]
             counts = [len(m) for m in ids]
-            extra = [masks, torch.cat([m.to(costs.device).long() for m in ids]) if sum(counts)
-                     else torch.zeros(0, dtype=torch.long)]
+            extra += [masks, torch.cat([m.to(costs.device).long() for m in ids]) if sum(counts)
+                      else torch.zeros(0, dtype=torch.long)]
         host = to_host(costs, *extra)
         costs = host[0]
+        if has_chk:
+            assert bool(host[1].all()), 'degenerate boxes (util/box_ops.py:44-45)'
+            host = host[:1] + host[2:]
+        elif checks:
+            assert all(bool(c) for c in checks)
         forced = []
         if tq:
             masks, ids = host[1], host[2].split(counts)

@@ -122,10 +122,18 @@ def box_iou(boxes1, boxes2):
     return inter / union, union
 
 
-def generalized_box_iou(boxes1, boxes2):
-    """util/box_ops.py:38-60 (degenerate boxes rejected the same way)."""
-    assert (boxes1[:, 2:] >= boxes1[:, :2]).all()
-    assert (boxes2[:, 2:] >= boxes2[:, :2]).all()
+def generalized_box_iou(boxes1, boxes2, checks=None):
+    """util/box_ops.py:38-60 (degenerate boxes rejected the same way).  checks: None asserts
+    right here, as the reference does (a device -> host sync per assert on GPU tensors); a
+    list receives the two device bool flags instead, for the caller to assert at a sync point
+    it already has (the matcher's cost-matrix copy, the training step's loss check)."""
+    ok1 = (boxes1[:, 2:] >= boxes1[:, :2]).all()
+    ok2 = (boxes2[:, 2:] >= boxes2[:, :2]).all()
+    if checks is None:
+        assert ok1
+        assert ok2
+    else:
+        checks += [ok1, ok2]
     iou, union = box_iou(boxes1, boxes2)
     lt = torch.min(boxes1[:, None, :2], boxes2[:, :2])
     rb = torch.max(boxes1[:, None, 2:], boxes2[:, 2:])

@@ -97,10 +97,19 @@ class MSDeformAttn(nn.Module):
         out = self.sample(query, reference_points, value, input_spatial_shapes, query_attn_mask)
         return K.linear(out, self.output_proj.weight, self.output_proj.bias)
 
-    def project_value(self, input_flatten, input_padding_mask=None):
+    def project_value(self, input_flatten, input_padding_mask=None, encoder_shapes=None):
         """value_proj + padding masked_fill (ms_deform_attn.py:64-66), written head-major
         (M, N, S, D) for the gather kernel; bf16 compute stores the values as f16 (more
-        mantissa, and the sampling kernel's mixed f16 x f32 FMA reads them directly)."""
+        mantissa, and the sampling kernel's mixed f16 x f32 FMA reads them directly).
+        encoder_shapes (host level shapes of an encoder call, Lq = S): a head_dim-36 layer then
+        writes the two planes of the split strip kernel (K.SplitValue)."""
+        D = self.d_model // self.n_heads
+        if encoder_shapes is not None and K.msda_split_supported(
+                input_flatten.dtype, D, encoder_shapes, input_flatten.shape[1], self.n_heads, self.n_levels,
+                self.n_points, input_flatten.shape[0]):
+            w, b = K.split_value_weights(self.value_proj.weight, self.value_proj.bias, self.n_heads)
+            return K.value_proj_headmajor_split(input_flatten, w, b, self.n_heads, row_mask=input_padding_mask,
+                                                out_dtype=value_dtype_for(input_flatten.dtype))
         return K.value_proj_headmajor(input_flatten, self.value_proj.weight, self.value_proj.bias,
                                       self.d_model // self.n_heads, row_mask=input_padding_mask,
                                       out_dtype=value_dtype_for(input_flatten.dtype))
@@ -151,6 +160,12 @@ class MSDeformAttn(nn.Module):
         pre-output_proj (N, Lq, d).  shapes_host: the level shapes as a host list (lets an
         encoder-sized call take kinet_msda_encoder_forward)."""
         N_, Lq = query.shape[:2]
+        if isinstance(value, K.SplitValue):
+            # head_dim 36 on the strip kernel (value planes from project_value(encoder_shapes=...))
+            w, b = self.packed_offsets_weights_headmajor()
+            offlog = K.offsets_proj_headmajor(query, w, b, self.n_heads, x_add=query_add)
+            return K.msda_encoder_split(value, shapes_host, offlog, reference_points, self.n_heads, query_attn_mask,
+                                        out_dtype=query.dtype, query_tile_order=query_order)
         if (query.dtype in (torch.bfloat16, torch.float16) and
                 K.msda_encoder_supported(value, shapes_host, Lq, self.n_heads, self.n_levels, self.n_points, N_)):
             if K.msda_records_supported(query, shapes_host, self.n_heads, self.n_levels, self.n_points):

@@ -67,9 +67,18 @@ def train_step(model, criterion, optimizer, samples, targets, clip_max_norm=0.1)
     outputs, targets, *_ = model(samples, targets)
     loss_dict = criterion(outputs, targets)
     losses = weighted_loss(loss_dict, criterion.weight_dict)
-    if not torch.isfinite(losses):
+    # one host read for the loss-finiteness check (engine.py:131-134) and the criterion's GIoU
+    # degenerate-box asserts (util/box_ops.py:44-45, deferred to here)
+    flags = [torch.isfinite(losses).reshape(())]
+    boxes_ok = criterion.pop_deferred_checks() if hasattr(criterion, 'pop_deferred_checks') else None
+    if boxes_ok is not None:
+        flags.append(boxes_ok.reshape(()))
+    flags = torch.stack(flags).tolist()
+    if not flags[0]:
         raise FloatingPointError(f'non-finite loss {losses.item()}: '
                                  + ', '.join(f'{k}={v.item():.4g}' for k, v in loss_dict.items()))
+    assert all(flags[1:]), 'degenerate boxes (util/box_ops.py:44-45)'
+
     optimizer.zero_grad()
     losses.backward()
     if clip_max_norm > 0:

@@ -458,6 +458,47 @@ def test_rw_conv1x1(K, Cin, Cout, res):
     assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
 
 
+@pytest.mark.parametrize('case', ['plain128', 'relu_mask256', 'f32_256', 'f16out_256', 'headmajor', 'conv1x1_128',
+                                  'conv1x1_s2'])
+def test_rw_row_tile_variants_bit_identical(K, gemm_flags, case):
+    """The resident-weight kernel's shipped 32-row tiles (two MFMA row tiles per wave, TMR = 2:
+    plain / masked / head-major GEMMs with K = 128 / 256 and no residual or LayerNorm, the 1x1
+    convs, the strided conv-row downsample) give the 16-row tiles' results bit for bit
+    (kinet_gemm_set_flags 131072) -- the 32-row SAMPLING-RECORDS tile of round 4 differed from
+    its 16-row tile, and these share its ring, counted waits and pending stores."""
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    def run(flags):
+        gemm_flags(flags)
+        if case.startswith('conv1x1'):
+            st = 2 if case.endswith('s2') else 1
+            cin, cout = (256, 512) if st == 2 else (128, 256)
+            x = torch.randn(2, 80 if st == 2 else 60, 130, cin, generator=torch.Generator().manual_seed(3)).bfloat16()
+            w = (torch.randn(cout, cin, 1, 1, generator=torch.Generator().manual_seed(4)) / cin ** 0.5).bfloat16()
+            sc = torch.rand(cout, generator=torch.Generator().manual_seed(5)) + 0.5
+            bi = torch.randn(cout, generator=torch.Generator().manual_seed(6))
+            return K.conv2d_nhwc(x.cuda(), K.pack_conv_weight(w.cuda(), torch.bfloat16), st, 0, scale=sc.cuda(),
+                                 bias=bi.cuda(), relu=True)
+        if case == 'headmajor':
+            x = torch.randn(2, 4500, 256, generator=torch.Generator().manual_seed(7)).bfloat16()
+            w = (torch.randn(256, 256, generator=torch.Generator().manual_seed(8)) / 16).bfloat16()
+            b = torch.randn(256, generator=torch.Generator().manual_seed(9))
+            m = torch.rand(2, 4500, generator=torch.Generator().manual_seed(10)) < 0.2
+            return K.value_proj_headmajor(x.cuda(), w.cuda(), b.cuda(), 32, row_mask=m.cuda(), out_dtype=torch.float16)
+        Kd = 128 if case.endswith('128') else 256
+        M, N = 10007, 384
+        x, w, b, kw, _ = _rw_case(M, N, Kd, {'plain128': 'plain', 'relu_mask256': 'relu_mask', 'f32_256': 'f32',
+                                             'f16out_256': 'plain'}[case], 21)
+        if case == 'f16out_256':
+            kw['out_dtype'] = torch.float16
+        return K.linear(x.cuda(), w.cuda(), b.cuda(), **kw)
+    y32 = run(0)
+    y16 = run(131072)
+    gemm_flags(0)
+    torch.cuda.synchronize()
+    assert y32.shape == y16.shape
+    assert torch.equal(y32, y16), (y32.float() - y16.float()).abs().max().item()
+
+
 # ---- split-K (few output tiles, long K): f32 slice partials + finalize epilogue ----------------
 
 @pytest.mark.parametrize('M,N,Kd,mode', [(1200, 256, 1024, 'res_ln_mask'), (4200, 256, 2048, 'plain'),

@@ -489,6 +489,125 @@ def test_encoder_kernel_strips_staged_and_far(shapes, noise):
     assert (o_enc.float()[qmask] == 0).all()
 
 
+# ---- head_dim 36: split value planes (kinet_gemm_headmajor_split -> kinet_msda_encoder_forward_split) ----
+
+def _split(value):
+    """(M, B, S, 36) -> K.SplitValue planes (M, B, S, 32) + (M, B, S, 4) in one buffer."""
+    from kinet_amd import kernels as K
+    M_, B, S, _ = value.shape
+    buf = torch.empty(M_ * B * S * 36, dtype=value.dtype, device=value.device)
+    main = buf[:M_ * B * S * 32].view(M_, B, S, 32)
+    tail = buf[M_ * B * S * 32:].view(M_, B, S, 4)
+    main.copy_(value[..., :32])
+    tail.copy_(value[..., 32:])
+    return K.SplitValue(main, tail)
+
+
+@pytest.mark.parametrize('masked_rows', [False, True])
+def test_value_proj_split_matches_headmajor(masked_rows):
+    """kinet_gemm_headmajor_split (weight rows reordered [heads x 32 | heads x 4]) writes the same
+    numbers as the (M, B, S, 36) head-major projection, bit for bit (same dot products, same
+    tile), with padding rows zeroed in both planes."""
+    from kinet_amd import kernels as K
+    g = torch.Generator().manual_seed(5)
+    B, S, d, M = 2, 3100, 288, 8
+    x = torch.randn(B, S, d, generator=g).half().cuda()
+    w = (torch.randn(d, d, generator=g) / 16).cuda()
+    b = torch.randn(d, generator=g).cuda()
+    mask = (torch.rand(B, S, generator=g) < 0.2).cuda() if masked_rows else None
+    ref = K.value_proj_headmajor(x, w, b, 36, row_mask=mask, out_dtype=torch.float16)
+    ws, bs = K.split_value_weights(w, b, M)
+    sv = K.value_proj_headmajor_split(x, ws, bs, M, row_mask=mask, out_dtype=torch.float16)
+    torch.cuda.synchronize()
+    assert sv.shape == (M, B, S, 36)
+    assert torch.equal(sv.main, ref[..., :32]) and torch.equal(sv.tail, ref[..., 32:])
+    if masked_rows:
+        assert (sv.tail.permute(1, 2, 0, 3)[mask] == 0).all()
+
+
+@pytest.mark.parametrize('shapes,ref_dim,noise', [
+    (((64, 84), (32, 42), (16, 21), (8, 11)), 2, 3.0),
+    (((64, 84), (32, 42), (16, 21), (8, 11)), 4, 6.0),       # box references, far-out samples
+    (((50, 60), (20, 30), (10, 13), (5, 7)), 2, 1.0),        # levels 1-3 staged
+    (((25, 40), (15, 20), (8, 10), (4, 5)), 2, 4.0),         # every level staged (Lq > S)
+    (((135, 240), (68, 120), (34, 60), (17, 30)), 2, 2.0),   # the config-5 geometry (1080x1920)
+])
+@pytest.mark.parametrize('out_dtype,masked', [(torch.float16, False), (torch.bfloat16, True)])
+def test_encoder_split_kernel_matches_generic(shapes, ref_dim, noise, out_dtype, masked):
+    """kinet_msda_encoder_forward_split (head_dim 36 as a 32- + 4-channel plane) against the
+    generic fused kernel on the same (M, B, S, 36) f16 values and f16 offsets / logits: the bound of
+    test_encoder_kernel_matches_fast_kernel (f16 tap weights, per-level f16 pair sums, one output
+    rounding), on the 32 main channels and the 4 tail channels alike."""
+    from kinet_amd import kernels as K
+    B, M, P = 2, 8, 4
+    S = sum(h * w for h, w in shapes)
+    Lq = max(S, 2304)
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, ref_dim, noise, Lq + 5 * ref_dim,
+                                                  dtype=torch.float16, D=36)
+    offlog = offlog.half()
+    qm = qmask if masked else None
+    plan = K.msda_encoder_plan(shapes, B, M, Lq, 36)
+    assert plan is not None and K.msda_split_supported(torch.float16, 36, shapes, Lq, M, 4, P, B)
+    order = K.encoder_tile_order(shapes, value.device) if Lq == S else None
+    o_enc = K.msda_encoder_split(_split(value), shapes, _hm(offlog, M), ref, M, qm, out_dtype=out_dtype,
+                                 query_tile_order=order)
+    o_gen = K.msda_fused(value, ss, offlog, ref, M, 4, P, qm, head_major=True, out_dtype=out_dtype)
+    torch.cuda.synchronize()
+    ulp = 2.0 ** -7 if out_dtype == torch.bfloat16 else 2.0 ** -10
+    d = (o_enc.float() - o_gen.float()).abs()
+    vmax = value.float().abs().max().item()
+    big = torch.maximum(o_gen.float().abs(), o_enc.float().abs())
+    bad = d > big * ulp + (2.0 ** -7 + 2.0 ** -11) * vmax
+    assert not bad.any(), (d.max().item(), bad.view(B, Lq, M, 36).sum((0, 1, 2)).tolist())
+    assert d.mean().item() <= 2e-3, d.mean().item()
+    tail = d.view(B, Lq, M, 36)[..., 32:]
+    assert tail.mean().item() <= 2e-3, tail.mean().item()
+    if masked:
+        assert (o_enc.float()[qmask] == 0).all()
+    assert torch.isfinite(o_enc.float()).all()
+
+
+def test_encoder_split_kernel_vs_oracle():
+    """The split kernel against the C oracle (cuh:165-237 restated, any channel count) on the
+    locations / attention weights the generic kernel reports for the same inputs."""
+    from kinet_amd import kernels as K
+    from oracle import msda_oracle as O
+    shapes = ((64, 84), (32, 42), (16, 21), (8, 11))
+    B, M, P = 2, 8, 4
+    Lq = sum(h * w for h, w in shapes)
+    value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 81, dtype=torch.float16, D=36)
+    offlog = offlog.half()
+    out = K.msda_encoder_split(_split(value), shapes, _hm(offlog, M), ref, M, qmask, out_dtype=torch.float16)
+    _, loc, aw = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, want_loc_attw=True, head_major=True,
+                              out_dtype=torch.float16)
+    torch.cuda.synchronize()
+    v = value.float().permute(1, 2, 0, 3).contiguous().cpu().numpy()
+    ref_out = torch.from_numpy(O.fwd(v, ss.cpu().numpy(), loc.cpu().numpy(), aw.cpu().numpy())).reshape(out.shape)
+    d = (out.float().cpu() - ref_out).abs()
+    bound = 4e-3 * ref_out.abs() + 4e-3 + 2.0 ** -7 * value.float().abs().max().item()
+    assert (d <= bound).all(), d.max().item()
+    assert d.mean().item() <= 2e-3, d.mean().item()
+
+
+def test_encoder_split_kernel_order_and_batch_invariant():
+    """Each query's result depends only on its own inputs (tile order, batch, rerun)."""
+    from kinet_amd import kernels as K
+    shapes = ((64, 84), (32, 42), (16, 21), (8, 11))
+    M, P = 8, 4
+    Lq = sum(h * w for h, w in shapes)
+    value, ss, offlog, ref, qmask = _fused_inputs(3, shapes, Lq, M, P, 2, 25.0, 9, dtype=torch.float16, D=36)
+    hm = _hm(offlog, M)
+    sv = _split(value)
+    order = K.encoder_tile_order(shapes, value.device)
+    o_nat = K.msda_encoder_split(sv, shapes, hm, ref, M, out_dtype=torch.bfloat16)
+    o_ord = K.msda_encoder_split(sv, shapes, hm, ref, M, out_dtype=torch.bfloat16, query_tile_order=order)
+    o_one = K.msda_encoder_split(_split(value[:, 1:2].contiguous()), shapes, hm[:, 1:2], ref[1:2], M,
+                                 out_dtype=torch.bfloat16, query_tile_order=order)
+    torch.cuda.synchronize()
+    assert torch.equal(o_nat, o_ord)
+    assert torch.equal(o_one[0], o_ord[1])
+
+
 # ---- sampling records (kinet_msda_sample_records -> kinet_msda_encoder_forward_records) ----
 
 def _record_problem(shapes, B, noise, seed, ref_dim=2, masked=False, dtype=torch.bfloat16):
