@@ -180,7 +180,11 @@ class _ConvNHWC(Function):
         dx = dw = db = None
         if ctx.needs_input_grad[1]:
             cols = x.reshape(B * H * W, I) if pointwise else K.im2col_nhwc(x, KH, KW, s, p)
-            dw = K.gemm_tn(dz2, cols).view(O, KH, KW, I).permute(0, 3, 1, 2).contiguous()
+            g = K.gemm_tn(dz2, cols)
+            # a 1x1 kernel's (O, I) rows already are the OIHW layout: viewed, not permuted, so the
+            # gradient carries the parameter's own strides (I, 1, 1, 1) -- a permuted view keeps
+            # (I, 1, I, I), which DDP's bucket views reject with a copy per step
+            dw = g.view(O, I, 1, 1) if KH == 1 and KW == 1 else g.view(O, KH, KW, I).permute(0, 3, 1, 2).contiguous()
         if ctx.needs_input_grad[0]:
             wpt = K.transpose2d(K.pack_conv_weight(weight, torch.float32).reshape(O, KH * KW * I))   # (KH*KW*I, O)
             dcols = K.linear(dz2, wpt)                                                            # (P, KH*KW*I)

@@ -118,52 +118,59 @@ __device__ __forceinline__ void unpack8(const u32x4& u, float* v, bool f16) {
 //   v = [x0 y0 x1 y1 x2 y2 x3 y3 | logit0..3] of level l (offsets in level pixels, the head's
 //   16 logits spread over the 4 lanes lane, lane^16, lane^32, lane^48 -- one per level);
 // softmax over the head's 16 logits, the locations (the reference's offsets / (H, W) on (x, y)
-// quirk for 2-d refs, :77-82), then per point
-//   * the corner rows / columns outside the level folded into the weight: a footprint with its
-//     top row above the level (hl = -1) becomes row 0 with weight a*lh and no second row; a
-//     bottom row below it (hl = H-1) keeps row H-1 with weight a*(1-lh); the same for columns --
-//     so the sampler needs no bounds tests (its second row / column only ever gets weight 0);
-//   * a sample outside the level (cuh:229): weight 0 at the query's own pixel;
-//   * location = fixed point u32 (hl << (16+fb)) | (round(lh 2^fb) << 16) | (wl << fb) | round(lw 2^fb)
-//     (a rounded-up fraction carries into the integer part), weight = f16.
+// quirk for 2-d refs, :77-82), then per point, with h = y H - 0.5, w = x W - 0.5:
+//   * the corner rows / columns outside the level folded into the weight by ONE factor per axis,
+//     clamp(min(h + 1, H - h), 0, 1): 1 inside, lh = h + 1 when the top row is -1 (the footprint
+//     becomes row 0 with weight a lh), 1 - lh = H - h when the bottom row is H (row H-1 keeps
+//     a (1 - lh)), 0 outside the level (cuh:229) -- so the sampler needs no bounds tests (its
+//     second row / column only ever gets weight 0); the same for columns;
+//   * location = round(clamp(h, 0, H-1) 2^fb) << 16 | round(clamp(w, 0, W-1) 2^fb): the
+//     fixed-point corner + fraction, (hl << (16+fb)) | (round(lh 2^fb) << 16) | (wl << fb) |
+//     round(lw 2^fb) with a rounded-up fraction carried into the corner (h 2^fb + 0.5 is exact in
+//     f32 for every level that fits the 16-bit field); a folded axis has fraction 0; a sample
+//     outside the level (weight 0) points at the query's own pixel of the level, which the
+//     sampler's strip always stages (finite values assumed: it multiplies that pixel by 0);
+//   * weight = f16.
 // out: 4 location words, then the 4 weights as 2 packed f16 words.
 // max / sum over the 4 lanes lane ^ {0, 16, 32, 48} (the 4 levels of one row): gfx950's row-swap
 // permutes (v_permlane16_swap / v_permlane32_swap) return {own, partner} in some order, so one
 // op per step combines them -- no LDS round trip as __shfl_xor's ds_bpermute takes
-template <bool MAX>
+template <bool MAX, bool SHFL = false>
 __device__ __forceinline__ float level_reduce(float x) {
+    if constexpr (SHFL) {   // diagnostic (DIAG 4): the same reduction through ds_bpermute, no row swaps
+        x = MAX ? fmaxf(x, __shfl_xor(x, 16)) : x + __shfl_xor(x, 16);
+        return MAX ? fmaxf(x, __shfl_xor(x, 32)) : x + __shfl_xor(x, 32);
+    }
     const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     x = MAX ? fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1])) : __uint_as_float(a[0]) + __uint_as_float(a[1]);
     const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return MAX ? fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1])) : __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+template <bool SHFL = false>
 __device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_lds, bool qmasked, int rl, int l,
                                              const float (&v)[12], uint32_t* out) {
     // level constants (lane-dependent level: selects, not an indexed kernel-argument load)
     const int Hl = l == 0 ? p.prep_H[0] : l == 1 ? p.prep_H[1] : l == 2 ? p.prep_H[2] : p.prep_H[3];
     const int Wl = l == 0 ? p.prep_W[0] : l == 1 ? p.prep_W[1] : l == 2 ? p.prep_W[2] : p.prep_W[3];
     const float Hf = (float)Hl, Wf = (float)Wl;
-    const float rH = __builtin_amdgcn_rcpf(Hf), rW = __builtin_amdgcn_rcpf(Wf);
-    const int fb = p.prep_fb;
-    const float fs = (float)(1 << fb);
-    const int fmask = (1 << fb) - 1;
-    const float mx = level_reduce<true>(fmaxf(fmaxf(v[8], v[9]), fmaxf(v[10], v[11])));
+    const float fs = (float)(1 << p.prep_fb);
+    const float mx = level_reduce<true, SHFL>(fmaxf(fmaxf(v[8], v[9]), fmaxf(v[10], v[11])));
     float e[4], es = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         e[q] = __expf(v[8 + q] - mx);
         es += e[q];
     }
-    es = level_reduce<false>(es);
+    es = level_reduce<false, SHFL>(es);
     const float ra = qmasked ? 0.f : __builtin_amdgcn_rcpf(es);
     float rx, ry, sx, sy;   // reference point and the offset scale of each axis
     if (p.prep_refd == 2) {
         const float2 r = *reinterpret_cast<const float2*>(ref_lds + (rl * 4 + l) * 8);
         rx = r.x;
         ry = r.y;
-        sx = rH;   // :77-79 (offsets / spatial_shapes, (H, W) on (x, y))
-        sy = rW;
+        sx = __builtin_amdgcn_rcpf(Hf);   // :77-79 (offsets / spatial_shapes, (H, W) on (x, y))
+        sy = __builtin_amdgcn_rcpf(Wf);
     } else {
         const float4 r = *reinterpret_cast<const float4*>(ref_lds + (rl * 4 + l) * 16);
         rx = r.x;
@@ -171,32 +178,21 @@ __device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_
         sx = 0.125f * r.z;   // :80-82 (/ n_points * wh * 0.5, n_points = 4)
         sy = 0.125f * r.w;
     }
+    const float H1 = Hf - 1.f, W1 = Wf - 1.f;
     // the query's own pixel of this level: where a sample outside the level points (weight 0)
     const int hr = min(max((int)floorf(ry * Hf), 0), Hl - 1), wr = min(max((int)floorf(rx * Wf), 0), Wl - 1);
-    const uint32_t own = ((uint32_t)hr << (16 + fb)) | ((uint32_t)wr << fb);
+    const uint32_t own = ((uint32_t)hr << (16 + p.prep_fb)) | ((uint32_t)wr << p.prep_fb);
     float aw[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const float x = fmaf(v[2 * q], sx, rx), y = fmaf(v[2 * q + 1], sy, ry);
         const float h = fmaf(y, Hf, -0.5f), w = fmaf(x, Wf, -0.5f);
-        const bool valid = h > -1.f && w > -1.f && h < Hf && w < Wf;
-        const float hfl = floorf(h), wfl = floorf(w);
-        const float lh = h - hfl, lw = w - wfl;
-        const int hl = (int)hfl, wl = (int)wfl;
-        // out-of-level corner rows / columns folded into the weight, branch-free
-        const bool top = hl < 0, bot = hl >= Hl - 1, lef = wl < 0, rig = wl >= Wl - 1;
-        const float fh = top ? lh : (bot ? 1.f - lh : 1.f);
-        const float fw = lef ? lw : (rig ? 1.f - lw : 1.f);
-        const float a = valid ? e[q] * ra * fh * fw : 0.f;
-        // fixed-point fraction (zero on a folded axis); a rounded-up fraction carries into the corner
-        int qh = (top || bot) ? 0 : (int)fmaf(lh, fs, 0.5f);
-        int qw = (lef || rig) ? 0 : (int)fmaf(lw, fs, 0.5f);
-        const int hc = min(max(hl, 0), Hl - 1) + (qh >> fb), wc = min(max(wl, 0), Wl - 1) + (qw >> fb);
-        qh &= fmask;
-        qw &= fmask;
-        const uint32_t word = ((uint32_t)hc << (16 + fb)) | ((uint32_t)qh << 16) | ((uint32_t)wc << fb) | (uint32_t)qw;
-        out[q] = valid ? word : own;
-        aw[q] = a;
+        const float fh = __builtin_amdgcn_fmed3f(fminf(h + 1.f, Hf - h), 0.f, 1.f);
+        const float fw = __builtin_amdgcn_fmed3f(fminf(w + 1.f, Wf - w), 0.f, 1.f);
+        aw[q] = e[q] * ra * fh * fw;
+        const uint32_t ph = (uint32_t)(int)fmaf(__builtin_amdgcn_fmed3f(h, 0.f, H1), fs, 0.5f);
+        const uint32_t pw = (uint32_t)(int)fmaf(__builtin_amdgcn_fmed3f(w, 0.f, W1), fs, 0.5f);
+        out[q] = fminf(fh, fw) > 0.f ? (ph << 16) | pw : own;   // fh, fw > 0: inside (-1, H) x (-1, W)
     }
     out[4] = (uint32_t)__builtin_bit_cast(uint16_t, (f16_t)aw[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, (f16_t)aw[1]) << 16);
     out[5] = (uint32_t)__builtin_bit_cast(uint16_t, (f16_t)aw[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, (f16_t)aw[3]) << 16);
@@ -464,6 +460,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
         } else if constexpr (DIAG == 2) {   // diagnostic: every wave's memory traffic retired first
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             __syncthreads();
+        } else if constexpr (DIAG == 3) {   // diagnostic: MFMAs and epilogue kept apart, no idle states
+            __builtin_amdgcn_sched_barrier(0);
         }
         // ---- epilogue (registers) ----
         float v[TMR][NC];
@@ -472,8 +470,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
             for (int t = 0; t < TMR; ++t) {
 #pragma unroll
                 for (int j = 0; j < NC; ++j) v[t][j] = acc[j >> 2][t][j & 3] + par[GW + cl0 + j];
-                prep_records(p, st + C_::REF_OFF, st[C_::MASK_OFF + t * 16 + (lane & 15)] != 0, t * 16 + (lane & 15),
-                             lane >> 4, v[t], pend[t]);
+                prep_records<DIAG == 4>(p, st + C_::REF_OFF, st[C_::MASK_OFF + t * 16 + (lane & 15)] != 0,
+                                        t * 16 + (lane & 15), lane >> 4, v[t], pend[t]);
             }
             pend_m0 = m0;
             continue;
@@ -765,10 +763,14 @@ extern "C" int kinet_msda_sample_records(const void* A, const void* A2, const vo
     // for the other streams' workgroups.  Four per CU (128 VGPRs) spills and loses 7 %.  Flag
     // 8192: the two-workgroup ring.
     // diagnostic (round 5): the 32-row records tile that differed from the 16-row tile in round 4
-    // (flag 16384; + 32768: idle wait states before the epilogue; + 65536: traffic drained first)
+    // (flag 16384; + 32768: idle wait states before the epilogue; + 65536: traffic drained first;
+    // + 262144: MFMAs and epilogue kept apart by a scheduling barrier only; + 524288: the level
+    // reductions through ds_bpermute instead of v_permlane16/32_swap)
     if ((kinet_gemm_flags & 16384) && A2 && in_dtype == KINET_BF16) {
         if (kinet_gemm_flags & 32768) launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2, 1>(a, s);
         else if (kinet_gemm_flags & 65536) launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2, 2>(a, s);
+        else if (kinet_gemm_flags & 262144) launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2, 3>(a, s);
+        else if (kinet_gemm_flags & 524288) launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2, 4>(a, s);
         else launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2>(a, s);
         KINET_LAUNCH_CHECK();
         return KINET_OK;

@@ -46,10 +46,13 @@ constexpr int EW = 16;             // waves per workgroup (one workgroup per CU)
 constexpr int EQT = 16;            // queries per wave tile
 constexpr int EMAP_PIX = 2544;     // LDS map pixels of 64 B (162,816 B; the level table fits beside)
 // head_dim 36 (TAIL): the value as a 32-channel plane + a 4-channel TAIL plane (8 B per pixel,
-// kinet_gemm_headmajor_split); the LDS map holds both, 72 B per pixel: 2261 main pixels, then the
-// tail map (pixel x at ETB + 8x, the same pixel indexing as the main map)
-constexpr int EMAP_T = 2261;
+// kinet_gemm_headmajor_split); the LDS map holds both, 72 B per pixel: 2256 main pixels, then the
+// tail map (pixel x at ETB + 8x, the same pixel indexing as the main map).  Both fills round up
+// (main: pieces of 16 pixels, tail: 256-byte pieces), so the main budget is a multiple of 16 (its
+// last piece must not reach the tail map) and the tail's rounded fill stays inside the array
+constexpr int EMAP_T = 2256;
 constexpr int ETB = EMAP_T * 64;
+static_assert(EMAP_T % 16 == 0 && ETB + (EMAP_T * 2 + 63) / 64 * 256 <= EMAP_PIX * 64, "tail map layout");
 constexpr int EWT = 12;   // TAIL: waves per workgroup (3 per SIMD: the tail's registers need > 128 VGPRs)
 constexpr int EL = 4, EP = 4;      // levels, points (the configs' values; host-checked)
 constexpr int EREC = EL * EP * 3;  // head-major offsets/logits per query and head (48)
@@ -863,9 +866,9 @@ int encoder_forward(const void* value, int64_t value_sb, int64_t value_sm, const
     KINET_CHECK_ARG(channels == (has_tail ? 36 : 32) && num_levels == EL && num_point == EP,
                     "msda encoder: head_dim %d, 4 levels, 4 points (got %d, %d, %d)", has_tail ? 36 : 32, channels,
                     num_levels, num_point);
-    KINET_CHECK_ARG(!has_tail || (!rec && ((uintptr_t)tail % 16) == 0 && tail_sb % 8 == 0 && tail_sm % 8 == 0 &&
+    KINET_CHECK_ARG(!has_tail || (!rec && ((uintptr_t)tail % 8) == 0 && tail_sb % 4 == 0 && tail_sm % 4 == 0 &&
                                   tail_sb >= (int64_t)spatial_size * 4 && tail_sm >= tail_sb),
-                    "msda encoder: tail plane must be 16-byte aligned (M, B, S, 4) with offsets/logits input");
+                    "msda encoder: tail plane must be an 8-byte aligned (M, B, S, 4) plane, offsets/logits input");
     if (!rec)
         KINET_CHECK_ARG(ref_dim == 2 || ref_dim == 4, "Last dim of reference_points must be 2 or 4, but get %d instead.",
                         ref_dim);

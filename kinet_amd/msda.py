@@ -181,12 +181,17 @@ class MSDeformAttn(nn.Module):
                                   out_dtype=query.dtype, query_tile_order=query_order)
         w, b = self.packed_offsets_weights()
         # bf16 compute: offsets/logits in f16 (half the bytes of f32 through HBM twice; f16
-        # keeps 11 mantissa bits for the pixel offsets); parity mode stays f32
-        od = torch.float16 if query.dtype == torch.bfloat16 else torch.float32
+        # keeps 11 mantissa bits for the pixel offsets); parity mode stays f32.  The f16 offsets
+        # and the bf16-from-f16 output are the head_dim-32 fast kernel's; other head dims (36)
+        # run the generic kernel on f32 offsets with the values' own output dtype
+        fast = self.d_model // self.n_heads == 32
+        od = torch.float16 if query.dtype == torch.bfloat16 and fast else torch.float32
         offlog = K.linear(query, w, b, out_dtype=od, x_add=query_add)
-        return K.msda_fused(value, input_spatial_shapes, offlog, reference_points,
-                            self.n_heads, self.n_levels, self.n_points, query_attn_mask,
-                            head_major=(value.dim() == 4), out_dtype=query.dtype, query_tile_order=query_order)
+        out = K.msda_fused(value, input_spatial_shapes, offlog, reference_points,
+                           self.n_heads, self.n_levels, self.n_points, query_attn_mask,
+                           head_major=(value.dim() == 4), out_dtype=query.dtype if fast else value.dtype,
+                           query_tile_order=query_order)
+        return out if out.dtype == query.dtype else out.to(query.dtype)
 
     def _forward_autograd(self, query, reference_points, input_flatten, input_spatial_shapes,
                           input_padding_mask, query_attn_mask):

@@ -153,9 +153,11 @@ def sample_records(loc, attw, ref, shapes, fb):
     """(loc, attw) as above + the (B, Lq, L, 2|4) reference points -> records (M, B, Lq, 24)
     int32 (96 bytes: [4 levels x 4 u32 locations | 4 levels x 4 f16 weights]), the encoding
     include/kinet_msda.h states: per sample h = y*H - 0.5, w = x*W - 0.5 (cuh:227-228); outside
-    (-1, H) x (-1, W) (cuh:229) weight 0 at the query's own pixel; a top row -1 becomes row 0 with
-    the weight times lh and lh = 0, a bottom row H-1 keeps the weight times (1 - lh) and lh = 0,
-    the same for columns; fractions rounded to fb bits (a carry moves the corner)."""
+    (-1, H) x (-1, W) (cuh:229) weight 0; a top row -1 becomes row 0 with the weight times lh and
+    lh = 0, a bottom row H-1 keeps the weight times (1 - lh) and lh = 0, the same for columns;
+    the location is the coordinate clamped into the level, rounded to fb fraction bits (a carry
+    moves the corner) -- exactly the folded corner + fraction above; a sample outside the level
+    has weight 0 at the query's own pixel."""
     loc = loc.double()
     a = attw.double().clone()
     B, Lq, M, L, P, _ = loc.shape
@@ -179,21 +181,17 @@ def sample_records(loc, attw, ref, shapes, fb):
     wl = torch.where(left, torch.zeros_like(wl), torch.where(right, W - 1 + 0 * wl, wl))
     lw = torch.where(left | right, torch.zeros_like(lw), lw)
     s = float(1 << fb)
-    qh, qw = torch.floor(lh * s + 0.5), torch.floor(lw * s + 0.5)
-    hl = torch.where(qh >= s, hl + 1, hl)
-    qh = torch.where(qh >= s, torch.zeros_like(qh), qh)
-    wl = torch.where(qw >= s, wl + 1, wl)
-    qw = torch.where(qw >= s, torch.zeros_like(qw), qw)
+    a = torch.where(valid, a, torch.zeros_like(a))
+    # fixed point of the clamped coordinate (= the folded corner + rounded fraction in the level)
+    ph = torch.floor(torch.minimum(torch.clamp(h, min=0.0), H - 1) * s + 0.5)
+    pw = torch.floor(torch.minimum(torch.clamp(w, min=0.0), W - 1) * s + 0.5)
     # outside the level: the query's own pixel, weight 0
     r = ref.double()[:, :, None, :, None, :]
-    hr = torch.clamp(torch.floor(r[..., 1] * H), torch.zeros_like(H), H - 1).expand_as(hl)
-    wr = torch.clamp(torch.floor(r[..., 0] * W), torch.zeros_like(W), W - 1).expand_as(wl)
-    a = torch.where(valid, a, torch.zeros_like(a))
-    hl = torch.where(valid, hl, hr)
-    wl = torch.where(valid, wl, wr)
-    qh = torch.where(valid, qh, torch.zeros_like(qh))
-    qw = torch.where(valid, qw, torch.zeros_like(qw))
-    word = (hl.long() << (16 + fb)) | (qh.long() << 16) | (wl.long() << fb) | qw.long()   # (B, Lq, M, L, P)
+    hr = torch.clamp(torch.floor(r[..., 1] * H), torch.zeros_like(H), H - 1).expand_as(ph)
+    wr = torch.clamp(torch.floor(r[..., 0] * W), torch.zeros_like(W), W - 1).expand_as(pw)
+    ph = torch.where(valid, ph, hr * s)
+    pw = torch.where(valid, pw, wr * s)
+    word = (ph.long() << 16) | pw.long()   # (B, Lq, M, L, P)
     word = word.to(torch.int64) & 0xffffffff
     locw = torch.where(word >= 2 ** 31, word - 2 ** 32, word).to(torch.int32)
     a16 = (a.to(torch.float16).view(torch.int16).to(torch.int32) & 0xffff).reshape(B, Lq, M, L * P)

@@ -85,6 +85,8 @@ def test_conv_fwd_bwd(cin, cout, k, stride, pad, bn, relu, res, bias):
     _close(y.detach(), z.detach().permute(0, 2, 3, 1), name='y')
     _close(x.grad, x2.grad.permute(0, 2, 3, 1), name='dx')
     _close(w.grad, w2.grad, name='dw')
+    # the parameter's own strides (DDP's bucket views copy a gradient whose strides differ)
+    assert w.grad.stride() == w.stride(), (w.grad.stride(), w.stride())
     if bias:
         _close(b.grad, b2.grad, name='db')
     if res:

@@ -23,10 +23,13 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-3
 # 16-bit compute vs the fp32 HIP path on the same frame and weights: max |diff| per tensor.
 # Logits/hs are O(1..10) (random-init weights keep activations O(1)); boxes are in [0, 1].
-# Measured on MI355X (profiles/r02b_fullsize_tolerances.log): bf16 0.188 / 0.0167 / 0.192,
-# fp16 0.054 / 0.0038 / 0.058; the bounds are ~2x the measured max.
-BF16_TOL = {'pred_logits': 0.4, 'pred_boxes': 0.035, 'hs_embed': 0.4}
-F16_TOL = {'pred_logits': 0.12, 'pred_boxes': 0.008, 'hs_embed': 0.12}
+# Measured on MI355X on the round-5 timed path (records sampling with 1/256-px locations, folded
+# bottleneck pairs, the stem from the f32 image; config 5 on the split head_dim-36 strip kernel),
+# profiles/r05b_fullsize_tolerances.log: bf16 0.1945 / 0.0182 / 0.2878, fp16 0.0509 / 0.0062 /
+# 0.0813 (round 2: bf16 0.188 / 0.0167 / 0.192, fp16 0.054 / 0.0038 / 0.058); the bounds are
+# ~1.6x the measured max.
+BF16_TOL = {'pred_logits': 0.3, 'pred_boxes': 0.03, 'hs_embed': 0.45}
+F16_TOL = {'pred_logits': 0.08, 'pred_boxes': 0.01, 'hs_embed': 0.13}
 
 
 def _frame(seed, h, w):

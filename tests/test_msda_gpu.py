@@ -551,7 +551,8 @@ def test_encoder_split_kernel_matches_generic(shapes, ref_dim, noise, out_dtype,
     order = K.encoder_tile_order(shapes, value.device) if Lq == S else None
     o_enc = K.msda_encoder_split(_split(value), shapes, _hm(offlog, M), ref, M, qm, out_dtype=out_dtype,
                                  query_tile_order=order)
-    o_gen = K.msda_fused(value, ss, offlog, ref, M, 4, P, qm, head_major=True, out_dtype=out_dtype)
+    # the generic kernel in f32 on the same (f16-exact) values and offsets / logits
+    o_gen = K.msda_fused(value.float(), ss, offlog.float(), ref, M, 4, P, qm, head_major=True)
     torch.cuda.synchronize()
     ulp = 2.0 ** -7 if out_dtype == torch.bfloat16 else 2.0 ** -10
     d = (o_enc.float() - o_gen.float()).abs()
@@ -578,8 +579,8 @@ def test_encoder_split_kernel_vs_oracle():
     value, ss, offlog, ref, qmask = _fused_inputs(B, shapes, Lq, M, P, 2, 3.0, 81, dtype=torch.float16, D=36)
     offlog = offlog.half()
     out = K.msda_encoder_split(_split(value), shapes, _hm(offlog, M), ref, M, qmask, out_dtype=torch.float16)
-    _, loc, aw = K.msda_fused(value, ss, offlog, ref, M, 4, P, qmask, want_loc_attw=True, head_major=True,
-                              out_dtype=torch.float16)
+    _, loc, aw = K.msda_fused(value.float(), ss, offlog.float(), ref, M, 4, P, qmask, want_loc_attw=True,
+                              head_major=True)
     torch.cuda.synchronize()
     v = value.float().permute(1, 2, 0, 3).contiguous().cpu().numpy()
     ref_out = torch.from_numpy(O.fwd(v, ss.cpu().numpy(), loc.cpu().numpy(), aw.cpu().numpy())).reshape(out.shape)
