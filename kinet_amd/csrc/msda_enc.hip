@@ -472,10 +472,13 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
             const uint32_t ob = quad_bcast<LV>(rec_o[p]);
             const uint32_t o = ob + cb;
             if constexpr (TAIL) {
-                // head-map offset / 8 = tail-plane offset of (hl, wl); an invalid sample's TAF
-                // offset lands past the tail plane's range (reads 0)
-                const uint32_t tco = (tr ? (uint32_t)wb[LV] >> 3 : 0u) + (uint32_t)tc * 8u;
-                gt[p] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rt, (ob >> 3) + tco, 0, 0));
+                // head-map offset / 8 = tail-plane offset; this lane's corner is added in the
+                // 64-byte domain first, where a footprint starting at row / column -1 wraps back
+                // to its in-level corners exactly as the main loads' offsets do (the shift must
+                // not see the wrapped value); an invalid sample's TAF offset lands past the tail
+                // plane's range (reads 0)
+                const uint32_t co = (tr ? (uint32_t)wb[LV] : 0u) + (uint32_t)tc * 64u;
+                gt[p] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rt, (ob + co) >> 3, 0, 0));
             }
             const uint32_t o1 = o + (uint32_t)wb[LV];
             g[p][0] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rv, o, 0, 0));

@@ -559,7 +559,8 @@ def test_encoder_split_kernel_matches_generic(shapes, ref_dim, noise, out_dtype,
     vmax = value.float().abs().max().item()
     big = torch.maximum(o_gen.float().abs(), o_enc.float().abs())
     bad = d > big * ulp + (2.0 ** -7 + 2.0 ** -11) * vmax
-    assert not bad.any(), (d.max().item(), bad.view(B, Lq, M, 36).sum((0, 1, 2)).tolist())
+    assert not bad.any(), (d.max().item(), int(bad.sum()),
+                           [(c, n) for c, n in enumerate(bad.view(B, Lq, M, 36).sum((0, 1, 2)).tolist()) if n])
     assert d.mean().item() <= 2e-3, d.mean().item()
     tail = d.view(B, Lq, M, 36)[..., 32:]
     assert tail.mean().item() <= 2e-3, tail.mean().item()
