@@ -343,8 +343,24 @@ class Joiner(nn.Sequential):
         out, pos = [], []
         for x in xs.values():
             out.append(x)
-            pos.append(self[1](x).to(x.tensors.dtype))
+            pos.append(self._pos(x))
         return out, pos
+
+    def _pos(self, x):
+        """The position embedding of level x (a function of its padding mask only).  When the mask
+        is fully determined by the image sizes (NestedTensor.sizes), the embedding is cached per
+        (sizes, level shape, dtype, device): the training path's op-for-op forward otherwise
+        recomputes 2 x 4 levels x frames of it per step."""
+        if x.sizes is None:
+            return self[1](x).to(x.tensors.dtype)
+        key = (x.sizes, tuple(x.tensors.shape), x.tensors.dtype, str(x.tensors.device))
+        cache = self.__dict__.setdefault('_pos_cache', {})
+        p = cache.get(key)
+        if p is None:
+            if len(cache) >= 16:
+                cache.clear()
+            p = cache[key] = self[1](x).to(x.tensors.dtype)
+        return p
 
 
 def build_backbone(args):

@@ -319,7 +319,8 @@ class DeformableDETR(nn.Module):
         for i in body.return_idx:
             x = xs[str(i)]
             features_all.append(NestedTensor(x, interp_mask(samples.mask, x.shape[-2:]), samples.sizes))
-        pos = [self.backbone[1](f).to(f.tensors.dtype) for f in features_all]
+        # (cached per image geometry: the embedding is a function of the padding mask only)
+        pos = [self.backbone._pos(f) for f in features_all]
         features = features_all[-3:]
         prev_features = features if prev_features is None else prev_features[-3:]
         frame_features = [prev_features, features] if self.multi_frame_attention else [features]
@@ -337,7 +338,7 @@ class DeformableDETR(nn.Module):
                 for l in range(_len, n_lv):
                     src = self._input_proj_autograd(l, frame_feat[-1].tensors if l == _len else src_list[-1])
                     m = interp_mask(frame_feat[0].mask, src.shape[-2:])
-                    pos_l = self.backbone[1](NestedTensor(src, m)).to(src.dtype)
+                    pos_l = self.backbone._pos(NestedTensor(src, m, getattr(frame_feat[0], 'sizes', None)))
                     src_list.append(src)
                     mask_list.append(m)
                     pos_list.append(pos_l[:, frame] if three_d else pos_l)
