@@ -91,6 +91,8 @@ def parse():
     ap.add_argument('--msda-records', type=int, default=1,
                     help='1: encoder MSDA calls through the sampling records (kinet_msda_sample_records); '
                          '0: the f16 offsets / logits path (A/B)')
+    ap.add_argument('--enc-panels', type=int, default=None,
+                    help='column panels per strip of the encoder MSDA tile order (kernels.ENC_PANELS; A/B)')
     ap.add_argument('--bneck-pairs', type=int, default=1,
                     help='1: ResNet stage-1 bottleneck pairs (conv3 -> next conv1) as one launch '
                          '(kinet_bottleneck_pair); 0: every conv on its own (A/B)')
@@ -267,6 +269,10 @@ def summarize_trace(trace, steps_traced=1):
         a['launches'] += 1
         if f == 'msda':
             msda.append((work.get('Lq'), work.get('S'), ms, work['bytes'], work.get('kernel', '?')))
+        elif work.get('role') == 'msda_prep':
+            # the projection that prepares an MSDA call (sampling records / offsets + logits):
+            # Lq = rows per frame, S = None (it is neither an encoder nor a decoder sampler launch)
+            msda.append((work['shape'][0], None, ms, work['bytes'], name, 'prep'))
     for a in fam.values():
         for k in ('ms', 'flops', 'bytes', 'launches'):
             a[k] /= steps_traced
@@ -533,6 +539,8 @@ def msda_roofline(name, msda, dec_touched):
     launches beside it; PMC traffic from the committed per-kernel summary."""
     if not msda:
         return None
+    prep = [m for m in msda if len(m) > 5]
+    msda = [m for m in msda if len(m) == 5]
     enc = [m for m in msda if m[0] == m[1]]
     dec = [m for m in msda if m[0] != m[1]]
 
@@ -567,6 +575,26 @@ def msda_roofline(name, msda, dec_touched):
                            'bytes': enc[0][3] if enc else None}
     r['decoder_launch'] = {'ms': statistics.mean(m[2] for m in dec) if dec else None,
                            'bytes': dec[0][3] if dec else None}
+    if enc:
+        # one encoder MSDA call = the projection that prepares it (records GEMM, or the head-major
+        # offsets / logits GEMM) + the sampler.  The encoder's prep launches are those with
+        # B*Lq = B*S rows: the decoder's run on the query rows only.
+        cand = [m for m in prep if m[0] % enc[0][0] == 0]
+        rows = max(m[0] for m in cand) if cand else None
+        ep = [m for m in cand if m[0] == rows]
+        if ep and len(ep) == len(enc):
+            p_ms = statistics.mean(m[2] for m in ep)
+            p_b = ep[0][3]
+            c_ms = p_ms + r['avg_launch_ms']
+            c_b = p_b + r['algorithmic_bytes_per_launch']
+            r['encoder_call'] = {
+                'ms': c_ms, 'prep_ms': p_ms, 'sampler_ms': r['avg_launch_ms'],
+                'prep_kernel': ep[0][4].split('(')[0][:120],
+                'bytes': c_b, 'prep_bytes': p_b, 'sampler_bytes': r['algorithmic_bytes_per_launch'],
+                'achieved': c_b / (c_ms * 1e-3) / 1e9, 'unit': 'GB/s', 'peak': HBM_PEAK_GBS,
+                'frac': c_b / (c_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                'basis': 'prep GEMM (input rows + weights + records or offsets/logits out) + sampler '
+                         '(value + records or offsets/logits + output), HIP events, single stream'}
     return r
 
 
@@ -585,6 +613,8 @@ def main():
         _native.lib().kinet_ffn_set_debug(a.ffn_knob)
     from kinet_amd import kernels as K
     K.MSDA_RECORDS[0] = bool(a.msda_records)
+    if a.enc_panels is not None:
+        K.ENC_PANELS[0] = a.enc_panels
     from kinet_amd.models import backbone as BB
     BB.FUSE_BOTTLENECK_PAIRS = bool(a.bneck_pairs)
     BB.STEM_FROM_IMAGE = bool(a.stem_image)

@@ -705,6 +705,50 @@ def encoder_tile_order(shapes, device, qt=16):
     return o
 
 
+# column panels per strip of the encoder's tile order (strip_panel_order); 1 = row sweeps
+ENC_PANELS = [1]
+_panel_orders = {}
+
+
+def strip_panel_order(order, shapes, nstrip, panels, qt=16):
+    """The encoder tile order `order` (encoder_tile_order: tiles sorted by normalised row)
+    re-sorted WITHIN each strip of the strip kernel's plan -- the contiguous slices
+    [s*n/nstrip, (s+1)*n/nstrip) of the order, one per workgroup of a head map -- by
+    (column panel, row): a strip walks `panels` vertical panels one after another instead of
+    sweeping whole rows.  Every strip keeps the same set of tiles (so the same staged LDS rows,
+    msda_enc.hip strip_rows) and any order gives the same per-query results; what changes is the
+    reuse distance of the texture-gathered levels' rows in L2 (a row of level 0 is reused by the
+    tiles a few rows away, 1/panels of a row sweep later).  Cached per (order, nstrip, panels)."""
+    if panels <= 1 or nstrip < 1 or order is None:
+        return order
+    key = (tuple(tuple(int(v) for v in s) for s in shapes), order.data_ptr(), int(nstrip), int(panels))
+    o = _panel_orders.get(key)
+    if o is None:
+        import numpy as np
+        base = order.cpu().numpy().astype(np.int64)
+        hw = np.array([h * w for h, w in key[0]], dtype=np.int64)
+        starts = np.concatenate([[0], np.cumsum(hw)[:-1]])
+        q = base * qt
+        lvl = np.searchsorted(starts, q, side='right') - 1
+        H = np.array([h for h, _ in key[0]], dtype=np.float64)[lvl]
+        W = np.array([w for _, w in key[0]], dtype=np.int64)[lvl]
+        r = q - starts[lvl]
+        y = (r // W + 0.5) / H
+        x = (r % W + 0.5) / W
+        pan = np.minimum((x * panels).astype(np.int64), panels - 1)
+        n = base.size
+        out = np.empty_like(base)
+        for st in range(nstrip):
+            t0, t1 = st * n // nstrip, (st + 1) * n // nstrip
+            idx = np.lexsort((np.arange(t1 - t0), y[t0:t1], pan[t0:t1]))
+            out[t0:t1] = base[t0:t1][idx]
+        o = torch.as_tensor(out.astype(np.int32), device=order.device)
+        _panel_orders[key] = (o, order)   # keep the base alive: its data_ptr is part of the key
+    else:
+        o = o[0]
+    return o
+
+
 _host_shapes = {}
 _enc_plans = {}
 # template-argument spelling of the element types in rocprofv3 kernel names
@@ -767,6 +811,8 @@ def msda_encoder_split(value, shapes, offlog_hm, reference_points, n_heads, quer
     offlog_hm = offlog_hm.contiguous()
     nsamp = B * Lq * M_ * 16
     plan = msda_encoder_plan(key, B, M_, Lq, 36)
+    if plan and query_tile_order is not None:
+        query_tile_order = strip_panel_order(query_tile_order, key, plan[1], ENC_PANELS[0])
     kname = 'msda_enc_kernel<%s, %d, %d, %s, false, true, 12>' % (_KT[od], plan[0] if plan else -1, ref.shape[-1],
                                                                   'true' if qm is not None else 'false')
     N.call('kinet_msda_encoder_forward_split', N.ptr(main), main.stride(1), main.stride(0), N.ptr(tail),
@@ -812,6 +858,7 @@ def offsets_proj_headmajor(x, weight, bias, heads, x_add=None, out_dtype=torch.f
     N.call('kinet_gemm_headmajor_ex', N.ptr(x2), N.ptr(a2), N.ptr(w), N.ptr(out), B * Lq, Nout, K, x2.stride(0), K,
            N.dtype_code(x.dtype), N.dtype_code(out_dtype), N.ptr(f32(bias)), None, Lq, rec, N.stream(x.device),
            work={'family': 'gemm', 'flops': 2.0 * B * Lq * Nout * K, 'shape': (B * Lq, Nout, K),
+                 'role': 'msda_prep',
                  'bytes': (B * Lq * K * (2 if a2 is not None else 1) + Nout * K) * e + B * Lq * Nout * 2})
     return out
 
@@ -837,6 +884,8 @@ def msda_encoder(value, shapes, offlog_hm, reference_points, n_heads, query_attn
     offlog_hm = offlog_hm.contiguous()
     nsamp = B * Lq * M_ * 16
     plan = msda_encoder_plan(key, B, M_, Lq)
+    if plan and query_tile_order is not None:
+        query_tile_order = strip_panel_order(query_tile_order, key, plan[1], ENC_PANELS[0])
     # the instantiation kinet_msda_encoder_forward launches (as rocprofv3 names it)
     kname = 'msda_enc_kernel<%s, %d, %d, %s>' % (_KT[od], plan[0] if plan else -1, ref.shape[-1],
                                                    'true' if qm is not None else 'false')
@@ -897,6 +946,7 @@ def msda_sample_records(x, weight, bias, heads, reference_points, shapes_host, x
            x2.stride(0), N.dtype_code(x.dtype), N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(hs), 4, 4, fb, N.ptr(rec),
            N.stream(x.device),
            work={'family': 'gemm', 'flops': 2.0 * B * Lq * heads * 48 * K_, 'shape': (B * Lq, heads * 48, K_),
+                 'role': 'msda_prep',
                  'bytes': (B * Lq * K_ * (2 if a2 is not None else 1) + heads * 48 * K_) * e + ref.numel() * 4
                  + rec.numel() * 4})
     return rec, fb
@@ -920,6 +970,8 @@ def msda_encoder_records(value, shapes, records, frac_bits, out_dtype=None, quer
     records = records.contiguous()
     nsamp = B * Lq * M_ * 16
     plan = msda_encoder_plan(key, B, M_, Lq)
+    if plan and query_tile_order is not None:
+        query_tile_order = strip_panel_order(query_tile_order, key, plan[1], ENC_PANELS[0])
     kname = 'msda_enc_kernel<%s, %d, 2, false, true>' % (_KT[od], plan[0] if plan else -1)
     N.call('kinet_msda_encoder_forward_records', N.ptr(value), value.stride(1), value.stride(0), N.ptr(hs),
            N.ptr(records), int(frac_bits), N.ptr(out), B, S, M_, D, 4, Lq, 4, N.dtype_code(od),

@@ -1,9 +1,9 @@
-"""Per-launch table of one config-2 inference forward (bench.py's model and input), aggregated
+"""Per-launch table of one inference forward of a bench workload (default config 2) (bench.py's model and input), aggregated
 by (kernel entry point, shape): launches, average us, achieved TFLOP/s and GB/s from the
 algorithmic flops / bytes each launch reports, sorted by total time.  HIP events around every
 launch on one stream (kinet_amd._native.trace_begin / trace_end).
 
-usage: python tools/launch_table.py [--batch 16] [--top 40]
+usage: python tools/launch_table.py [--workload config2|config3|config5] [--batch N] [--top 40]
 """
 import argparse
 import os
@@ -19,27 +19,42 @@ from kinet_amd import _native  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--batch', type=int, default=16)
+    ap.add_argument('--workload', default='config2', choices=sorted(bench.WORKLOADS))
+    ap.add_argument('--batch', type=int, default=None, help='default: the workload\'s bench batch')
     ap.add_argument('--top', type=int, default=40)
     ap.add_argument('--gemm-flags', type=int, default=0, help='kinet_gemm_set_flags value (A/B runs)')
     ap.add_argument('--filter', default='', help='only rows whose shape contains this text')
     a = ap.parse_args()
     if a.gemm_flags:
         _native.lib().kinet_gemm_set_flags(a.gemm_flags)
-    wl = bench.WORKLOADS['config2']
+    wl = bench.WORKLOADS[a.workload]
+    a.batch = a.batch or wl['batch']
     dev = torch.device('cuda', 0)
     dt = {'bf16': torch.bfloat16, 'f16': torch.float16, 'f32': torch.float32}[wl['dtype']]
     model = bench.build(dev, dt, wl)
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(a.batch, 3, wl['h'], wl['w'], device=dev, generator=g)
+    extra = ()
+    if wl['K']:
+        # tracking inputs as bench.run_workload builds them: K track queries per frame and the
+        # previous frame's features
+        K_, d = wl['K'], model.hidden_dim
+        with torch.no_grad():
+            feats = model(list(torch.randn(a.batch, 3, wl['h'], wl['w'], device=dev, generator=g)))[2]
+        boxes = torch.cat([torch.rand(a.batch, K_, 2, generator=g, device=dev) * 0.8 + 0.1,
+                           torch.rand(a.batch, K_, 2, generator=g, device=dev) * 0.2 + 0.02], -1)
+        hs = torch.randn(a.batch, K_, d, generator=g, device=dev)
+        extra = ([{'track_query_hs_embeds': hs[b], 'track_query_boxes': boxes[b]} for b in range(a.batch)], feats)
     with torch.no_grad():
         for _ in range(2):
-            model(list(x))
+            model(list(x), *extra)
     torch.cuda.synchronize()
     _native.trace_begin()
-    with torch.no_grad():
-        model(list(x))
-    trace = _native.trace_end()
+    try:
+        with torch.no_grad():
+            model(list(x), *extra)
+    finally:
+        trace = _native.trace_end()
     torch.cuda.synchronize()
     agg = {}
     tot = 0.0
