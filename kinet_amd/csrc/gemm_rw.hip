@@ -34,33 +34,50 @@
 namespace kinet {
 namespace {
 
-template <int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2, bool PREP = false>
+// NW waves per workgroup (4, or 6 for the d = 288 LayerNorm rows: 6 x 48 = 288 columns);
+// rows of K = 32*KC 16-bit elements: a power-of-two number of 16-byte chunks, or a multiple of
+// 4 (K = 288: 36 chunks).  A tile region whose bytes are not whole DMA rounds (NW*64 lanes x
+// 16 B) is padded to whole rounds; the padding chunks read zeros (out of range) and nothing
+// reads them back.
+template <int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2, bool PREP = false, int NW = 4>
 struct RwCfg {
+    static constexpr int NTHR = NW * 64;
+    static constexpr int OPB = NTHR * 16;                   // bytes per DMA round
     static constexpr int ROW = KC * 64;                     // A row bytes (K = 32*KC, 16-bit)
     static constexpr int CPR = ROW / 16;                    // 16-byte chunks per A row
+    static constexpr bool POW2 = (CPR & (CPR - 1)) == 0;
     static constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;   // source-side XOR swizzle mask
-    static constexpr int GW = 4 * NT * 16;                  // columns per workgroup
+    static constexpr int GW = NW * NT * 16;                 // columns per workgroup
     static constexpr int A_BYTES = BMR * ROW;
-    static constexpr int A2_BYTES = HAS_A2 ? A_BYTES : 0;   // second A operand (A + A2)
+    static constexpr int A_OPS = (A_BYTES + OPB - 1) / OPB;   // DMA instructions per thread per tile
+    static constexpr int A_SPAN = A_OPS * OPB;
+    static constexpr int A2_BYTES = HAS_A2 ? A_SPAN : 0;    // second A operand (A + A2)
     static constexpr int R_ROW = GW * 2;
     static constexpr int R_CPR = R_ROW / 16;
+    static constexpr bool R_POW2 = (R_CPR & (R_CPR - 1)) == 0;
     static constexpr int R_SWM = (R_CPR < 16 ? R_CPR : 16) - 1;
-    static constexpr int R_BYTES = HAS_R ? BMR * R_ROW : 0;
-    static constexpr int R_OFF = A_BYTES + A2_BYTES;
+    static constexpr int R_OPS = HAS_R ? (BMR * R_ROW + OPB - 1) / OPB : 0;
+    static constexpr int R_BYTES = R_OPS * OPB;
+    static constexpr int R_OFF = A_SPAN + A2_BYTES;
     static constexpr int MASK_OFF = R_OFF + R_BYTES;
     static constexpr int REF_OFF = MASK_OFF + 1024;         // PREP: the tile's reference points
     static constexpr int REF_OPS = PREP ? BMR / 16 : 0;     // 1 KiB DMAs: BMR rows x 4 levels x <= 16 B
     static constexpr int STAGE = REF_OFF + REF_OPS * 1024;  // + one DMA of row-mask bytes (+ refs)
     static constexpr int PAR = 4 * GW * 4;                  // scale, bias, gamma, beta (f32)
-    static constexpr int LNS = LN ? 2 * BMR * 4 * 4 : 0;    // [2][BMR][4 waves] partial sums
+    static constexpr int LNS = LN ? 2 * BMR * NW * 4 : 0;   // [2][BMR][NW waves] partial sums
     static constexpr int BYTES = PAR + LNS + NS * STAGE;
-    static constexpr int A_OPS = A_BYTES / 4096;            // DMA instructions per thread per tile
-    static constexpr int R_OPS = R_BYTES / 4096;
     static constexpr int D = A_OPS * (HAS_A2 ? 2 : 1) + R_OPS + 1 + REF_OPS;
-    static_assert(!PREP || (NT == 3 && (BMR == 16 || BMR == 32) && !HAS_R && !LN),
-                  "sampling records: 12 columns per lane, 16- or 32-row tiles");
-    static_assert(A_BYTES % 4096 == 0 && R_BYTES % 4096 == 0, "whole DMA rounds per tile");
-    static_assert((CPR & (CPR - 1)) == 0 && (!HAS_R || (R_CPR & (R_CPR - 1)) == 0), "power-of-two rows");
+    // LDS position of 16-byte chunk c of tile row r (an involution: the DMA fills position c
+    // with source chunk sw(r, c), a reader of logical chunk q reads position sw(r, q)).  Rows of
+    // 36 chunks (K = 288, 576 B = 144 banks: rows r and r + 4 share banks) swap chunks within
+    // aligned groups of 4 by (r >> 2) & 3, so 16 rows read at one chunk hit 16 distinct
+    // 4-bank groups
+    __device__ static constexpr int sw(int r, int c) { return POW2 ? c ^ (r & SWM) : c ^ ((r >> 2) & 3); }
+    __device__ static constexpr int rsw(int r, int c) { return R_POW2 ? c ^ (r & R_SWM) : c ^ ((r >> 2) & 3); }
+    static_assert(!PREP || (NT == 3 && NW == 4 && (BMR == 16 || BMR == 32) && !HAS_R && !LN),
+                  "sampling records: 4 waves x 12 columns per lane, 16- or 32-row tiles");
+    static_assert(POW2 || CPR % 4 == 0, "A rows: power-of-two or multiple-of-4 chunks");
+    static_assert(!HAS_R || R_POW2 || R_CPR % 4 == 0, "residual rows: power-of-two or multiple-of-4 chunks");
     static_assert(BMR / 16 <= 64, "mask DMA lanes");
 };
 
@@ -75,6 +92,20 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+}
+
+// the NW waves' partial sums of one row, in wave order
+template <int NW>
+__device__ __forceinline__ float wave_sum(const float* w) {
+    if constexpr (NW == 4) {
+        const f32x4 w4 = *reinterpret_cast<const f32x4*>(w);
+        return w4[0] + w4[1] + w4[2] + w4[3];
+    } else {
+        float s = w[0];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) s += w[i];
+        return s;
+    }
 }
 
 template <typename TO> struct Pack;
@@ -203,9 +234,10 @@ __device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_
 // pack_image_kwfold_kernel): K = KH*Cin, logical chunk q of the row = 8 channels of tap
 // kh = q / (Cin/8) read from input row oh*stride - pad + kh (zeros outside the image and past K)
 template <typename T, typename TO, int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2, bool CR,
-          bool PREP = false, int OCC = 2, int DIAG = 0>
-__global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, const int n_mtiles) {
-    using C_ = RwCfg<KC, NT, BMR, NS, HAS_R, LN, HAS_A2, PREP>;
+          bool PREP = false, int OCC = 2, int DIAG = 0, int NW = 4>
+__global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p, const int n_mtiles) {
+    using C_ = RwCfg<KC, NT, BMR, NS, HAS_R, LN, HAS_A2, PREP, NW>;
+    constexpr int NTHR = C_::NTHR;
     constexpr int TMR = BMR / 16;             // 16-row MFMA tiles per row tile
     constexpr int GW = C_::GW;
     constexpr int NC = NT * 4;                // consecutive columns per lane
@@ -223,7 +255,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
     const int M = p.M, N = p.N;
     const int cnt = bx < n_mtiles ? (n_mtiles - 1 - bx) / P + 1 : 0;
 
-    for (int i = tid; i < GW; i += 256) {
+    for (int i = tid; i < GW; i += NTHR) {
         const int n = ncol0 + i;
         const bool ok = n < N;
         par[i] = (ok && p.scale) ? p.scale[n] : 1.f;
@@ -268,15 +300,15 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
     int cr_kh[C_::A_OPS];
 #pragma unroll
     for (int j = 0; j < C_::A_OPS; ++j) {
-        const int idx = j * 256 + tid;
+        const int idx = j * NTHR + tid;
         const int row = idx / C_::CPR, s = idx % C_::CPR;
-        a_row[j] = row;
-        a_lo[j] = ((unsigned)row * (unsigned)p.lda + (unsigned)((s ^ (row & C_::SWM)) * 8)) * 2u;
+        a_row[j] = row < BMR ? row : (1 << 30);   // round padding: never in range
+        a_lo[j] = ((unsigned)row * (unsigned)p.lda + (unsigned)(C_::sw(row, s) * 8)) * 2u;
         cr_kh[j] = 0;
         if (CR) {
             // tap and in-tap channel offset of logical chunk q (lane constants); chunks past K
             // get a tap index that never lands inside the image
-            const int q = s ^ (row & C_::SWM), cpt = p.Cin >> 3;
+            const int q = C_::sw(row, s), cpt = p.Cin >> 3;
             const int kh = q / cpt;
             cr_kh[j] = q * 8 < p.K ? kh : (1 << 28);
             a_lo[j] = (unsigned)((q - kh * cpt) * 8);
@@ -286,10 +318,10 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
     int r_row[C_::R_OPS > 0 ? C_::R_OPS : 1];
 #pragma unroll
     for (int j = 0; j < C_::R_OPS; ++j) {
-        const int idx = j * 256 + tid;
+        const int idx = j * NTHR + tid;
         const int row = idx / C_::R_CPR, s = idx % C_::R_CPR;
-        const int n = ncol0 + (s ^ (row & C_::R_SWM)) * 8;
-        r_row[j] = n < N ? row : (1 << 30);   // columns past N: never in range
+        const int n = ncol0 + C_::rsw(row, s) * 8;
+        r_row[j] = (n < N && row < BMR) ? row : (1 << 30);   // columns past N, round padding: never in range
         r_lo[j] = ((unsigned)row * (unsigned)p.ldr + (unsigned)n) * 2u;
     }
     auto issue = [&](int i) {
@@ -317,14 +349,14 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
                 const bool ok = m0 + a_row[j] < M && (unsigned)ih < (unsigned)p.Hin;
                 off = ok ? ((unsigned)((img * p.Hin + ih) * p.Win + ow * p.stride_w) * (unsigned)p.Cin + a_lo[j]) * 2u : OOB;
             }
-            dma16(ra, st + (j * 256 + wave * 64) * 16, off);
-            if (HAS_A2) dma16(ra2, st + C_::A_BYTES + (j * 256 + wave * 64) * 16, off);
+            dma16(ra, st + (j * NTHR + wave * 64) * 16, off);
+            if (HAS_A2) dma16(ra2, st + C_::A_SPAN + (j * NTHR + wave * 64) * 16, off);
         }
         const unsigned rbase = (unsigned)m0 * (unsigned)p.ldr * 2u;
 #pragma unroll
         for (int j = 0; j < C_::R_OPS; ++j) {
             const unsigned off = m0 + r_row[j] < M ? rbase + r_lo[j] : OOB;
-            dma16(rr, st + C_::R_OFF + (j * 256 + wave * 64) * 16, off);
+            dma16(rr, st + C_::R_OFF + (j * NTHR + wave * 64) * 16, off);
         }
         // row-mask bytes m0 .. m0+BMR (every wave writes the same 1 KiB; bytes past M read 0)
         dma16(rm, st + C_::MASK_OFF, lane < TMR ? (unsigned)(m0 + lane * 16) : OOB);
@@ -353,14 +385,22 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
     // counted waits below know exactly how many vector-memory ops are younger than a DMA
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, p.c_bytes, 0x00020000);
     constexpr int EPC16 = 16 / (int)sizeof(TO);     // elements per 16-byte store
+    // store unit: 16 bytes, or 4 columns when a lane's NC columns are not whole 16-byte runs
+    // (NT = 3: 12 columns = 16-bit 8-byte units, never straddling a head of 4k columns)
+    constexpr int SU = NC % EPC16 == 0 ? EPC16 : 4;
+    constexpr int NU = NC / SU;                     // store units per lane-row
+    constexpr int WPU = SU * (int)sizeof(TO) / 4;   // packed words per unit
     // stores per lane per row tile (PREP: one 16-byte location store + one 8-byte weight store)
-    constexpr int S = TMR * (PREP ? 2 : NC / EPC16);
+    constexpr int S = TMR * (PREP ? 2 : NU);
     static_assert(NS >= 2 && NS <= 4 && (NS - 2) * (C_::D + S) <= 63, "ring depth / vmcnt range");
     // element offset of (row m, column n): m * rs + colpart(n); head-major (hm_rows > 0):
-    // ((g*hm_batch + b)*hm_rows + s)*hm_d + d = g*M*hm_d + m*hm_d + d for m = b*hm_rows + s
+    // ((g*hm_batch + b)*hm_rows + s)*hm_d + d = g*M*hm_d + m*hm_d + d for m = b*hm_rows + s;
+    // split head-major (hm_split > 0): columns n >= hm_split in the second plane at
+    // hm_split*M elements, row stride hm_d2 (one 4-column unit per head)
     const int rs = PREP ? 96 / (int)sizeof(TO) : (p.hm_rows ? p.hm_d : p.ldc);
-    constexpr int NSL = PREP ? 2 : NC / EPC16;
+    constexpr int NSL = PREP ? 2 : NU;
     unsigned s_lo[TMR][NSL];
+    unsigned s_rs[NSL];
     bool s_nok[NSL];
     if constexpr (PREP) {
         // record (head h, row m) at (h*M + m)*96 bytes: [4 levels x 16 B locations | 4 levels x 8 B weights];
@@ -374,21 +414,32 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
             s_lo[t][1] = r + 64u + l * 8u;
         }
         s_nok[0] = s_nok[1] = false;
+        s_rs[0] = s_rs[1] = (unsigned)rs;
     }
 #pragma unroll
-    for (int h = 0; h < (PREP ? 0 : NC / EPC16); ++h) {
-        const int n = ncol0 + cl0 + h * EPC16;
+    for (int h = 0; h < (PREP ? 0 : NU); ++h) {
+        const int n = ncol0 + cl0 + h * SU;
         s_nok[h] = n >= N;
-        const int g = p.hm_rows ? n / p.hm_d : 0;
-        const unsigned colpart = p.hm_rows ? (unsigned)g * (unsigned)M * (unsigned)p.hm_d + (unsigned)(n - g * p.hm_d)
-                                           : (unsigned)n;
+        unsigned colpart = (unsigned)n, r_s = (unsigned)rs;
+        if (p.hm_rows) {
+            if (p.hm_split && n >= p.hm_split) {
+                const int n2 = n - p.hm_split, g = n2 / p.hm_d2;
+                colpart = (unsigned)p.hm_split * (unsigned)M + (unsigned)g * (unsigned)M * (unsigned)p.hm_d2 +
+                          (unsigned)(n2 - g * p.hm_d2);
+                r_s = (unsigned)p.hm_d2;
+            } else {
+                const int g = n / p.hm_d;
+                colpart = (unsigned)g * (unsigned)M * (unsigned)p.hm_d + (unsigned)(n - g * p.hm_d);
+            }
+        }
+        s_rs[h] = r_s;
 #pragma unroll
         for (int t = 0; t < TMR; ++t)
-            s_lo[t][h] = ((unsigned)(t * 16 + (lane & 15)) * (unsigned)rs + colpart) * (unsigned)sizeof(TO);
+            s_lo[t][h] = ((unsigned)(t * 16 + (lane & 15)) * r_s + colpart) * (unsigned)sizeof(TO);
     }
     auto store_pending = [&](bool valid) {
-        const unsigned base = (unsigned)pend_m0 * (unsigned)rs * (unsigned)sizeof(TO);
         if constexpr (PREP) {
+            const unsigned base = (unsigned)pend_m0 * (unsigned)rs * (unsigned)sizeof(TO);
 #pragma unroll
             for (int t = 0; t < TMR; ++t) {
                 const bool mok = valid && pend_m0 + t * 16 + (lane & 15) < M;
@@ -404,10 +455,16 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
         for (int t = 0; t < TMR; ++t) {
             const bool mok = valid && pend_m0 + t * 16 + (lane & 15) < M;
 #pragma unroll
-            for (int h = 0; h < NC / EPC16; ++h) {
+            for (int h = 0; h < NU; ++h) {
+                const unsigned base = (unsigned)pend_m0 * s_rs[h] * (unsigned)sizeof(TO);
                 const unsigned off = (mok && !s_nok[h]) ? base + s_lo[t][h] : OOB;
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    u32x4{pend[t][4 * h], pend[t][4 * h + 1], pend[t][4 * h + 2], pend[t][4 * h + 3]}, rc, off, 0, 0);
+                if constexpr (WPU == 4) {
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        u32x4{pend[t][4 * h], pend[t][4 * h + 1], pend[t][4 * h + 2], pend[t][4 * h + 3]}, rc, off, 0, 0);
+                } else {
+                    typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2_{pend[t][2 * h], pend[t][2 * h + 1]}, rc, off, 0, 0);
+                }
             }
         }
     };
@@ -426,8 +483,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
             char* st = stages + (i % NS) * C_::STAGE;
 #pragma unroll
             for (int j = 0; j < C_::A_OPS; ++j) {
-                u32x4* pa = reinterpret_cast<u32x4*>(st + (j * 256 + tid) * 16);
-                *pa = Mma<T>::add(*pa, *reinterpret_cast<const u32x4*>(st + C_::A_BYTES + (j * 256 + tid) * 16));
+                u32x4* pa = reinterpret_cast<u32x4*>(st + (j * NTHR + tid) * 16);
+                *pa = Mma<T>::add(*pa, *reinterpret_cast<const u32x4*>(st + C_::A_SPAN + (j * NTHR + tid) * 16));
             }
         }
         lds_barrier();
@@ -447,7 +504,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
             for (int t = 0; t < TMR; ++t) {
                 const int row = t * 16 + (lane & 15);
                 const int q = c * 4 + (lane >> 4);
-                const int xo = row * C_::ROW + ((q ^ (row & C_::SWM)) << 4);
+                const int xo = row * C_::ROW + (C_::sw(row, q) << 4);
                 const u32x4 xf = *reinterpret_cast<const u32x4*>(st + xo);
 #pragma unroll
                 for (int a = 0; a < NT; ++a) Mma<T>::run(acc[a][t], wf[a][c], xf);
@@ -482,16 +539,28 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
 #pragma unroll
             for (int j = 0; j < NC; ++j)
                 v[t][j] = acc[j >> 2][t][j & 3] * par[cl0 + j] + par[GW + cl0 + j];
-            if (HAS_R) {
+            if constexpr (HAS_R && NC % 8 == 0) {
 #pragma unroll
                 for (int h = 0; h < NC / 8; ++h) {
                     const int q = (cl0 >> 3) + h;
                     const u32x4 u = *reinterpret_cast<const u32x4*>(st + C_::R_OFF + rl * C_::R_ROW +
-                                                                    ((q ^ (rl & C_::R_SWM)) << 4));
+                                                                    (C_::rsw(rl, q) << 4));
                     float r8[8];
                     unpack8(u, r8, std::is_same<TO, f16_t>::value);
 #pragma unroll
                     for (int e = 0; e < 8; ++e) v[t][h * 8 + e] += r8[e];
+                }
+            } else if constexpr (HAS_R) {
+                // 4-column pieces (NT = 3: a lane's 12 columns start at a multiple of 4)
+#pragma unroll
+                for (int h = 0; h < NC / 4; ++h) {
+                    const int col = cl0 + 4 * h, q = col >> 3;
+                    const uint2 u = *reinterpret_cast<const uint2*>(st + C_::R_OFF + rl * C_::R_ROW +
+                                                                    (C_::rsw(rl, q) << 4) + ((col >> 2) & 1) * 8);
+                    float r8[8];
+                    unpack8(u32x4{u.x, u.y, 0u, 0u}, r8, std::is_same<TO, f16_t>::value);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[t][h * 4 + e] += r8[e];
                 }
             }
             if (p.relu)
@@ -508,13 +577,12 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
                 for (int j = 0; j < NC; ++j) s += v[t][j];
                 s += __shfl_xor(s, 16);
                 s += __shfl_xor(s, 32);
-                if ((lane >> 4) == 0) lns[(t * 16 + (lane & 15)) * 4 + wave] = s;
+                if ((lane >> 4) == 0) lns[(t * 16 + (lane & 15)) * NW + wave] = s;
             }
             lds_barrier();
 #pragma unroll
             for (int t = 0; t < TMR; ++t) {
-                const f32x4 w4 = *reinterpret_cast<const f32x4*>(lns + (t * 16 + (lane & 15)) * 4);
-                mean[t] = (w4[0] + w4[1] + w4[2] + w4[3]) / (float)N;
+                mean[t] = wave_sum<NW>(lns + (t * 16 + (lane & 15)) * NW) / (float)N;
                 float q = 0.f;
 #pragma unroll
                 for (int j = 0; j < NC; ++j) {
@@ -523,13 +591,12 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
                 }
                 q += __shfl_xor(q, 16);
                 q += __shfl_xor(q, 32);
-                if ((lane >> 4) == 0) lns[BMR * 4 + (t * 16 + (lane & 15)) * 4 + wave] = q;
+                if ((lane >> 4) == 0) lns[BMR * NW + (t * 16 + (lane & 15)) * NW + wave] = q;
             }
             lds_barrier();
 #pragma unroll
             for (int t = 0; t < TMR; ++t) {
-                const f32x4 w4 = *reinterpret_cast<const f32x4*>(lns + BMR * 4 + (t * 16 + (lane & 15)) * 4);
-                rstd[t] = rsqrtf((w4[0] + w4[1] + w4[2] + w4[3]) / (float)N + p.ln_eps);
+                rstd[t] = rsqrtf(wave_sum<NW>(lns + BMR * NW + (t * 16 + (lane & 15)) * NW) / (float)N + p.ln_eps);
 #pragma unroll
                 for (int j = 0; j < NC; ++j)
                     v[t][j] = (v[t][j] - mean[t]) * rstd[t] * par[2 * GW + cl0 + j] + par[3 * GW + cl0 + j];
@@ -550,9 +617,9 @@ __global__ __launch_bounds__(256, OCC) void gemm_rw_kernel(const GemmArgs p, con
 }
 
 template <typename T, typename TO, int KC, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2 = false, int NT = 4,
-          bool CR = false, bool PREP = false, int OCC = 2, int DIAG = 0>
+          bool CR = false, bool PREP = false, int OCC = 2, int DIAG = 0, int NW = 4>
 void launch_cfg(const GemmArgs& a, hipStream_t stream) {
-    constexpr int GW = 4 * NT * 16;
+    constexpr int GW = NW * NT * 16;
     const int n_mtiles = (a.M + BMR - 1) / BMR;
     const int ng = (a.N + GW - 1) / GW;
     // 2 resident workgroups per CU over all groups: never more than the 512 slots (a second
@@ -562,18 +629,32 @@ void launch_cfg(const GemmArgs& a, hipStream_t stream) {
     const int slots = 256 * OCC;
     int P = slots / ng >= 8 ? slots / ng / 8 * 8 : slots / ng;
     if (P > n_mtiles) P = n_mtiles;
-    dim3 grid(P, ng), block(256);
-    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR, PREP, OCC, DIAG>), grid, block, 0, stream,
-                       a, n_mtiles);
+    dim3 grid(P, ng), block(NW * 64);
+    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR, PREP, OCC, DIAG, NW>), grid, block, 0,
+                       stream, a, n_mtiles);
 }
 
 // deepest DMA ring (<= 4 row tiles) that keeps the workgroup within 80 KiB of LDS (two per CU)
-template <int KC, int BMR, bool HAS_R, bool LN, bool HAS_A2, int NT = 4, bool PREP = false>
+template <int KC, int BMR, bool HAS_R, bool LN, bool HAS_A2, int NT = 4, bool PREP = false, int NW = 4,
+          int BUDGET = 80 * 1024>
 constexpr int ring_depth() {
-    constexpr int base = RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2, PREP>::BYTES -
-                         RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2, PREP>::STAGE;
-    constexpr int stage = RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2, PREP>::STAGE;
-    return (80 * 1024 - base) / stage >= 4 ? 4 : (80 * 1024 - base) / stage;
+    constexpr int base = RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2, PREP, NW>::BYTES -
+                         RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2, PREP, NW>::STAGE;
+    constexpr int stage = RwCfg<KC, NT, BMR, 1, HAS_R, LN, HAS_A2, PREP, NW>::STAGE;
+    return (BUDGET - base) / stage >= 4 ? 4 : (BUDGET - base) / stage;
+}
+
+// K = 288 (d = 288: configs 3-5): 16-row tiles, 12 columns per lane (NT = 3, 108 weight VGPRs;
+// 180-210 in all: two waves per SIMD).  LayerNorm rows (N <= 288) need the whole row in one
+// workgroup: 6 waves x 48 columns, one workgroup per CU with a ring of up to 4 tiles in 160 KiB;
+// the other epilogues take 4-wave 192-column groups, two per CU (a row tile is shared by its
+// groups through the XCD's L2, as at K = 256).
+template <typename T, typename TO, bool HAS_R, bool LN, bool HAS_A2, int NW>
+void launch_288(const GemmArgs& a, hipStream_t stream) {
+    constexpr int OCC = NW == 4 ? 2 : 1;
+    constexpr int NS = ring_depth<9, 16, HAS_R, LN, HAS_A2, 3, false, NW, 160 * 1024 / OCC>();
+    static_assert(NS >= 2, "LDS budget");
+    launch_cfg<T, TO, 9, 16, NS, HAS_R, LN, HAS_A2, 3, false, false, OCC, 0, NW>(a, stream);
 }
 
 template <typename T, typename TO, int KC, bool HAS_R, bool LN, bool HAS_A2, int NT = 4>
@@ -616,6 +697,15 @@ void launch_k(const GemmArgs& a, hipStream_t stream) {
 // 2 column groups, which share each row tile through the XCD's L2)
 template <typename T, typename TO>
 void launch_t(const GemmArgs& a, hipStream_t stream) {
+    if (a.K == 288) {
+        const bool r = a.R != nullptr, ln = a.ln_g != nullptr;
+        if (a.A2 != nullptr) launch_288<T, TO, false, false, true, 4>(a, stream);
+        else if (r && ln) launch_288<T, TO, true, true, false, 6>(a, stream);
+        else if (ln) launch_288<T, TO, false, true, false, 6>(a, stream);
+        else if (r) launch_288<T, TO, true, false, false, 4>(a, stream);
+        else launch_288<T, TO, false, false, false, 4>(a, stream);
+        return;
+    }
     if (a.K == 64) launch_k<T, TO, 2>(a, stream);
     else if (a.K == 128) launch_k<T, TO, 4>(a, stream);
     else if (a.K == 256) launch_k<T, TO, 8>(a, stream);
@@ -632,17 +722,22 @@ thread_local int rw_min_m = 4096;   // smallest M routed to the resident-weight 
 // fits it; false leaves the call to the tiled kernel.
 bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t stream) {
     if (in_dtype != KINET_BF16 && in_dtype != KINET_F16) return false;
-    if (a.M < rw_min_m || (a.K != 64 && a.K != 128 && a.K != 256 && a.K != 512)) return false;
+    if (a.M < rw_min_m || (a.K != 64 && a.K != 128 && a.K != 256 && a.K != 512 && a.K != 288)) return false;
+    if (a.K == 288 && (kinet_gemm_flags & 1048576)) return false;   // flag: K = 288 on the tiled kernels (A/B)
     if (a.K == 512 && (a.N > 256 || a.R != nullptr || a.ln_g != nullptr || a.A2 != nullptr || (kinet_gemm_flags & 256)))
         return false;
     if (a.A2 != nullptr && (a.R != nullptr || a.ln_g != nullptr || !al16(a.A2))) return false;
-    if (a.N % 8 != 0 || (a.ln_g != nullptr && a.N > 256)) return false;
+    if (a.N % 8 != 0 || (a.ln_g != nullptr && a.N > (a.K == 288 ? 288 : 256))) return false;
     const bool o16 = out_dtype == in_dtype || (in_dtype == KINET_BF16 && out_dtype == KINET_F16);
     const bool o32 = out_dtype == KINET_F32;
     if (!o16 && !o32) return false;
     if (o16 ? (a.ldc % 8 != 0) : (a.ldc % 4 != 0)) return false;
     if (!al16(a.C) || (a.R != nullptr && (!o16 || a.ldr % 8 != 0 || !al16(a.R)))) return false;
-    if (a.hm_rows && (a.hm_d % 8 != 0 || a.hm_split)) return false;
+    // head-major stores: 16-byte units need hm_d % 8 == 0; the K = 288 path stores 4-column
+    // units (hm_d % 4 == 0) and takes the split planes (hm_d2 == 4)
+    if (a.hm_rows && (a.K == 288 ? (a.hm_d % 4 != 0 || (a.hm_split && (a.hm_d2 != 4 || a.hm_split % a.hm_d != 0)))
+                                 : (a.hm_d % 8 != 0 || a.hm_split)))
+        return false;
     // output descriptor extent (buffer stores; offsets must stay below 2^31)
     const long long osz = out_dtype == KINET_F32 ? 4 : 2;
     const long long cb = a.hm_rows ? (long long)a.M * a.N * osz

@@ -355,16 +355,16 @@ def test_big_conv_vs_fp32(K, big, B, H, W, Cin, Cout, k, s, p):
 
 # ---- resident-weight streaming kernel (gemm_rw.hip: 16-bit, K in {64, 128, 256, 512}, M >= 4096) ----
 
-def _rw_case(M, N, Kd, mode, seed):
+def _rw_case(M, N, Kd, mode, seed, dtype=torch.bfloat16):
     g = torch.Generator().manual_seed(seed)
-    x = torch.randn(M, Kd, generator=g).bfloat16()
-    x2 = torch.randn(M, Kd, generator=g).bfloat16()
-    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).bfloat16()
+    x = torch.randn(M, Kd, generator=g).to(dtype)
+    x2 = torch.randn(M, Kd, generator=g).to(dtype)
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).to(dtype)
     b = torch.randn(N, generator=g)
-    r = torch.randn(M, N, generator=g).bfloat16()
+    r = torch.randn(M, N, generator=g).to(dtype)
     mask = torch.rand(M, generator=g) < 0.1
     gam, bet = torch.rand(N, generator=g) + 0.5, torch.randn(N, generator=g)
-    xin = (x.float() + x2.float()).bfloat16() if 'add' in mode else x
+    xin = (x.float() + x2.float()).to(dtype) if 'add' in mode else x
     ref = F.linear(xin.float(), w.float(), b)
     kw = {}
     if 'res' in mode:
@@ -455,6 +455,74 @@ def test_rw_conv1x1(K, Cin, Cout, res):
                       residual=r.permute(0, 2, 3, 1).contiguous().cuda() if res else None)
     torch.cuda.synchronize()
     err = (y.permute(0, 3, 1, 2).float().cpu() - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
+
+
+# ---- K = 288 (d = 288, configs 3-5): 16-row tiles, 12 columns per lane; LayerNorm rows on 6-wave
+# 288-column groups, the other epilogues on 4-wave 192-column groups ----
+
+@pytest.mark.parametrize('M,N,mode', [(20011, 288, 'res_ln'), (9000, 288, 'res_ln_mask'), (8197, 280, 'res_ln'),
+                                      (9001, 288, 'ln'), (8200, 384, 'add'), (8200, 384, 'add_f32'),
+                                      (8197, 288, 'plain'), (8197, 1728, 'relu'), (5000, 288, 'res_relu_mask'),
+                                      (4099, 200, 'f32'), (12000, 296, 'res_mask')])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_rw288_vs_fp32(K, M, N, mode, dtype):
+    """The K = 288 projections (value / offsets / output + LayerNorm of a d = 288 layer, the
+    decoder's concatenated value projections) against torch fp32 on the same 16-bit operands:
+    f32 accumulation, one output rounding."""
+    x, w, b, kw, ref = _rw_case(M, N, 288, mode, M + N, dtype)
+    y = K.linear(x.cuda(), w.cuda(), b.cuda(), **kw)
+    torch.cuda.synchronize()
+    assert y.dtype == (torch.float32 if 'f32' in mode else dtype)
+    err = (y.float().cpu() - ref).abs()
+    tol = (1e-4 * ref.abs() + 2e-3) if 'f32' in mode else (1e-2 * ref.abs() + 2e-2)
+    assert (err <= tol).all(), err.max().item()
+
+
+@pytest.mark.parametrize('M,N,mode', [(10001, 288, 'res_ln_mask'), (8200, 384, 'add'), (8197, 1728, 'relu'),
+                                      (9001, 288, 'ln'), (8200, 384, 'add_f32')])
+def test_rw288_matches_tiled_kernel(K, gemm_flags, M, N, mode):
+    """K = 288 on the resident-weight kernel vs the tiled kernels (flag 1048576): the same
+    16-bit products summed in the same K order in f32 -- (nearly) the last bit."""
+    x, w, b, kw, _ = _rw_case(M, N, 288, mode, 9, torch.float16)
+    args = (x.cuda(), w.cuda(), b.cuda())
+    gemm_flags(0)
+    y_rw = K.linear(*args, **kw)
+    gemm_flags(1048576)
+    y_tiled = K.linear(*args, **kw)
+    torch.cuda.synchronize()
+    d = (y_rw.float() - y_tiled.float()).abs()
+    tol = y_tiled.float().abs() * 2.0 ** -9 + 1e-5
+    assert (d <= tol).all(), d.max().item()
+    assert (d == 0).float().mean().item() > 0.9
+
+
+@pytest.mark.parametrize('hd', [36, 48, 'split'])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_rw288_headmajor(K, hd, dtype):
+    """Head-major stores of the K = 288 kernel in 4-column units: the d = 288 value projection
+    (8 heads x 36), the offsets / logits projection layout (8 x 48) and the split planes
+    (32-channel + 4-channel) of the head_dim-36 strip encoder."""
+    B, S, d = 2, 4700, 288
+    Nout = 384 if hd == 48 else 288
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(B, S, d, generator=g).to(dtype)
+    w = (torch.randn(Nout, d, generator=g) / 17).to(dtype)
+    b = torch.randn(Nout, generator=g)
+    mask = torch.rand(B, S, generator=g) < 0.2
+    ref = F.linear(x.float(), w.float(), b).masked_fill(mask[..., None], 0)      # (B, S, Nout)
+    if hd == 'split':
+        ws, bs = K.split_value_weights(w.cuda(), b.cuda(), 8)
+        sv = K.value_proj_headmajor_split(x.cuda(), ws, bs, 8, row_mask=mask.cuda())
+        torch.cuda.synchronize()
+        y = torch.cat([sv.main, sv.tail], -1)                                     # (8, B, S, 36)
+        ref = ref.view(B, S, 8, 36).permute(2, 0, 1, 3)
+    else:
+        y = K.value_proj_headmajor(x.cuda(), w.cuda(), b.cuda(), hd, row_mask=mask.cuda())
+        torch.cuda.synchronize()
+        ref = ref.view(B, S, Nout // hd, hd).permute(2, 0, 1, 3)
+    assert tuple(y.shape) == tuple(ref.shape)
+    err = (y.float().cpu() - ref).abs()
     assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
 
 
