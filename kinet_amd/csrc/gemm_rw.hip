@@ -74,8 +74,8 @@ struct RwCfg {
     // 4-bank groups
     __device__ static constexpr int sw(int r, int c) { return POW2 ? c ^ (r & SWM) : c ^ ((r >> 2) & 3); }
     __device__ static constexpr int rsw(int r, int c) { return R_POW2 ? c ^ (r & R_SWM) : c ^ ((r >> 2) & 3); }
-    static_assert(!PREP || (NT == 3 && NW == 4 && (BMR == 16 || BMR == 32) && !HAS_R && !LN),
-                  "sampling records: 4 waves x 12 columns per lane, 16- or 32-row tiles");
+    static_assert(!PREP || (NT == 3 && (NW == 4 || NW == 8) && (BMR == 16 || BMR == 32) && !HAS_R && !LN),
+                  "sampling records: one head per wave (12 columns per lane), 16- or 32-row tiles");
     static_assert(POW2 || CPR % 4 == 0, "A rows: power-of-two or multiple-of-4 chunks");
     static_assert(!HAS_R || R_POW2 || R_CPR % 4 == 0, "residual rows: power-of-two or multiple-of-4 chunks");
     static_assert(BMR / 16 <= 64, "mask DMA lanes");
@@ -404,8 +404,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
     bool s_nok[NSL];
     if constexpr (PREP) {
         // record (head h, row m) at (h*M + m)*96 bytes: [4 levels x 16 B locations | 4 levels x 8 B weights];
-        // this lane writes level lane >> 4 of head blockIdx.y*4 + wave
-        const unsigned hb = (unsigned)(blockIdx.y * 4 + wave) * (unsigned)M;
+        // this lane writes level lane >> 4 of head blockIdx.y*NW + wave
+        const unsigned hb = (unsigned)(blockIdx.y * NW + wave) * (unsigned)M;
         const unsigned l = (unsigned)(lane >> 4);
 #pragma unroll
         for (int t = 0; t < TMR; ++t) {

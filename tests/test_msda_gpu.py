@@ -781,7 +781,8 @@ def test_encoder_records_path_matches_offlog_path():
 
 
 @pytest.mark.parametrize('masked', [False, True])
-def test_sample_records_occupancy_variants_bit_identical(masked):
+@pytest.mark.parametrize('flag', [8192])
+def test_sample_records_occupancy_variants_bit_identical(masked, flag):
     """The records GEMM at three workgroups per CU (the default: 2-slot ring, <= 168 VGPRs) runs
     the same per-row arithmetic as two per CU with a 4-slot ring (kinet_gemm_set_flags 8192):
     bit-identical records, incl. the ragged last tile."""
@@ -792,7 +793,7 @@ def test_sample_records_occupancy_variants_bit_identical(masked):
     args = (x.cuda(), w.cuda(), bias.cuda(), 8, ref.cuda(), shapes)
     kw = dict(x_add=pos.cuda(), query_attn_mask=qmask.cuda() if qmask is not None else None)
     r0, fb0 = K.msda_sample_records(*args, **kw)
-    old = _native.lib().kinet_gemm_set_flags(8192)
+    old = _native.lib().kinet_gemm_set_flags(flag)
     try:
         r1, fb1 = K.msda_sample_records(*args, **kw)
     finally:

@@ -3,7 +3,8 @@ logits projection GEMM -> f16 head-major offsets + logits -> kinet_msda_encoder_
 the sampling-records pipeline (kinet_msda_sample_records -> kinet_msda_encoder_forward_records).
 Times each kernel alone (HIP events, interleaved repeats) and prints the max output difference.
 
-usage: python tools/rec_ab.py [--batch 16] [--iters 30] [--reps 3]
+usage: python tools/rec_ab.py [--batch 16] [--iters 30] [--reps 3] [--rec-flags 0,8192,2097152]
+(--rec-flags: time the records GEMM alone under each kinet_gemm_set_flags value, interleaved)
 """
 import argparse
 import os
@@ -33,6 +34,7 @@ def main():
     ap.add_argument('--batch', type=int, default=16)
     ap.add_argument('--iters', type=int, default=30)
     ap.add_argument('--reps', type=int, default=3)
+    ap.add_argument('--rec-flags', default='')
     a = ap.parse_args()
     shapes = [(100, 167), (50, 84), (25, 42), (13, 21)]
     B, S = a.batch, sum(h * w for h, w in shapes)
@@ -76,6 +78,17 @@ def main():
             t = [time_call(f, a.iters) * 1e3 for f in (proj_old, samp_old, proj_rec, samp_rec)]
             print(f'rep {r}: offlog GEMM {t[0]:.1f} us + sampler {t[1]:.1f} us = {t[0] + t[1]:.1f} | '
                   f'records GEMM {t[2]:.1f} us + sampler {t[3]:.1f} us = {t[2] + t[3]:.1f}  (B={B})', flush=True)
+        if a.rec_flags:
+            from kinet_amd import _native
+            flags = [int(f) for f in a.rec_flags.split(',')]
+            for r in range(a.reps):
+                t = []
+                for f in flags:
+                    _native.lib().kinet_gemm_set_flags(f)
+                    t.append(time_call(proj_rec, a.iters) * 1e3)
+                _native.lib().kinet_gemm_set_flags(0)
+                print(f'rep {r}: records GEMM ' + ' | '.join(f'flags {f}: {x:.1f} us' for f, x in zip(flags, t)),
+                      flush=True)
         d = (state['o_old'].float() - state['o_rec'].float()).abs()
         print(f'max |old - records| {d.max().item():.4g}  mean {d.mean().item():.3g}  '
               f'max |old| {state["o_old"].float().abs().max().item():.3g}')
