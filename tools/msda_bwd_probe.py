@@ -8,7 +8,10 @@ have random reference points.  Offsets: the reference init (8-direction grid, po
 radius i+1 pixels) + N(0, noise) pixels.  Times the direct-atomic kernel (tune mode -1) and the
 LDS-table kernel at the given table shapes, and checks they agree.
 
-    python tools/msda_bwd_probe.py [--iters 10] [--noise 0.5] [--sweep] [--phases]
+    python tools/msda_bwd_probe.py [--iters 10] [--noise 0.5] [--sweep] [--phases] [--ab FLAGS]
+
+--ab FLAGS: the default kernel vs the one kinet_msda_backward_debug(FLAGS) selects (result-valid
+variants: 16 = DPP row sums in phase 2), interleaved 4 times, with the max difference.
 
 --phases: the on-chip-sum kernel with each timing-only phase knob (kinet_msda_backward_debug:
 1 no value loads in the location / weight gradients, 2 no row atomics, 4 no row-sum phase,
@@ -55,6 +58,7 @@ def main():
     ap.add_argument('--sweep', action='store_true')
     ap.add_argument('--case', default='encoder,decoder')
     ap.add_argument('--phases', action='store_true')
+    ap.add_argument('--ab', type=int, default=0)
     a = ap.parse_args()
     from kinet_amd import _native
     from kinet_amd.MultiScaleDeformableAttention import ms_deform_attn_backward
@@ -75,6 +79,25 @@ def main():
         runs = [(c, 0) for c in cfgs]
         if a.phases:
             runs += [((0, 0, 0, 0, 0), f) for f in (1, 2, 4, 8, 1 | 4, 1 | 8)]
+        if a.ab:
+            for rep in range(4):
+                outs = []
+                for flags in (0, a.ab):
+                    dbg(flags)
+                    out = ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
+                    torch.cuda.synchronize()
+                    outs.append([t.clone() for t in out])
+                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s.record()
+                    for _ in range(a.iters):
+                        ms_deform_attn_backward(v, ss, loc, attw, gout, 64)
+                    e.record()
+                    torch.cuda.synchronize()
+                    print(f'{name:8s} rep {rep} flags {flags}: {s.elapsed_time(e) / a.iters:8.3f} ms', flush=True)
+                dbg(0)
+                err = max(((o - r).abs().max() / r.abs().max().clamp_min(1e-30)).item() for o, r in zip(*outs))
+                print(f'{name:8s} rep {rep} max rel diff {err:.2e}', flush=True)
+            continue
         for cfg, flags in runs:
             tune(*cfg)
             dbg(flags)

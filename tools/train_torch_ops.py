@@ -49,6 +49,16 @@ def main():
     rows = sorted(ev, key=lambda e: -e.self_device_time_total)
     tot = sum(e.self_device_time_total for e in ev)
     print(f'total self device time over 2 steps: {tot / 1e3:.1f} ms')
+    # device kernels only (the op-level rows carry the same time again): kinet vs the rest
+    from torch.autograd import DeviceType
+    kern = [e for e in ev if e.device_type == DeviceType.CUDA]
+    kt = sum(e.self_device_time_total for e in kern)
+    kin = sum(e.self_device_time_total for e in kern if 'kinet' in e.key)
+    print(f'device kernels: {kt / 2e3:.2f} ms per step, kinet {kin / 2e3:.2f} ms, other {(kt - kin) / 2e3:.2f} ms '
+          f'= {(kt - kin) / max(kt, 1):.3f} of kernel time')
+    other = sorted([e for e in kern if 'kinet' not in e.key], key=lambda e: -e.self_device_time_total)
+    for e in other[:15]:
+        print(f'   {e.self_device_time_total / 2e3:8.3f} ms/step  {e.count // 2:5d}x  {e.key[:100]}')
     for e in rows[:a.top]:
         print(f'{e.self_device_time_total / 1e3:9.2f} ms  {e.count:6d}x  {e.key[:60]:60s} {str(e.input_shapes)[:90]}')
     # Python sources of the copy / add / fill launches
