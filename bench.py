@@ -71,6 +71,9 @@ def parse():
     ap.add_argument('--batch', type=int, default=None, help='frames per GPU per step')
     ap.add_argument('--streams', type=int, default=None,
                     help='batches in flight per GPU, each on its own HIP stream (serving-style pipelining)')
+    ap.add_argument('--graph', type=int, default=1,
+                    help='1: each in-flight slot\'s forward captured once in a HIP graph after the warm-up and '
+                         'replayed for the timed steps (bit-identical to eager, tools/graph_probe.py); 0: eager')
     ap.add_argument('--height', type=int, default=None)
     ap.add_argument('--width', type=int, default=None)
     ap.add_argument('--dtype', default=None, choices=['bf16', 'f16', 'f32'])
@@ -497,6 +500,31 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
             # streams read them from step 1 on
             torch.cuda.synchronize()
     torch.cuda.synchronize()
+    graphed = False
+    if getattr(a, 'graph', 0):
+        # one HIP graph per in-flight slot: the whole forward of that slot's batch (the same
+        # kernels, buffers and streams as the eager step), replayed for every timed step
+        try:
+            pool = torch.cuda.graph_pool_handle()
+            graphs, gouts = [], []
+            for k in range(nst):
+                gr = torch.cuda.CUDAGraph()
+                with torch.no_grad(), torch.cuda.graph(gr, pool=pool, stream=strs[k]):
+                    gouts.append(model(batches[k], *extra[k]))
+                graphs.append(gr)
+            torch.cuda.synchronize()
+
+            def step(i=0):   # noqa: F811
+                with torch.cuda.stream(strs[i % nst]):
+                    graphs[i % nst].replay()
+                return gouts[i % nst]
+            for i in range(nst):
+                out = step(i)
+            torch.cuda.synchronize()
+            graphed = True
+        except RuntimeError as ex:   # a capture-unsafe host sync: stay eager (reported in the line)
+            print(f'[bench] {name}: HIP graph capture failed ({str(ex)[:120]}), timing eager', file=sys.stderr)
+            torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -513,6 +541,9 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
         elapsed = t.item()
     assert torch.isfinite(out[0]['pred_boxes']).all()
     del out
+    if graphed:
+        del graphs, gouts
+    run_workload.graphed[name] = graphed
 
     # roofline pass: HIP events around every launch of 3 more steps, one stream (the traced
     # kernel durations must not overlap)
@@ -531,6 +562,9 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return elapsed, fam, msda, split, dec_touched
+
+
+run_workload.graphed = {}
 
 
 def msda_roofline(name, msda, dec_touched):
@@ -631,6 +665,7 @@ def main():
         el5, fam5, msda5, split5, _ = run_workload(a, 'config5', dev, world, rank, w5['batch'], w5['streams'],
                                                    w5['h'], w5['w'], w5['dtype'], a.config5_steps, 2)
         c5 = {'workload': w5['desc'], 'value': w5['batch'] * a.config5_steps * world / el5, 'unit': 'frames/s',
+              'launch': 'HIP graph replay' if run_workload.graphed.get('config5') else 'eager',
               'frames_per_gpu_per_step': w5['batch'], 'in_flight_batches': w5['streams'],
               'frame': [3, w5['h'], w5['w']], 'dtype': w5['dtype'], 'steps': a.config5_steps, 'warmup': 2,
               'ms_per_step': el5 / a.config5_steps * 1e3,
@@ -645,6 +680,7 @@ def main():
         el3, fam3, msda3, split3, _ = run_workload(a, 'config3', dev, world, rank, w3['batch'], w3['streams'],
                                                    w3['h'], w3['w'], w3['dtype'], a.config3_steps, 2)
         c3 = {'workload': w3['desc'], 'value': w3['batch'] * a.config3_steps * world / el3, 'unit': 'frames/s',
+              'launch': 'HIP graph replay' if run_workload.graphed.get('config3') else 'eager',
               'frames_per_gpu_per_step': w3['batch'], 'in_flight_batches': w3['streams'],
               'frame': [3, w3['h'], w3['w']], 'dtype': w3['dtype'], 'steps': a.config3_steps, 'warmup': 2,
               'ms_per_step': el3 / a.config3_steps * 1e3,
@@ -693,6 +729,8 @@ def main():
             'config': {'workload': wl['desc'],
                        'frames_per_gpu_per_step': a.batch, 'in_flight_batches': max(1, a.streams),
                        'frame': [3, a.height, a.width],
+                       'launch': 'HIP graph replay per in-flight slot' if run_workload.graphed.get(a.workload)
+                                 else 'eager',
                        'parallelism': f'replicas x{world}'},
             'roofline': roofline,
             'roofline_mfma': mfma_roof,
