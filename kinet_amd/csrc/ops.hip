@@ -202,19 +202,59 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, 
     }
 }
 
-// 16-byte vector forms (C and C/groups multiples of V = 16/sizeof(T)): a thread owns V
-// consecutive channels (one group), 16-byte loads and stores, 32-bit index math.
-template <typename T>
+// 16-byte vector forms (C a multiple of V = 16/sizeof(T)): a thread owns V consecutive
+// channels, 16-byte loads and stores, 32-bit index math.  C/groups a multiple of V: the V
+// channels are one group (one partial per thread); otherwise (STRADDLE, e.g. d = 288 in 32
+// groups of 9) a vector may span two groups, so the partials are kept per channel and summed per
+// group over (slot, channel) in a fixed order, and the apply looks the group up per element.
+template <typename T, bool STRADDLE = false>
 __global__ __launch_bounds__(256) void gn_stats_vec_kernel(const T* __restrict__ x, float* __restrict__ part, int HW,
                                                            int C, int groups, int pix_per_block) {
     constexpr int V = 16 / (int)sizeof(T);
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    __shared__ float red[2][256];   // per-thread partials, summed per group in a fixed order
+    __shared__ float red[2][STRADDLE ? 256 * V : 256];   // partials, summed per group in a fixed order
     const int n = blockIdx.y;
     const int p0 = blockIdx.x * pix_per_block;
     const int p1 = min(HW, p0 + pix_per_block);
     const int CV = C / V, nslot = 256 / CV;
     const int cv = threadIdx.x % CV, slot = threadIdx.x / CV;
+    float* out = part + ((long)n * gridDim.x + blockIdx.x) * 2 * groups;
+    if constexpr (STRADDLE) {
+        float s[V], q[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) s[j] = q[j] = 0.f;
+        if (slot < nslot) {
+            const T* xb = x + (long)n * HW * C + cv * V;
+            for (int p = p0 + slot; p < p1; p += nslot) {
+                const u4 v = *reinterpret_cast<const u4*>(xb + (long)p * C);
+                const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const float t = to_f32(e[j]);
+                    s[j] += t;
+                    q[j] += t * t;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                red[0][slot * C + cv * V + j] = s[j];
+                red[1][slot * C + cv * V + j] = q[j];
+            }
+        }
+        __syncthreads();
+        const int cpg = C / groups;
+        for (int g = threadIdx.x; g < groups; g += blockDim.x) {
+            float gs = 0.f, gq = 0.f;
+            for (int sl = 0; sl < nslot; ++sl)
+                for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+                    gs += red[0][sl * C + c];
+                    gq += red[1][sl * C + c];
+                }
+            out[2 * g] = gs;
+            out[2 * g + 1] = gq;
+        }
+        return;
+    }
     float s = 0.f, q = 0.f;
     if (slot < nslot) {
         const T* xb = x + (long)n * HW * C + cv * V;
@@ -233,7 +273,6 @@ __global__ __launch_bounds__(256) void gn_stats_vec_kernel(const T* __restrict__
     red[1][threadIdx.x] = q;
     __syncthreads();
     const int vpg = C / groups / V;   // channel vectors per group
-    float* out = part + ((long)n * gridDim.x + blockIdx.x) * 2 * groups;
     for (int g = threadIdx.x; g < groups; g += blockDim.x) {
         float gs = 0.f, gq = 0.f;
         for (int sl = 0; sl < nslot; ++sl)
@@ -246,7 +285,7 @@ __global__ __launch_bounds__(256) void gn_stats_vec_kernel(const T* __restrict__
     }
 }
 
-template <typename T>
+template <typename T, bool STRADDLE = false>
 __global__ __launch_bounds__(256) void gn_apply_vec_kernel(const T* __restrict__ x, const float* __restrict__ stats,
                                                            const float* __restrict__ g, const float* __restrict__ b,
                                                            T* __restrict__ y, int HW, int C, int groups, long y_bs,
@@ -268,6 +307,21 @@ __global__ __launch_bounds__(256) void gn_apply_vec_kernel(const T* __restrict__
     const T* e = reinterpret_cast<const T*>(&v);
     u4 o;
     T* oe = reinterpret_cast<T*>(&o);
+    if constexpr (STRADDLE) {
+        // the vector's second group (if it reaches one): channels from its first channel on
+        const int split = (grp + 1) * cpg - c0;
+        const int grp2 = min(grp + 1, groups - 1);
+        const float mean2 = stats[(long)n * 2 * groups + 2 * grp2] / cnt;
+        const float var2 = fmaxf(stats[(long)n * 2 * groups + 2 * grp2 + 1] / cnt - mean2 * mean2, 0.f);
+        const float rstd2 = rsqrtf(var2 + eps);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const bool hi = j >= split;
+            st(oe + j, (to_f32(e[j]) - (hi ? mean2 : mean)) * (hi ? rstd2 : rstd) * g[c0 + j] + b[c0 + j]);
+        }
+        *reinterpret_cast<u4*>(y + (long)n * y_bs + (long)p * C + c0) = o;
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < V; ++j) st(oe + j, (to_f32(e[j]) - mean) * rstd * g[c0 + j] + b[c0 + j]);
     *reinterpret_cast<u4*>(y + (long)n * y_bs + (long)p * C + c0) = o;
@@ -577,7 +631,8 @@ namespace {
 // pixels per stats block: 128 on the vector path, 64 on the scalar path
 bool gn_vec_ok(const void* x, const void* y, int HW, int C, int groups, int y_batch_stride, int N, int dtype) {
     const int V = dtype == KINET_F32 ? 4 : 8;
-    return dtype != KINET_F64 && C % V == 0 && (C / groups) % V == 0 && C / V <= 256 && y_batch_stride % V == 0 &&
+    // (groups of fewer than V channels would need a third group per vector: scalar path)
+    return dtype != KINET_F64 && C % V == 0 && C / groups >= V && C / V <= 256 && y_batch_stride % V == 0 &&
            (((uintptr_t)x | (uintptr_t)y) & 15) == 0 && (long)HW * (C / V) < (1L << 31) && N <= 65535;
 }
 long gn_workspace(int N, int HW, int groups, int ppb) {
@@ -609,16 +664,24 @@ extern "C" int kinet_groupnorm(const void* x, const float* gamma, const float* b
     if (vec) {
         const int V = dtype == KINET_F32 ? 4 : 8;
         const dim3 g2((unsigned)(((long)HW * (C / V) + 255) / 256), N);
-#define GNV(TT)                                                                                                  \
+        const bool straddle = (C / groups) % V != 0;
+#define GNV(TT, SD)                                                                                              \
     do {                                                                                                         \
-        hipLaunchKernelGGL((gn_stats_vec_kernel<TT>), g1, dim3(256), 0, s, (const TT*)x, part, HW, C, groups, ppb); \
+        hipLaunchKernelGGL((gn_stats_vec_kernel<TT, SD>), g1, dim3(256), 0, s, (const TT*)x, part, HW, C, groups, \
+                           ppb);                                                                                 \
         hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, (const float*)part, stats, nblk, groups); \
-        hipLaunchKernelGGL((gn_apply_vec_kernel<TT>), g2, dim3(256), 0, s, (const TT*)x, stats, gamma, beta,     \
+        hipLaunchKernelGGL((gn_apply_vec_kernel<TT, SD>), g2, dim3(256), 0, s, (const TT*)x, stats, gamma, beta, \
                            (TT*)y, HW, C, groups, (long)y_batch_stride, eps);                                    \
     } while (0)
-        if (dtype == KINET_BF16) GNV(bf16_t);
-        else if (dtype == KINET_F16) GNV(f16_t);
-        else GNV(float);
+        if (straddle) {
+            if (dtype == KINET_BF16) GNV(bf16_t, true);
+            else if (dtype == KINET_F16) GNV(f16_t, true);
+            else GNV(float, true);
+        } else {
+            if (dtype == KINET_BF16) GNV(bf16_t, false);
+            else if (dtype == KINET_F16) GNV(f16_t, false);
+            else GNV(float, false);
+        }
 #undef GNV
         KINET_LAUNCH_CHECK();
         return KINET_OK;
