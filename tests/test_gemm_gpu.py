@@ -189,13 +189,15 @@ def test_mha_core(K, D, Lq):
     assert _rel(y, ref) < 1e-5
 
 
-@pytest.mark.parametrize('Lq,Lk', [(300, 300), (57, 333), (130, 37)])
+@pytest.mark.parametrize('D,Lq,Lk', [(32, 300, 300), (32, 57, 333), (32, 130, 37), (36, 520, 520), (36, 57, 333),
+                                    (36, 130, 37), (36, 500, 640)])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
-def test_mha_core_mfma(K, Lq, Lk, dtype):
-    """head_dim 32, 16-bit: the MFMA kernel (attn.hip) vs fp32 SDPA with a key padding mask,
-    and vs the FMA kernel on the same 16-bit inputs."""
+def test_mha_core_mfma(K, D, Lq, Lk, dtype):
+    """head_dim 32 / 36, 16-bit: the MFMA kernels (attn.hip; 36 = the d = 288 decoder's
+    500 + 20 queries, head dim padded to two K-steps) vs fp32 SDPA with a key padding mask, and
+    vs the FMA kernel on the same 16-bit inputs."""
     from kinet_amd import _native
-    heads, B, D = 8, 3, 32
+    heads, B = 8, 3
     E = heads * D
     g = torch.Generator().manual_seed(Lq + Lk)
     q, k, v = (torch.randn(B, n, E, generator=g).to(dtype) for n in (Lq, Lk, Lk))
