@@ -50,12 +50,12 @@ WORKLOADS = {
                     K=0, desc='config2 cfgs/train_deformable.yaml: R-50 Deformable-DETR inference forward, '
                               'd=256, 4 levels, 6/6 layers, 300 queries, box refine'),
     'config3': dict(cfgs=('train_deformable', 'train_multi_frame', 'train_tracking'), over=dict(dataset='mot'),
-                    h=800, w=1333, batch=8, streams=2, dtype='f16', K=20,
+                    h=800, w=1333, batch=8, streams=3, dtype='f16', K=20,
                     desc='config3 tracking forward (cfgs/train_tracking.yaml on the multi-frame d=288 stack): R-50, '
                          '500 object + 20 track queries (SURVEY 8(d) row 3), separate per-frame encoders (L=4), 8-level decoder, '
                          'prev-frame features resident, 800x1333 frame pairs'),
     'config5': dict(cfgs=('train_deformable', 'train_multi_frame', 'train_tracking', 'train_full_res'),
-                    over=dict(dataset='mot', backbone='resnet101'), h=1080, w=1920, batch=4, streams=2, dtype='f16',
+                    over=dict(dataset='mot', backbone='resnet101'), h=1080, w=1920, batch=4, streams=3, dtype='f16',
                     K=20, desc='config5 cfgs/train_full_res.yaml: R-101 multi-frame tracking forward, d=288, '
                                '500 object + 20 track queries, separate per-frame encoders (L=4), 8-level decoder, '
                                'prev-frame features resident'),
