@@ -386,8 +386,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, p.c_bytes, 0x00020000);
     constexpr int EPC16 = 16 / (int)sizeof(TO);     // elements per 16-byte store
     // store unit: 16 bytes, or 4 columns when a lane's NC columns are not whole 16-byte runs
-    // (NT = 3: 12 columns = 16-bit 8-byte units, never straddling a head of 4k columns)
-    constexpr int SU = NC % EPC16 == 0 ? EPC16 : 4;
+    // (NT = 3: 12 columns = 16-bit 8-byte units, never straddling a head of 4k columns; the
+    // 9-wave K = 288 groups without LayerNorm store 4-column units too: head-major d = 36)
+    constexpr int SU = (NC % EPC16 == 0 && !(KC == 9 && NT == 2 && !LN)) ? EPC16 : 4;
     constexpr int NU = NC / SU;                     // store units per lane-row
     constexpr int WPU = SU * (int)sizeof(TO) / 4;   // packed words per unit
     // stores per lane per row tile (PREP: one 16-byte location store + one 8-byte weight store)
@@ -649,12 +650,11 @@ constexpr int ring_depth() {
 // workgroup: 6 waves x 48 columns, one workgroup per CU with a ring of up to 4 tiles in 160 KiB;
 // the other epilogues take 4-wave 192-column groups, two per CU (a row tile is shared by its
 // groups through the XCD's L2, as at K = 256).
-template <typename T, typename TO, bool HAS_R, bool LN, bool HAS_A2, int NW>
+template <typename T, typename TO, bool HAS_R, bool LN, bool HAS_A2, int NW, int NT = 3, int OCC = NW == 4 ? 2 : 1>
 void launch_288(const GemmArgs& a, hipStream_t stream) {
-    constexpr int OCC = NW == 4 ? 2 : 1;
-    constexpr int NS = ring_depth<9, 16, HAS_R, LN, HAS_A2, 3, false, NW, 160 * 1024 / OCC>();
+    constexpr int NS = ring_depth<9, 16, HAS_R, LN, HAS_A2, NT, false, NW, 160 * 1024 / OCC>();
     static_assert(NS >= 2, "LDS budget");
-    launch_cfg<T, TO, 9, 16, NS, HAS_R, LN, HAS_A2, 3, false, false, OCC, 0, NW>(a, stream);
+    launch_cfg<T, TO, 9, 16, NS, HAS_R, LN, HAS_A2, NT, false, false, OCC, 0, NW>(a, stream);
 }
 
 template <typename T, typename TO, int KC, bool HAS_R, bool LN, bool HAS_A2, int NT = 4>
@@ -699,11 +699,27 @@ template <typename T, typename TO>
 void launch_t(const GemmArgs& a, hipStream_t stream) {
     if (a.K == 288) {
         const bool r = a.R != nullptr, ln = a.ln_g != nullptr;
-        if (a.A2 != nullptr) launch_288<T, TO, false, false, true, 4>(a, stream);
-        else if (r && ln) launch_288<T, TO, true, true, false, 6>(a, stream);
-        else if (ln) launch_288<T, TO, false, true, false, 6>(a, stream);
-        else if (r) launch_288<T, TO, true, false, false, 4>(a, stream);
-        else launch_288<T, TO, false, false, false, 4>(a, stream);
+        if (a.A2 != nullptr) {
+            launch_288<T, TO, false, false, true, 4>(a, stream);
+            return;
+        }
+        // LayerNorm rows: 9 waves x 32 columns (one 288-column group; flag 4194304: the 6-wave x
+        // 48-column groups, A/B and tests); N <= 288 without LayerNorm: 9-wave groups under flag
+        // 2097152 (A/B), else 4-wave 192-column groups
+        const bool w9 = a.N <= 288 && (kinet_gemm_flags & 2097152);
+        if (r && ln) {
+            if (kinet_gemm_flags & 4194304) launch_288<T, TO, true, true, false, 6>(a, stream);
+            else launch_288<T, TO, true, true, false, 9, 2>(a, stream);
+        } else if (ln) {
+            if (kinet_gemm_flags & 4194304) launch_288<T, TO, false, true, false, 6>(a, stream);
+            else launch_288<T, TO, false, true, false, 9, 2>(a, stream);
+        } else if (r) {
+            if (w9) launch_288<T, TO, true, false, false, 9, 2>(a, stream);
+            else launch_288<T, TO, true, false, false, 4>(a, stream);
+        } else {
+            if (w9) launch_288<T, TO, false, false, false, 9, 2>(a, stream);
+            else launch_288<T, TO, false, false, false, 4>(a, stream);
+        }
         return;
     }
     if (a.K == 64) launch_k<T, TO, 2>(a, stream);

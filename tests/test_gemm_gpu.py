@@ -503,6 +503,60 @@ def test_rw288_matches_tiled_kernel(K, gemm_flags, M, N, mode):
     assert (d == 0).float().mean().item() > 0.9
 
 
+@pytest.mark.parametrize('M,N,mode', [(10001, 288, 'res_ln_mask'), (20011, 288, 'res_ln'), (8197, 280, 'res_ln'),
+                                      (9001, 288, 'ln')])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_rw288_ln_wave_variants(K, gemm_flags, M, N, mode, dtype):
+    """The LayerNorm rows of the K = 288 kernel on 9 waves x 32 columns (the default) vs 6 waves
+    x 48 columns (flag 4194304): the same products in the same K order per column; only the row
+    statistics' partial sums are grouped differently (f32) -- within one output rounding, mostly
+    equal."""
+    x, w, b, kw, ref = _rw_case(M, N, 288, mode, 21, dtype)
+    args = (x.cuda(), w.cuda(), b.cuda())
+    gemm_flags(0)
+    y9 = K.linear(*args, **kw)
+    gemm_flags(4194304)
+    y6 = K.linear(*args, **kw)
+    torch.cuda.synchronize()
+    d = (y9.float() - y6.float()).abs()
+    tol = y6.float().abs() * (2.0 ** -7 if dtype == torch.bfloat16 else 2.0 ** -10) + 1e-5
+    assert (d <= tol).all(), d.max().item()
+    assert (d == 0).float().mean().item() > 0.9
+    err = (y9.float().cpu() - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
+
+
+@pytest.mark.parametrize('case', ['plain', 'res_mask', 'f32', 'hm36', 'split'])
+def test_rw288_nine_wave_groups_bit_identical(K, gemm_flags, case):
+    """N <= 288 without LayerNorm on one 9-wave x 32-column group (flag 2097152) vs the 4-wave x
+    48-column groups: every output element is the same K-ordered MFMA chain -- bit for bit,
+    row-major, head-major (d = 36) and split-plane stores alike."""
+    dtype = torch.float16
+    if case in ('hm36', 'split'):
+        g = torch.Generator().manual_seed(31)
+        x = torch.randn(2, 4700, 288, generator=g).to(dtype).cuda()
+        w = (torch.randn(288, 288, generator=g) / 17).to(dtype).cuda()
+        b = torch.randn(288, generator=g).cuda()
+        mask = (torch.rand(2, 4700, generator=g) < 0.2).cuda()
+        if case == 'split':
+            ws, bs = K.split_value_weights(w, b, 8)
+            def run():
+                sv = K.value_proj_headmajor_split(x, ws, bs, 8, row_mask=mask)
+                return torch.cat([sv.main.reshape(-1), sv.tail.reshape(-1)])
+        else:
+            run = lambda: K.value_proj_headmajor(x, w, b, 36, row_mask=mask)
+    else:
+        M, N = {'plain': (8197, 288), 'res_mask': (12000, 280), 'f32': (4099, 200)}[case]
+        x, w, b, kw, _ = _rw_case(M, N, 288, case, 33, dtype)
+        run = lambda: K.linear(x.cuda(), w.cuda(), b.cuda(), **kw)
+    gemm_flags(0)
+    y4 = run().clone()
+    gemm_flags(2097152)
+    y9 = run().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(y4, y9), (y4.float() - y9.float()).abs().max().item()
+
+
 @pytest.mark.parametrize('hd', [36, 48, 'split'])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
 def test_rw288_headmajor(K, hd, dtype):
