@@ -10,7 +10,8 @@ import os
 
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libkinet_amd.so')
+# KINET_AMD_LIB: an alternative build of the same sources (A/B tooling only)
+_LIB_PATH = os.environ.get('KINET_AMD_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libkinet_amd.so')
 
 P = ctypes.c_void_p
 I = ctypes.c_int

@@ -57,7 +57,10 @@ constexpr int EWT = 12;   // TAIL: waves per workgroup (3 per SIMD: the tail's r
 constexpr int EL = 4, EP = 4;      // levels, points (the configs' values; host-checked)
 constexpr int EREC = EL * EP * 3;  // head-major offsets/logits per query and head (48)
 constexpr int EHALO = 4;           // rows staged beyond a strip's query rows on each side
-constexpr uint32_t TAF = 0x80000000u;   // record flag: an LDS level's sample gathered from HBM
+constexpr uint32_t TAF = 0x80000000u;
+#ifndef KINET_ENC_DYN
+#define KINET_ENC_DYN 1
+#endif   // record flag: an LDS level's sample gathered from HBM
 
 // one level's constants as phase 1 reads them: 48 contiguous bytes = three ds_read_b128 from one
 // address per lane (its level), instead of eleven ds_read_b32 of the per-field arrays
@@ -74,6 +77,7 @@ struct EncLevels {
     int rn[EL];   // LDS level: staged rows
     int lb[EL];   // LDS level: map pixel of (row r, col c) = lb + r*W + c
     LevelRec rec[EL];
+    int next_tile;   // the strip's next unclaimed tile (waves claim tiles as they finish one)
 };
 
 // launch plan (host): levels [0, fl) are gathered from the head map, levels [fl, EL) staged
@@ -525,6 +529,7 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
         lv.rec[lane] = rc;
     }
 
+    if (KINET_ENC_DYN && wave == 0 && lane == 0) lv.next_tile = t0 + NW;
     // the first tile's phase-1 inputs ahead of the DMA (so waiting for them does not wait for it)
     if (has) load_tile<REFD, QM, REC>(in, ro, rr, rq, b, Lq, q0 + qi, l1);
     // ---- LDS-DMA fill of the staged regions, in flight with the first tile's setup and gathers (pieces
@@ -581,7 +586,14 @@ __device__ __forceinline__ void enc_tiles(const EncArgs& a, EncLevels& lv, u32x4
     const int stride = NW;
 #pragma unroll 1
     for (;;) {
-        const int tn = t + stride;
+        int tn = t + stride;
+        if constexpr (KINET_ENC_DYN) {
+            // dynamic claim: a wave that finishes early takes the next tile, so the strip ends
+            // when the tiles run out rather than with the slowest wave's fixed share
+            int c = 0;
+            if (lane_id_here() == 0) c = atomicAdd(&lv.next_tile, 1);
+            tn = __builtin_amdgcn_readfirstlane(c);
+        }
         const bool more = tn < t1;
         const int qn0 = more ? tile_q0(tn) : 0;
         // the next tile's phase-1 inputs, behind this tile's gathers
