@@ -19,6 +19,8 @@ rm -rf gpurun_out/prof_$tag
 run 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python bench.py --steps "$steps" --warmup 3 --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1
 cp gpurun_out/prof_$tag/run_kernel_stats.csv gpurun_out/${tag}_kernel_stats.csv
 python tools/pmc_summary.py gpurun_out/${tag}_trace_summary.json gpurun_out/prof_$tag
+# all vs isolated (single-stream) dispatches: the cross-check of the bench line's HIP-event roofline
+python tools/trace_isolated.py gpurun_out/prof_$tag gpurun_out/${tag}_trace_isolated.json > gpurun_out/${tag}_trace_isolated.txt 2>&1
 rm -rf gpurun_out/prof_$tag
 tf=gpurun_out/pmc_traffic.json
 rm -f $tf
