@@ -544,27 +544,77 @@ __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(const T* __restrict
     }
 }
 
+// pass 1 for C % 4 == 0: a workgroup covers its rows with whole 4-channel vectors per thread
+// (256 / (C/4) rows at a time, e.g. 3 rows of 72 float4 at C = 288), so every lane streams
+// contiguous 16-byte pieces and the grid has enough workgroups to fill the chip; the row groups'
+// sums are added in LDS in a fixed order (deterministic)
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_partial_vec_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                                 float* __restrict__ part, int HW, int C, int rb) {
+    __shared__ float red[4 * 1024];   // [row group][4 sums][C], rows_per_it * C <= 1024
+    const int n = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
+    const int p0 = blk * rb, p1 = min(HW, p0 + rb);
+    const int C4 = C >> 2, rpi = 256 / C4;
+    const int tr = threadIdx.x / C4, tc = threadIdx.x - tr * C4;
+    float a[4][4] = {};
+    if (tr < rpi) {
+        for (int p = p0 + tr; p < p1; p += rpi) {
+            const long o = ((long)n * HW + p) * C + tc * 4;
+            float xv[4], dv[4];
+            if constexpr (std::is_same<T, float>::value) {
+                const float4 x4 = *reinterpret_cast<const float4*>(x + o), d4 = *reinterpret_cast<const float4*>(dy + o);
+                xv[0] = x4.x; xv[1] = x4.y; xv[2] = x4.z; xv[3] = x4.w;
+                dv[0] = d4.x; dv[1] = d4.y; dv[2] = d4.z; dv[3] = d4.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { xv[j] = ld(x + o + j); dv[j] = ld(dy + o + j); }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                a[0][j] += dv[j];
+                a[1][j] += dv[j] * xv[j];
+                a[2][j] += xv[j];
+                a[3][j] += xv[j] * xv[j];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) red[(tr * 4 + k) * C + tc * 4 + j] = a[k][j];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4 * C; i += 256) {
+        float v = 0.f;
+        for (int r = 0; r < rpi; ++r) v += red[r * 4 * C + i];   // i = k*C + c
+        part[((long)n * nblk + blk) * 4 * C + i] = v;
+    }
+}
+
 // pass 2 (one workgroup per image): per-channel sums over the blocks, then per group the
 // statistics and the two backward scalars; writes stats[n][g] = (mean, rstd, a/cnt, bsum/cnt)
 // and per-image channel sums for dgamma / dbeta
-__global__ __launch_bounds__(256) void gn_bwd_stats_kernel(const float* __restrict__ part, const float* __restrict__ gamma,
-                                                           float* __restrict__ stats, float* __restrict__ chan,
-                                                           int HW, int C, int G, int nblk, float eps) {
+__global__ __launch_bounds__(1024) void gn_bwd_stats_kernel(const float* __restrict__ part, const float* __restrict__ gamma,
+                                                            float* __restrict__ stats, float* __restrict__ chan,
+                                                            int HW, int C, int G, int nblk, float eps) {
     extern __shared__ float sm[];   // [4][C]
     const int n = blockIdx.x;
-    for (int c = threadIdx.x; c < C; c += 256) {
-        float s[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int b = 0; b < nblk; ++b) {
-            const float* q = part + (((long)n * nblk + b) * 4) * C + c;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) s[k] += q[k * C];
+    // one (sum, channel) per thread, the blocks summed in order (4 independent loads in flight)
+    for (int i = threadIdx.x; i < 4 * C; i += blockDim.x) {
+        const float* q = part + (long)n * nblk * 4 * C + i;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int b = 0;
+        for (; b + 3 < nblk; b += 4) {
+            s0 += q[(long)b * 4 * C];
+            s1 += q[(long)(b + 1) * 4 * C];
+            s2 += q[(long)(b + 2) * 4 * C];
+            s3 += q[(long)(b + 3) * 4 * C];
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) sm[k * C + c] = s[k];
+        for (; b < nblk; ++b) s0 += q[(long)b * 4 * C];
+        sm[i] = (s0 + s1) + (s2 + s3);
     }
     __syncthreads();
     const int cg = C / G;
-    for (int g = threadIdx.x; g < G; g += 256) {
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
         float sx = 0.f, sxx = 0.f, a = 0.f, bs = 0.f;
         for (int c = g * cg; c < (g + 1) * cg; ++c) {
             sx += sm[2 * C + c];
@@ -585,7 +635,7 @@ __global__ __launch_bounds__(256) void gn_bwd_stats_kernel(const float* __restri
         st4[3] = bx / cnt;
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += 256) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
         const float* st4 = stats + ((long)n * G + c / cg) * 4;
         // dgamma_n[c] = sum dy*xhat = rstd*(sum dy*x - mean*sum dy); dbeta_n[c] = sum dy
         chan[((long)n * 2) * C + c] = st4[1] * (sm[C + c] - st4[0] * sm[c]);
@@ -604,6 +654,40 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__
         const float* st4 = stats + (n * G + c / cg) * 4;
         const float xh = (ld(x + i) - st4[0]) * st4[1];
         st(dx + i, st4[1] * (ld(dy + i) * gamma[c] - st4[2] - xh * st4[3]));
+    }
+}
+
+// the same for C % 4 == 0 and fewer than 2^31 elements: 4 channels per thread, 32-bit index math
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_apply_vec_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                               const float* __restrict__ gamma, const float* __restrict__ stats,
+                                                               T* __restrict__ dx, int HW, int C, int G, int total4) {
+    const int cg = C / G, img = HW * C;
+    for (int i4 = blockIdx.x * 256 + threadIdx.x; i4 < total4; i4 += gridDim.x * 256) {
+        const int i = i4 * 4;
+        const int n = i / img;
+        const int c0 = (i - n * img) % C;   // C % 4 == 0: the 4 channels lie in one row
+        float xv[4], dv[4], o[4];
+        if constexpr (std::is_same<T, float>::value) {
+            const float4 x4 = *reinterpret_cast<const float4*>(x + i), d4 = *reinterpret_cast<const float4*>(dy + i);
+            xv[0] = x4.x; xv[1] = x4.y; xv[2] = x4.z; xv[3] = x4.w;
+            dv[0] = d4.x; dv[1] = d4.y; dv[2] = d4.z; dv[3] = d4.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { xv[j] = ld(x + i + j); dv[j] = ld(dy + i + j); }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 st4 = *reinterpret_cast<const float4*>(stats + ((long)n * G + (c0 + j) / cg) * 4);
+            const float xh = (xv[j] - st4.x) * st4.y;
+            o[j] = st4.y * (dv[j] * gamma[c0 + j] - st4.z - xh * st4.w);
+        }
+        if constexpr (std::is_same<T, float>::value) {
+            *reinterpret_cast<float4*>(dx + i) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) st(dx + i + j, o[j]);
+        }
     }
 }
 
@@ -1057,7 +1141,9 @@ extern "C" int kinet_layernorm_backward(const void* dy, const void* x, const flo
     return KINET_OK;
 }
 
-static int gn_blocks(int HW) { return std::max(1, std::min(64, HW / 256)); }
+// 128-row blocks (up to 512 per image): at the config-4 input projections (2 x 16700 x 288) 260
+// workgroups instead of 128 one-channel-per-thread loops over 261 rows
+static int gn_blocks(int HW) { return std::max(1, std::min(512, HW / 128)); }
 
 extern "C" int64_t kinet_groupnorm_backward_workspace(int N, int HW, int C, int groups) {
     const long long nb = gn_blocks(HW);
@@ -1077,14 +1163,24 @@ extern "C" int kinet_groupnorm_backward(const void* dy, const void* x, const flo
     float* stats = part + (long)N * nb * 4 * C;
     float* chan = stats + (long)N * groups * 4;
     const long total = (long)N * HW * C;
+    const bool vec = C % 4 == 0 && C <= 1024 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)dy % 16) == 0;
 #define GN_BWD(T)                                                                                                  \
-    hipLaunchKernelGGL(gn_bwd_partial_kernel<T>, dim3(nb, N), dim3(256), 0, s, (const T*)dy, (const T*)x, part, HW, C, rb); \
+    if (vec)                                                                                                       \
+        hipLaunchKernelGGL(gn_bwd_partial_vec_kernel<T>, dim3(nb, N), dim3(256), 0, s, (const T*)dy, (const T*)x, part, \
+                           HW, C, rb);                                                                             \
+    else                                                                                                           \
+        hipLaunchKernelGGL(gn_bwd_partial_kernel<T>, dim3(nb, N), dim3(256), 0, s, (const T*)dy, (const T*)x, part, HW, \
+                           C, rb);                                                                                 \
     KINET_LAUNCH_CHECK();                                                                                          \
-    hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(N), dim3(256), 4 * (size_t)C * sizeof(float), s, part, gamma, stats,  \
+    hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(N), dim3(1024), 4 * (size_t)C * sizeof(float), s, part, gamma, stats, \
                        chan, HW, C, groups, nb, eps);                                                              \
     KINET_LAUNCH_CHECK();                                                                                          \
-    hipLaunchKernelGGL(gn_bwd_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, (const T*)dy, (const T*)x,  \
-                       gamma, stats, (T*)dx, HW, C, groups, total);                                                \
+    if (vec && total < (1L << 31) && ((uintptr_t)dx % 16) == 0)                                                 \
+        hipLaunchKernelGGL(gn_bwd_apply_vec_kernel<T>, dim3(grid_for(total / 4)), dim3(256), 0, s, (const T*)dy,    \
+                           (const T*)x, gamma, stats, (T*)dx, HW, C, groups, (int)(total / 4));                    \
+    else                                                                                                           \
+        hipLaunchKernelGGL(gn_bwd_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, (const T*)dy, (const T*)x, \
+                           gamma, stats, (T*)dx, HW, C, groups, total);                                            \
     KINET_LAUNCH_CHECK();
     if (dtype == KINET_F32) { GN_BWD(float) }
     else if (dtype == KINET_BF16) { GN_BWD(bf16_t) }
