@@ -84,7 +84,23 @@ __global__ __launch_bounds__(256) void drop_add_ln_bwd_kernel(const float* __res
 #pragma unroll
     for (int v = 0; v < MAXV; ++v) g_acc[v] = b_acc[v] = 0.f;
     const int r_begin = (blockIdx.x * 4 + wave) * rpw;
-    for (int row = r_begin; row < min(rows, r_begin + rpw); ++row) {
+    const int r_end = min(rows, r_begin + rpw);
+    // the next row's x / r / dy are loaded while this row is reduced (one row of loads in flight
+    // behind the arithmetic instead of a load -> reduce -> store chain per row)
+    float nx[MAXV], nr[MAXV], nd[MAXV];
+    auto load_row = [&](int row) {
+        const long base = (long)row * d;
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) {
+            const int c = v * 64 + lane;
+            const bool ok = c < d && row < r_end;
+            nx[v] = ok ? x[base + c] : 0.f;
+            nr[v] = ok ? r[base + c] : 0.f;
+            nd[v] = ok ? dy[base + c] : 0.f;
+        }
+    };
+    load_row(r_begin);
+    for (int row = r_begin; row < r_end; ++row) {
         const long base = (long)row * d;
         float zv[MAXV], dv[MAXV];
         bool kp[MAXV];
@@ -96,11 +112,12 @@ __global__ __launch_bounds__(256) void drop_add_ln_bwd_kernel(const float* __res
             zv[v] = dv[v] = 0.f;
             if (c < d) {
                 kp[v] = dropout_keep(seed, (uint64_t)(base + c), thresh);
-                zv[v] = x[base + c] + (kp[v] ? r[base + c] * keep_scale : 0.f);
-                dv[v] = dy[base + c];
+                zv[v] = nx[v] + (kp[v] ? nr[v] * keep_scale : 0.f);
+                dv[v] = nd[v];
             }
             s += zv[v];
         }
+        load_row(row + 1);
         const float mean = wsum(s) / (float)d;
         float q = 0.f;
 #pragma unroll
@@ -569,7 +586,7 @@ extern "C" int kinet_dropout_add_layernorm(const float* x, const float* r, const
 }
 
 namespace {
-constexpr int kLnRowsPerWave = 8;   // ~22 waves per CU at the encoder rows
+constexpr int kLnRowsPerWave = 8;   // ~22 waves per CU at the encoder rows (4: no faster)
 }
 
 extern "C" int64_t kinet_dropout_add_layernorm_backward_workspace(int rows, int d) {

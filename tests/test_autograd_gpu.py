@@ -281,7 +281,7 @@ def _leaf(t):
     return t.detach().clone().requires_grad_()
 
 
-@pytest.mark.parametrize('rows,d,p', [(3001, 288, 0.1), (517, 256, 0.5), (64, 256, 0.0), (7, 90, 0.3)])
+@pytest.mark.parametrize('rows,d,p', [(3001, 288, 0.1), (517, 256, 0.5), (64, 256, 0.0), (7, 90, 0.3), (22223, 288, 0.1)])
 def test_dropout_add_layernorm_fixed_mask(rows, d, p):
     """LayerNorm(x + dropout(r)) (deformable_transformer.py:100,108,186,196,199) and its
     gradients equal torch fp32 autograd of F.layer_norm(x + r * Z) with the SAME keep mask Z
