@@ -485,6 +485,15 @@ int launch(const GemmArgs& a, hipStream_t stream) {
         // 3x3 convs (K >= 9*128) with >= ~2 rounds of 128x128 tiles over the 512 resident
         // slots: 3-6 % faster than 64x128 at batch 16 (tools/sweep_conv.py 16), neutral at 8
         if (CONV && a.K >= 1152 && a.N >= 128 && t128 >= 1000) bm = bn = 128;
+        // KINET_F32_X3 with N just past a multiple of 128 (d = 288 of the config-4 training
+        // GEMMs): 128 x 64 tiles waste 10 % of the columns instead of 25 % -- x3 (44446, 288,
+        // 1024) 157 -> 132 us, (44446, 288, 288) 60 -> 51 us (profiles/r05x_x3_tiles.log);
+        // flag 33554432 keeps the default (A/B)
+        if (std::is_same<T, f32x3_t>::value && a.N > 64 && a.N % 128 != 0 && a.N % 128 <= 64 &&
+            !(kinet_gemm_flags & 33554432)) {
+            bm = 128;
+            bn = 64;
+        }
     }
     // 8-wave LDS-DMA tiles (one workgroup per CU: 256 slots per round): chosen for long-K
     // problems whose rounds of tiles are well filled (a square 4096^3 bf16 GEMM: 1115 TF/s

@@ -744,7 +744,8 @@ def _x3_bound(a64, b64):
     return 4e-5 * (a64.abs() @ b64.abs()) + 1e-6
 
 
-@pytest.mark.parametrize('M,N,Kd', [(37, 91, 256), (1000, 1024, 256), (513, 256, 1024), (4200, 384, 2048)])
+@pytest.mark.parametrize('M,N,Kd', [(37, 91, 256), (1000, 1024, 256), (513, 256, 1024), (4200, 384, 2048),
+                                    (9001, 288, 1024), (9001, 288, 288), (5000, 200, 64)])
 def test_linear_f32_x3_vs_f64(K, x3_precision, M, N, Kd):
     g = torch.Generator().manual_seed(M + N + Kd)
     x = torch.randn(M, Kd, generator=g, dtype=torch.float64)

@@ -42,13 +42,17 @@ def main():
         b = torch.randn(Kd, N, device=dev)
         cases.append((f'gemm_tn K={Kd} M={M} N={N}', lambda a=a, b=b: K.gemm_tn(a, b), 2.0 * M * N * Kd))
     flags = int(os.environ.get('X3_FLAGS', '0'))
+    tile = [int(v) for v in os.environ.get('X3_TILE', '0,0').split(',')]   # kinet_gemm_force_tile for the x3 runs
     from kinet_amd import _native as N
     for name, fn, flops in cases:
         r = {}
         for prec in ('highest', 'high'):
             torch.set_float32_matmul_precision(prec)
             N.lib().kinet_gemm_set_flags(flags)
+            if prec == 'high':
+                N.lib().kinet_gemm_force_tile(*tile)
             r[prec] = timeit(fn)
+            N.lib().kinet_gemm_force_tile(0, 0)
             N.lib().kinet_gemm_set_flags(0)
         torch.set_float32_matmul_precision('highest')
         print(f'{name:34s} exact {r["highest"]*1e3:8.1f} us ({flops/r["highest"]/1e9:6.1f} TF/s)   '
