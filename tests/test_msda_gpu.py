@@ -99,12 +99,14 @@ def test_large_encoder_shape_vs_oracle(MSDA):
 
 @pytest.mark.parametrize('tune,extra', [((0, 0, 0, 0, 0), 0), ((1, 0, 0, 0, 0), 57), ((1, 6, 32, 256, 0), 57),
                                         ((1, 6, 64, 512, 16), 57), ((1, 10, 512, 512, 64), 0),
-                                        ((2, 0, 0, 0, 0), 0), ((0, 0, 0, 0, 0), 57), ((-1, 0, 0, 0, 0), 0)])
+                                        ((2, 0, 0, 0, 0), 0), ((0, 0, 0, 0, 0), 57), ((-1, 0, 0, 0, 0), 0),
+                                        ((4, 0, 0, 0, 0), 0), ((4, 6, 64, 512, 16), 57), ((4, 10, 512, 512, 64), 0)])
 @pytest.mark.parametrize('D', [32, 36])
 def test_backward_list_kernel_vs_oracle(MSDA, tune, extra, D):
     """Encoder-call backward: grad_value rows summed on chip per pass of queries
     (msda_bwd_list_kernel; automatic when Lq == S -- queries walked in 8-pixel-wide blocks of
-    each level -- forced by tune mode 1, index order by mode 2).  Encoder-like
+    each level -- forced by tune mode 1, index order by mode 2, counting-sorted corner lists by
+    mode 4).  Encoder-like
     queries (raster-ordered pixel centres + grid offsets, heavy row reuse) plus `extra` random
     ones; hash sizes from automatic down to 64 rows (most corners overflow to the direct
     global add), passes of 16-64 queries, and the one-atomic-per-corner kernel (mode -1 and

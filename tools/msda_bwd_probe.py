@@ -67,7 +67,7 @@ def main():
     lv = [(100, 167), (50, 84), (25, 42), (13, 21)]
     cases = {'encoder': (2, lv, 22223, True), 'decoder': (2, lv + lv, 520, False)}
     # (mode, log2 hash rows, queries per block, threads, queries per pass)
-    cfgs = [(-1, 0, 0, 0, 0), (0, 0, 0, 0, 0), (2, 0, 0, 0, 0), (3, 0, 0, 0, 0)]
+    cfgs = [(-1, 0, 0, 0, 0), (0, 0, 0, 0, 0), (2, 0, 0, 0, 0), (3, 0, 0, 0, 0), (4, 0, 0, 0, 0)]
     if a.sweep:
         cfgs += [(0, l2, 0, th, qp) for l2 in (9, 10, 11) for th in (256, 512) for qp in (16, 32, 64)
                  if qp >= th // 32]
