@@ -16,13 +16,17 @@ from kinet_amd import kernels as K  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=20)
+    ap.add_argument('--shapes', default='', help='B,H,W,Cin,Cout,k,s;... (default: the batch-16 3x3 convs)')
     a = ap.parse_args()
     L = _native.lib()
     shapes = [(16, 200, 334, 64, 64, 3, 1), (16, 100, 167, 128, 128, 3, 1), (16, 50, 84, 256, 256, 3, 1),
               (16, 25, 42, 512, 512, 3, 1)]
+    if a.shapes:
+        shapes = [tuple(int(v) for v in t.split(',')) for t in a.shapes.split(';')]
     variants = [('heuristic', 0, (0, 0)), ('dma4', 16, (0, 0)), ('t128x64', 0, (128, 64)), ('t64x128', 0, (64, 128)),
                 ('t128x128', 0, (128, 128)), ('t64x64', 0, (64, 64)), ('t256x128', 0, (256, 128)),
-                ('dma4_128x64', 16, (128, 64)), ('dma4_128x128', 16, (128, 128))]
+                ('dma4_128x64', 16, (128, 64)), ('dma4_128x128', 16, (128, 128)), ('t256x256', 0, (256, 256)),
+                ('t128x256', 0, (128, 256)), ('tiled_only', 4, (0, 0))]
     for B, H, W, Cin, Cout, k, s in shapes:
         g = torch.Generator(device='cuda').manual_seed(0)
         x = torch.randn(B, H, W, Cin, device='cuda', dtype=torch.bfloat16, generator=g)
