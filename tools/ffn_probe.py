@@ -12,12 +12,17 @@ from kinet_amd import kernels as K  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument('--rows', type=int, default=8 * 22223)
 ap.add_argument('--iters', type=int, default=5)
+ap.add_argument('--d', type=int, default=256)
+ap.add_argument('--knobs', default='0,2,8', help='kinet_ffn_set_debug values (D = 288: 0 = wave pairs, 32 = 4 waves)')
+ap.add_argument('--dtype', default='bf16', choices=['bf16', 'f16'])
 a = ap.parse_args()
-lin1, lin2, norm = torch.nn.Linear(256, 1024).cuda(), torch.nn.Linear(1024, 256).cuda(), torch.nn.LayerNorm(256).cuda()
-x = torch.randn(a.rows, 256, device='cuda', dtype=torch.bfloat16)
+D = a.d
+dt = torch.bfloat16 if a.dtype == 'bf16' else torch.float16
+lin1, lin2, norm = torch.nn.Linear(D, 1024).cuda(), torch.nn.Linear(1024, D).cuda(), torch.nn.LayerNorm(D).cuda()
+x = torch.randn(a.rows, D, device='cuda', dtype=dt)
 from kinet_amd import _native as N  # noqa: E402
 ref = None
-for knob in (0, 2, 8):
+for knob in [int(k) for k in a.knobs.split(',')]:
     N.lib().kinet_ffn_set_debug(knob)
     for _ in range(2):
         y = K.ffn_fused(x, lin1, lin2, norm)
@@ -28,7 +33,7 @@ for knob in (0, 2, 8):
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) * 1e3 / a.iters
-    tf = 4.0 * a.rows * 256 * 1024 / (us * 1e-6) / 1e12
+    tf = 4.0 * a.rows * D * 1024 / (us * 1e-6) / 1e12
     same = 'ref' if ref is None else ('bit-identical' if torch.equal(ref, y) else
                                      'max diff %.3g' % (ref.float() - y.float()).abs().max().item())
     ref = y if ref is None else ref
