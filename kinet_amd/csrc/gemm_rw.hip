@@ -647,9 +647,10 @@ constexpr int ring_depth() {
 
 // K = 288 (d = 288: configs 3-5): 16-row tiles, 12 columns per lane (NT = 3, 108 weight VGPRs;
 // 180-210 in all: two waves per SIMD).  LayerNorm rows (N <= 288) need the whole row in one
-// workgroup: 6 waves x 48 columns, one workgroup per CU with a ring of up to 4 tiles in 160 KiB;
-// the other epilogues take 4-wave 192-column groups, two per CU (a row tile is shared by its
-// groups through the XCD's L2, as at K = 256).
+// workgroup: 9 waves x 32 columns (NT = 2, 126-152 VGPRs; the 6-wave x 48-column group under
+// flag 4194304), one workgroup per CU with a ring of up to 4 tiles in 160 KiB; the other
+// epilogues take 4-wave 192-column groups, two per CU (a row tile is shared by its groups
+// through the XCD's L2, as at K = 256).
 template <typename T, typename TO, bool HAS_R, bool LN, bool HAS_A2, int NW, int NT = 3, int OCC = NW == 4 ? 2 : 1>
 void launch_288(const GemmArgs& a, hipStream_t stream) {
     constexpr int NS = ring_depth<9, 16, HAS_R, LN, HAS_A2, NT, false, NW, 160 * 1024 / OCC>();
