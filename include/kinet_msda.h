@@ -200,6 +200,11 @@ int kinet_msda_encoder_forward_split(const void* value_main, int64_t main_sb, in
                                      int num_levels, int num_query, int num_point, int output_dtype,
                                      const int32_t* query_tile_order, kinet_stream_t stream);
 
+/* Strips per head map for the calling thread's encoder launches (0 = the plan's own choice; a
+ * count is used when it fits the LDS map, else the plan's choice).  Returns the previous value;
+ * KINET_ERR_ARG outside [0, 64].  Tuning / A/B only: any strip count gives the same output. */
+int kinet_msda_encoder_set_strips(int strips);
+
 /* kinet_msda_encoder_plan for head_dim `channels` (32, or 36: the split kernel, whose LDS map
  * holds 72 bytes per staged pixel). */
 int kinet_msda_encoder_plan_ex(const int64_t* spatial_shapes_host, int batch, int num_heads, int num_query,

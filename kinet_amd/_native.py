@@ -28,6 +28,7 @@ _SIGS = {
     'kinet_msda_backward_last_kernel': [],
     'kinet_msda_encoder_forward': [P, I64, I64, P, P, P, I, P, P] + [I] * 8 + [P, P],
     'kinet_msda_encoder_plan': [P, I, I, I, P],
+    'kinet_msda_encoder_set_strips': [I],
     'kinet_msda_encoder_plan_ex': [P, I, I, I, I, P],
     'kinet_msda_encoder_forward_split': [P, I64, I64, P, I64, I64, P, P, P, I, P, P] + [I] * 8 + [P, P],
     'kinet_msda_sample_records': [P, P, P, P, I, I, I, I, I, P, I, P, P, I, I, I, P, P],

@@ -814,6 +814,10 @@ bool plan_layout(const int64_t* shapes, int fl, int n, EncPlan& pl, int budget =
     return true;
 }
 
+// strips per head map requested by kinet_msda_encoder_set_strips for the calling thread (0 = the
+// plan's own choice; honoured when that many strips fit the LDS map)
+thread_local int enc_strips = 0;
+
 // the fewest gathered levels whose staged levels fit with strips of at least 16 tiles, then the
 // fewest strips (>= what fits) whose workgroups fill >= 90 % of their last round of one per CU
 bool enc_plan(const int64_t* shapes, int batch, int heads, int num_query, EncPlan& pl, bool tail = false) {
@@ -838,6 +842,8 @@ bool enc_plan(const int64_t* shapes, int batch, int heads, int num_query, EncPla
                 break;
             }
         }
+        if (enc_strips >= nmin && enc_strips <= std::min(nmax, 64) && plan_layout(shapes, fl, enc_strips, pl, budget))
+            return true;
         return plan_layout(shapes, fl, n, pl, budget);
     }
     return false;
@@ -847,6 +853,13 @@ bool enc_plan(const int64_t* shapes, int batch, int heads, int num_query, EncPla
 }  // namespace kinet
 
 using namespace kinet;
+
+extern "C" int kinet_msda_encoder_set_strips(int strips) {
+    KINET_CHECK_ARG(strips >= 0 && strips <= 64, "msda encoder: strips must be in [0, 64] (got %d)", strips);
+    const int old = enc_strips;
+    enc_strips = strips;
+    return old;
+}
 
 extern "C" int kinet_msda_encoder_plan(const int64_t* spatial_shapes_host, int batch, int num_heads, int num_query,
                                        int32_t* plan_out) {

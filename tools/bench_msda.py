@@ -76,6 +76,9 @@ def main():
                     help='encoder kernel on sampling records (kinet_msda_encoder_forward_records); the records are '
                          'made once by kinet_msda_sample_records from an identity-like projection of the offsets')
     a = ap.parse_args()
+    if os.environ.get('KINET_ENC_STRIPS'):   # encoder strips per head map (kinet_msda_encoder_set_strips)
+        from kinet_amd import _native
+        _native.lib().kinet_msda_encoder_set_strips(int(os.environ['KINET_ENC_STRIPS']))
     value, ss, offlog, ref, (M, L, P) = make_inputs(B=a.batch, noise=a.noise, decoder=a.decoder,
                                                     dtype=torch.float16)
     offlog = offlog.half()
