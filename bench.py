@@ -46,11 +46,14 @@ PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
 PMC_MFMA = os.path.join(HERE, 'profiles', 'pmc_mfma.json')
 
 WORKLOADS = {
-    'config2': dict(cfgs=('train_deformable',), over={}, h=800, w=1333, batch=16, streams=3, dtype='bf16',
+    # batch per in-flight slot: the interleaved --batch sweeps of round 5 (profiles/r05zz_batch_sweep.txt)
+    # -- config 2: 16 -> 1314-1321, 24 -> 1352-1358, 28 -> 1353-1355, 32 -> 1299-1302 frames/s;
+    # config 3: 8 -> 610-613, 12 -> 627-630, 16 -> 616; config 5: 4, 6, 8 within 1 %
+    'config2': dict(cfgs=('train_deformable',), over={}, h=800, w=1333, batch=24, streams=3, dtype='bf16',
                     K=0, desc='config2 cfgs/train_deformable.yaml: R-50 Deformable-DETR inference forward, '
                               'd=256, 4 levels, 6/6 layers, 300 queries, box refine'),
     'config3': dict(cfgs=('train_deformable', 'train_multi_frame', 'train_tracking'), over=dict(dataset='mot'),
-                    h=800, w=1333, batch=8, streams=3, dtype='f16', K=20,
+                    h=800, w=1333, batch=12, streams=3, dtype='f16', K=20,
                     desc='config3 tracking forward (cfgs/train_tracking.yaml on the multi-frame d=288 stack): R-50, '
                          '500 object + 20 track queries (SURVEY 8(d) row 3), separate per-frame encoders (L=4), 8-level decoder, '
                          'prev-frame features resident, 800x1333 frame pairs'),
