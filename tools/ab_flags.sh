@@ -9,7 +9,7 @@ for f in $fa $fb $fa $fb; do
 import json, sys
 line = [l for l in open(sys.argv[1]) if l.startswith('{')][-1]
 d = json.loads(line)
-t = d.get('train', {}).get('value')
+t = (d.get('train') or {}).get('value')
 print(f"{sys.argv[2]} flags={sys.argv[3]} value={d['value']:.2f}" + (f" train={t:.3f}" if t else ''))
 PY
 done
