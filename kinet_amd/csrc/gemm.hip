@@ -596,7 +596,7 @@ int launch(const GemmArgs& a, hipStream_t stream) {
             if (mfull == 0 && mt_all * nN8 >= 128) mfull = mt_all;
             // a remainder of more than a quarter round: the partly filled last round of 8-wave
             // tiles beats the 4-wave tail (layer-3 3x3 at batch 24: 394 m-tiles = 256 + 138,
-            // 140 vs 171 us, profiles/r05f2_conv24.log); flag 8388608 keeps the split (A/B)
+            // 140 vs 151 us, profiles/r05f2_conv24.log); flag 8388608 keeps the split (A/B)
             if (mfull >= 1 && (mt_all - mfull) * nN8 > 64 && !(kinet_gemm_flags & 8388608)) mfull = mt_all;
             if (mfull >= 1) {
                 int rc = run(a, 256, tn, mfull);
