@@ -97,20 +97,24 @@ def parse():
     ap.add_argument('--msda-records', type=int, default=1,
                     help='1: encoder MSDA calls through the sampling records (kinet_msda_sample_records); '
                          '0: the f16 offsets / logits path (A/B)')
-    ap.add_argument('--enc-panels', type=int, default=None,
-                    help='column panels per strip of the encoder MSDA tile order (kernels.ENC_PANELS; A/B)')
     ap.add_argument('--bneck-pairs', type=int, default=1,
                     help='1: ResNet stage-1 bottleneck pairs (conv3 -> next conv1) as one launch '
                          '(kinet_bottleneck_pair); 0: every conv on its own (A/B)')
+    ap.add_argument('--pair-widths', default=None,
+                    help='comma list of bottleneck widths whose conv3 -> next conv1 run as one kinet_bottleneck_pair '
+                         'launch (backbone.FUSE_PAIR_WIDTHS; A/B)')
+    ap.add_argument('--share-pos', type=int, default=1,
+                    help='1: unpadded frames read one shared position embedding in the encoder projections '
+                         '(DeformableTransformer.share_frame_pos); 0: per-frame rows (A/B)')
     ap.add_argument('--stem-image', type=int, default=1,
                     help='1: the stem conv reads the f32 image directly (kinet_stem_conv_image); '
                          '0: pack_image_kwfold + the folded conv (A/B)')
-    ap.add_argument('--stem-pool', type=int, default=0,
-                    help='1: stem conv + max-pool in one launch (kinet_stem_pool_image; measured slower, '
-                         'DESIGN.md §4); 0: separate')
-    ap.add_argument('--pool-pair', type=int, default=0,
-                    help='1: max-pool + layer1[0].conv1 + downsample in one launch (kinet_pool_conv1x1_pair; '
-                         'measured slower, DESIGN.md §4); 0: separate')
+    ap.add_argument('--ddp-find-unused', type=int, default=1,
+                    help='train leg: DistributedDataParallel find_unused_parameters (1 = the reference, '
+                         'train.py:89-91; 0 skips the extra graph traversal -- every parameter gets a gradient)')
+    ap.add_argument('--detail', default=None,
+                    help='where the full JSON record goes (default gpurun_out/bench_detail.json); stdout '
+                         'carries the compact line')
     ap.add_argument('--cpu-stub', action='store_true',
                     help='tests only: run the launch/timing skeleton with a tiny CPU model over gloo')
     a = ap.parse_args()
@@ -446,7 +450,8 @@ def train_leg(a, dev, world):
                                 device_id=dev)
         own = True
     try:
-        return benchmark_train(steps=a.train_steps, warmup=2, device=dev)
+        return benchmark_train(steps=a.train_steps, warmup=2, device=dev,
+                               find_unused_parameters=bool(a.ddp_find_unused))
     finally:
         if own:
             dist.destroy_process_group()
@@ -496,6 +501,7 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
             with torch.cuda.stream(strs[i % nst]):
                 return model(batches[i % nst], *extra[i % nst])
 
+    eager_step = step
     for i in range(max(1, warmup)):
         out = step(i)
         if i == 0:
@@ -504,15 +510,21 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
             torch.cuda.synchronize()
     torch.cuda.synchronize()
     graphed = False
+    graph_check = None
     if getattr(a, 'graph', 0):
         # one HIP graph per in-flight slot: the whole forward of that slot's batch (the same
-        # kernels, buffers and streams as the eager step), replayed for every timed step
+        # kernels, buffers and streams as the eager step), replayed for every timed step; each
+        # slot captures into its OWN memory pool (the slots replay concurrently on their streams)
+        eager = []
+        for k in range(nst):   # the eager outputs of every slot, kept to check the replays against
+            o = step(k)
+            eager.append((o[0]['pred_logits'].clone(), o[0]['pred_boxes'].clone()))
+        torch.cuda.synchronize()
         try:
-            pool = torch.cuda.graph_pool_handle()
             graphs, gouts = [], []
             for k in range(nst):
                 gr = torch.cuda.CUDAGraph()
-                with torch.no_grad(), torch.cuda.graph(gr, pool=pool, stream=strs[k]):
+                with torch.no_grad(), torch.cuda.graph(gr, pool=torch.cuda.graph_pool_handle(), stream=strs[k]):
                     gouts.append(model(batches[k], *extra[k]))
                 graphs.append(gr)
             torch.cuda.synchronize()
@@ -521,13 +533,25 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
                 with torch.cuda.stream(strs[i % nst]):
                     graphs[i % nst].replay()
                 return gouts[i % nst]
-            for i in range(nst):
+            for i in range(2 * nst):   # every slot replayed twice, concurrently with the others
                 out = step(i)
             torch.cuda.synchronize()
-            graphed = True
+            # the forward is deterministic (fixed-order reductions): replays must equal eager bit for bit
+            same = all(torch.equal(gouts[k][0]['pred_logits'], eager[k][0]) and
+                       torch.equal(gouts[k][0]['pred_boxes'], eager[k][1]) for k in range(nst))
+            if same:
+                graphed, graph_check = True, 'replays bit-identical to eager (every slot)'
+            else:
+                print(f'[bench] {name}: graph replay differs from eager, timing eager', file=sys.stderr)
+                graph_check = 'replay differed from eager: timed eager'
+                del graphs, gouts
+                step = eager_step
         except RuntimeError as ex:   # a capture-unsafe host sync: stay eager (reported in the line)
             print(f'[bench] {name}: HIP graph capture failed ({str(ex)[:120]}), timing eager', file=sys.stderr)
+            graph_check = 'capture failed: timed eager'
+            step = eager_step
             torch.cuda.synchronize()
+        del eager
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -547,6 +571,7 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
     if graphed:
         del graphs, gouts
     run_workload.graphed[name] = graphed
+    run_workload.graph_check[name] = graph_check
 
     # roofline pass: HIP events around every launch of 3 more steps, one stream (the traced
     # kernel durations must not overlap)
@@ -559,7 +584,7 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
         trace = _native.trace_end()
     torch.cuda.synchronize()
     fam, msda = summarize_trace(trace, 3)
-    dec_touched = decoder_touched_bytes(model, samples, extra[0]) if name == 'config2' else None
+    dec_touched = decoder_touched_bytes(model, samples, extra[0])
     split = roofline_split(trace, 3, MFMA_PEAK_TFLOPS[dtype_name])
     del model, batches, extra, trace
     torch.cuda.synchronize()
@@ -568,6 +593,7 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
 
 
 run_workload.graphed = {}
+run_workload.graph_check = {}
 
 
 def msda_roofline(name, msda, dec_touched):
@@ -635,6 +661,116 @@ def msda_roofline(name, msda, dec_touched):
     return r
 
 
+def _r(x, n=4):
+    """x rounded to n significant digits (floats only)."""
+    if isinstance(x, float):
+        return float('%.*g' % (n, x)) if x == x else x
+    return x
+
+
+def _kname(k):
+    """'msda_enc_kernel<kinet::bf16_t, 1, 2, false, true> (encoder launches, ...)' -> short form."""
+    if not k:
+        return k
+    return k.split(' (')[0].replace('kinet::', '').replace(', ', ',')
+
+
+def _roof_c(r, keys=('frac', 'achieved', 'avg_launch_ms', 'algorithmic_bytes_per_launch', 'traffic')):
+    if not r:
+        return None
+    out = {'kernel': _kname(r.get('kernel'))}
+    out.update({k: _r(r.get(k)) for k in keys if r.get(k) is not None})
+    return out
+
+
+def _msda_c(roof):
+    """The MSDA roofline of one workload, compact: encoder sampler (+ traffic), decoder sampler
+    (touched-bytes basis), and the whole encoder call (prep GEMM + sampler)."""
+    if not roof:
+        return None
+    out = {'bound': roof.get('bound'), 'unit': roof.get('unit'), 'peak': roof.get('peak')}
+    out.update(_roof_c(roof))
+    out['launches_per_step'] = _r(roof.get('launches_per_step'))
+    if roof.get('traffic'):
+        out['traffic_x_algorithmic'] = _r(roof['traffic'] / roof['algorithmic_bytes_per_launch'], 3)
+    if roof.get('decoder_kernel'):
+        out['decoder_kernel'] = _roof_c(roof['decoder_kernel'])
+        if roof['decoder_kernel'].get('bytes_basis'):
+            out['decoder_kernel']['basis'] = 'touched value rows + offsets/logits + refs + output'
+    ec = roof.get('encoder_call')
+    if ec:
+        out['encoder_call'] = {k: _r(ec[k]) for k in ('ms', 'prep_ms', 'sampler_ms', 'bytes', 'frac')}
+    return out
+
+
+def _split_c(split):
+    if not split:
+        return None
+    return {k: {'frac': _r(v['frac'], 3), 'ms_per_step': _r(v['ms_per_step'], 3), 'unit': v['unit']}
+            for k, v in split.items() if isinstance(v, dict)}
+
+
+def _sub_c(c):
+    """config3 / config5 sub-object, compact."""
+    if not c:
+        return None
+    return {'workload': c['workload'].split(':')[0], 'value': _r(c['value']), 'unit': c['unit'],
+            'ms_per_step': _r(c['ms_per_step']), 'frames_per_gpu_per_step': c['frames_per_gpu_per_step'],
+            'in_flight_batches': c['in_flight_batches'], 'frame': c['frame'], 'dtype': c['dtype'],
+            'launch': c['launch'], 'graph_check': c.get('graph_check'),
+            'msda_roofline': _msda_c(c.get('roofline')),
+            'gemm_conv_split': _split_c(c.get('roofline_gemm_conv_split')),
+            'device_ms_per_step_by_family': {k: _r(v, 3) for k, v in c['device_ms_per_step_by_family'].items()}}
+
+
+def _train_c(t):
+    if not t:
+        return None
+    hg = t.get('host_glue') or {}
+    mb = t.get('msda_bwd_roofline') or {}
+    dg = t.get('dense_grad_roofline') or {}
+    return {'metric': t['metric'], 'value': _r(t['value']), 'unit': t['unit'], 's_per_step': _r(t['s_per_step']),
+            'steps': t['steps'], 'loss': _r(t['loss']), 'parallelism': t['config']['parallelism'],
+            'host_glue_ms': _r(hg.get('ms_per_step')), 'host_only_ms': _r(hg.get('host_only_ms_per_step')),
+            'msda_bwd': {'kernel': _kname(mb.get('kernel')), 'frac': _r(mb.get('frac')),
+                         'avg_launch_ms': _r(mb.get('avg_launch_ms'))} if mb else None,
+            'dense_grad': {'frac': _r(dg.get('frac')), 'achieved': _r(dg.get('achieved')), 'unit': dg.get('unit'),
+                           'device_ms_per_step': _r(dg.get('device_ms_per_step'))} if dg else None}
+
+
+def compact_line(full, detail_path):
+    """The stdout line: the driver contract's keys, every roofline / sub-benchmark number DESIGN.md
+    quotes, rounded to 4 significant digits, without the long provenance strings (those stay in
+    the full record at `detail_path`) -- so the whole line fits the driver's stdout tail."""
+    line = {k: _r(full[k]) for k in ('metric', 'value', 'unit', 'n_gpus', 'world_size', 'steps', 'warmup',
+                                       'ms_per_step', 'higher_is_better', 'scaling', 'vs_baseline', 'dtype', 'data',
+                                       'config')}
+    line['roofline'] = _msda_c(full['roofline']) if full['roofline'].get('bound') == 'hbm' else full['roofline']
+    if line['roofline'] and full['roofline'].get('traffic_source'):
+        line['roofline']['traffic_pmc'] = 'rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes (profiles/pmc_traffic.json)'
+    rm = full['roofline_mfma']
+    pmc = (rm.get('pmc_mfma_util') or {}).get('groups') or {}
+    line['roofline_mfma'] = {'bound': 'mfma', 'kernel': 'all GEMM + conv launches', 'achieved': _r(rm['achieved']),
+                             'peak': rm['peak'], 'unit': rm['unit'], 'frac': _r(rm['frac']), 'traffic': None,
+                             'device_ms_per_step': _r(rm['device_ms_per_step']),
+                             'algorithmic_flops_per_frame': _r(rm['algorithmic_flops_per_frame']),
+                             'pmc_mfma_busy': {k: _r(v['util'], 3) for k, v in pmc.items()} or None}
+    line['roofline_gemm_conv_split'] = _split_c(full['roofline_gemm_conv_split'])
+    line['msda_ms_per_call'] = {k: _r(v) for k, v in full['msda_ms_per_call'].items()}
+    line['device_ms_per_step_by_family'] = {k: _r(v, 3) for k, v in full['device_ms_per_step_by_family'].items()}
+    line['config3'] = _sub_c(full.get('config3'))
+    line['config5'] = _sub_c(full.get('config5'))
+    line['train'] = _train_c(full.get('train'))
+    cb = full.get('cpu_baseline')
+    line['cpu_baseline'] = None if not cb else {
+        'value': _r(cb['value']), 'unit': cb['unit'], 'cores': cb['cores'], 'kind': cb['kind'],
+        'cpu_model': cb.get('cpu_model'), 'sample': cb['sample'],
+        'msda_encoder_ms_per_call': _r(cb['msda_encoder_ms_per_call']),
+        'config5_msda_encoder_ms_per_call': _r(cb['config5_msda_encoder_ms_per_call'])}
+    line['detail'] = detail_path
+    return line
+
+
 def main():
     a = parse()
     if a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
@@ -650,13 +786,13 @@ def main():
         _native.lib().kinet_ffn_set_debug(a.ffn_knob)
     from kinet_amd import kernels as K
     K.MSDA_RECORDS[0] = bool(a.msda_records)
-    if a.enc_panels is not None:
-        K.ENC_PANELS[0] = a.enc_panels
     from kinet_amd.models import backbone as BB
     BB.FUSE_BOTTLENECK_PAIRS = bool(a.bneck_pairs)
+    from kinet_amd.models.deformable_transformer import DeformableTransformer
+    DeformableTransformer.share_frame_pos = bool(a.share_pos)
+    if a.pair_widths is not None:
+        BB.FUSE_PAIR_WIDTHS = tuple(int(v) for v in a.pair_widths.split(',') if v)
     BB.STEM_FROM_IMAGE = bool(a.stem_image)
-    BB.STEM_POOL = bool(a.stem_pool)
-    BB.POOL_PAIR = bool(a.pool_pair)
     elapsed, fam, msda, split, dec_touched = run_workload(a, a.workload, dev, world, rank, a.batch, a.streams,
                                                           a.height, a.width, a.dtype, a.steps, a.warmup)
 
@@ -665,14 +801,15 @@ def main():
     c5 = None
     if a.workload == 'config2' and not a.no_config5:
         w5 = WORKLOADS['config5']
-        el5, fam5, msda5, split5, _ = run_workload(a, 'config5', dev, world, rank, w5['batch'], w5['streams'],
+        el5, fam5, msda5, split5, dt5 = run_workload(a, 'config5', dev, world, rank, w5['batch'], w5['streams'],
                                                    w5['h'], w5['w'], w5['dtype'], a.config5_steps, 2)
         c5 = {'workload': w5['desc'], 'value': w5['batch'] * a.config5_steps * world / el5, 'unit': 'frames/s',
               'launch': 'HIP graph replay' if run_workload.graphed.get('config5') else 'eager',
+              'graph_check': run_workload.graph_check.get('config5'),
               'frames_per_gpu_per_step': w5['batch'], 'in_flight_batches': w5['streams'],
               'frame': [3, w5['h'], w5['w']], 'dtype': w5['dtype'], 'steps': a.config5_steps, 'warmup': 2,
               'ms_per_step': el5 / a.config5_steps * 1e3,
-              'roofline': msda_roofline('config5', msda5, None),
+              'roofline': msda_roofline('config5', msda5, dt5),
               'roofline_gemm_conv_split': split5,
               'device_ms_per_step_by_family': {k: round(v['ms'], 4) for k, v in fam5.items()}}
 
@@ -680,14 +817,15 @@ def main():
     c3 = None
     if a.workload == 'config2' and not a.no_config3:
         w3 = WORKLOADS['config3']
-        el3, fam3, msda3, split3, _ = run_workload(a, 'config3', dev, world, rank, w3['batch'], w3['streams'],
+        el3, fam3, msda3, split3, dt3 = run_workload(a, 'config3', dev, world, rank, w3['batch'], w3['streams'],
                                                    w3['h'], w3['w'], w3['dtype'], a.config3_steps, 2)
         c3 = {'workload': w3['desc'], 'value': w3['batch'] * a.config3_steps * world / el3, 'unit': 'frames/s',
               'launch': 'HIP graph replay' if run_workload.graphed.get('config3') else 'eager',
+              'graph_check': run_workload.graph_check.get('config3'),
               'frames_per_gpu_per_step': w3['batch'], 'in_flight_batches': w3['streams'],
               'frame': [3, w3['h'], w3['w']], 'dtype': w3['dtype'], 'steps': a.config3_steps, 'warmup': 2,
               'ms_per_step': el3 / a.config3_steps * 1e3,
-              'roofline': msda_roofline('config3', msda3, None),
+              'roofline': msda_roofline('config3', msda3, dt3),
               'roofline_gemm_conv_split': split3,
               'device_ms_per_step_by_family': {k: round(v['ms'], 4) for k, v in fam3.items()}}
 
@@ -734,6 +872,7 @@ def main():
                        'frame': [3, a.height, a.width],
                        'launch': 'HIP graph replay per in-flight slot' if run_workload.graphed.get(a.workload)
                                  else 'eager',
+                       'graph_check': run_workload.graph_check.get(a.workload),
                        'parallelism': f'replicas x{world}'},
             'roofline': roofline,
             'roofline_mfma': mfma_roof,
@@ -745,7 +884,14 @@ def main():
             'cpu_baseline': cpu,
             'train': train,
         }
-        print(json.dumps(line))
+        detail = a.detail or os.path.join('gpurun_out', 'bench_detail.json')
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(detail)), exist_ok=True)
+            with open(detail, 'w') as f:
+                json.dump(line, f)
+        except OSError:
+            detail = None
+        print(json.dumps(compact_line(line, detail), separators=(',', ':')))
     if world > 1:
         dist.destroy_process_group()
 

@@ -76,10 +76,12 @@ int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M, int N, in
 /* kinet_gemm_headmajor with A + A2 as the left operand (the position embedding added at load
  * time, `with_pos_embed` of deformable_transformer.py:278); the MSDA offsets / logits
  * projection of the encoder writes (M, N, Lq, L*P*3) head-major this way
- * (kinet_msda_encoder_forward). */
+ * (kinet_msda_encoder_forward).  a2_rows: 0 = A2 has M rows like A; else A2 has a2_rows rows
+ * (>= 32, dividing M) and row m adds A2 row m % a2_rows -- one frame's position embedding
+ * shared by every frame of an unpadded batch (the same values the reference adds per frame). */
 int kinet_gemm_headmajor_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K,
                             int lda, int ldb, int in_dtype, int out_dtype, const float* bias,
-                            const uint8_t* row_mask, int rows_per_batch, int head_dim,
+                            const uint8_t* row_mask, int rows_per_batch, int head_dim, int a2_rows,
                             kinet_stream_t stream);
 
 /* Split head-major store (round 5, the head_dim-36 MSDA value of configs 3-5): the weight rows
@@ -116,31 +118,13 @@ int kinet_conv2d_splitk(const void* X, const void* Wt, void* Y, int batch, int H
 int kinet_stem_conv_image(const float* img, const void* w_packed, const float* scale, const float* bias,
                           void* Y, int N, int H, int W, int dtype, kinet_stream_t stream);
 
-/* kinet_stem_conv_image followed by torchvision's maxpool (3x3, stride 2, pad 1) in ONE launch:
- * Y NHWC (N, (Ho-1)/2+1, (Wo-1)/2+1, 64) with (Ho, Wo) the conv output; the conv map is never
- * written (bit-identical to kinet_stem_conv_image + kinet_maxpool2d_3x3s2). */
-int kinet_stem_pool_image(const float* img, const void* w_packed, const float* scale, const float* bias,
-                          void* Y, int N, int H, int W, int dtype, kinet_stream_t stream);
-
-/* ResNet stage-1 entry (torchvision resnet50 / 101 as backbone.py:102 builds it): maxpool
- * (3x3 / 2, pad 1) of the stem output X (N, Ho, Wo, 64) NHWC, then layer1[0].conv1 (64 -> 64,
- * + folded bn1, + ReLU) -> T1 (N, Hp, Wp, 64) and layer1[0].downsample (64 -> 256, + folded BN)
- * -> ID (N, Hp, Wp, 256), in ONE launch (the pooled map is not written).  W (320, 64) = conv1
- * weight rows then downsample weight rows (dtype); scale / bias (320) f32 = bn1 then the
- * downsample BN, folded.  dtype KINET_BF16 / KINET_F16. */
-int kinet_pool_conv1x1_pair(const void* X, const void* W, const float* scale, const float* bias, void* T1,
-                            void* ID, int N, int Ho, int Wo, int dtype, kinet_stream_t stream);
-
 /* Diagnostic kernel-selection knob (no reference counterpart; used by the kernel
  * benchmarks to A/B GEMM kernels in one process).  bit 1: allow the 512-thread
  * 256x256-tile LDS-DMA kernel for large-M problems; bit 2: never use the
  * resident-weight streaming kernel; bit 8 (256): keep K = 512 problems off it (the
  * tiled kernel, as before round 3); bit 1024: never the direct 3x3 64 -> 64 channel
  * convolution (the implicit GEMM instead); bit 2048: strided 1x1 convolutions (the stage-2
- * downsample) on the implicit-GEMM kernel instead of the resident-weight conv-row kernel; bit 4096:
- * the direct 3x3 128 -> 128 channel convolution for stage 2's conv2 (opt-in: measured slower than
- * the implicit GEMM); bit 8192: the encoder sampling-records GEMM (kinet_msda_sample_records with
- * x_add) at two workgroups per CU with a 4-slot ring instead of three with a 2-slot ring.
+ * downsample) on the implicit-GEMM kernel instead of the resident-weight conv-row kernel.
  * Returns the previous flags.  Per CALLING THREAD: torch
  * runs autograd backward for device tensors on its own engine thread, so flags set here do
  * NOT reach the backward kernels launched through autograd (only forward / direct calls). */

@@ -157,7 +157,8 @@ int kinet_msda_encoder_plan(const int64_t* spatial_shapes_host, int batch, int n
  * is -1 becomes row 0 with weight a*lh and lh = 0, a bottom row H-1 keeps weight a*(1-lh) and
  * lh = 0; the same for columns), a sample outside the level has weight 0.
  * W: (num_heads*48, K) weight rows grouped (head, level, [x0 y0 .. x3 y3 | logit0 .. logit3]);
- * bias likewise (f32).  A (M, K) rows of stride lda, A2 (optional) added at load (query_pos).
+ * bias likewise (f32).  A (M, K) rows of stride lda, A2 (optional) added at load (query_pos);
+ * a2_rows as kinet_gemm_headmajor_ex (0, or A2 of a2_rows rows shared by every frame).
  * ref_points (M, 4, ref_dim) f32, query_attn_mask (M) bytes or NULL, spatial_shapes_host 4 x
  * (H, W) on the host, each <= 2^(16 - frac_bits); frac_bits in [6, 10]; num_heads % 4 == 0.
  * Replaces the offsets / attention-weight nn.Linear + F.softmax + location arithmetic of
@@ -165,7 +166,7 @@ int kinet_msda_encoder_plan(const int64_t* spatial_shapes_host, int batch, int n
 int kinet_msda_sample_records(const void* A, const void* A2, const void* W, const float* bias, int M,
                               int num_heads, int K, int lda, int in_dtype, const float* ref_points,
                               int ref_dim, const uint8_t* query_attn_mask, const int64_t* spatial_shapes_host,
-                              int num_levels, int num_point, int frac_bits, void* records,
+                              int num_levels, int num_point, int frac_bits, void* records, int a2_rows,
                               kinet_stream_t stream);
 
 /* kinet_msda_encoder_forward fed by sampling records (kinet_msda_sample_records) instead of

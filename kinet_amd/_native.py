@@ -31,13 +31,13 @@ _SIGS = {
     'kinet_msda_encoder_set_strips': [I],
     'kinet_msda_encoder_plan_ex': [P, I, I, I, I, P],
     'kinet_msda_encoder_forward_split': [P, I64, I64, P, I64, I64, P, P, P, I, P, P] + [I] * 8 + [P, P],
-    'kinet_msda_sample_records': [P, P, P, P, I, I, I, I, I, P, I, P, P, I, I, I, P, P],
+    'kinet_msda_sample_records': [P, P, P, P, I, I, I, I, I, P, I, P, P, I, I, I, P, I, P],
     'kinet_msda_encoder_forward_records': [P, I64, I64, P, P, I, P] + [I] * 8 + [P, P],
     'kinet_msda_fused_forward': [P, I64, I64, I64, P, P, I, P, I, P, P, P, P] + [I] * 10 + [P, P],
     'kinet_gemm_set_flags': [I],
     'kinet_gemm_force_tile': [I, I],
     'kinet_gemm_headmajor': [P, P, P] + [I] * 7 + [P, P, I, I, P],
-    'kinet_gemm_headmajor_ex': [P, P, P, P] + [I] * 7 + [P, P, I, I, P],
+    'kinet_gemm_headmajor_ex': [P, P, P, P] + [I] * 7 + [P, P, I, I, I, P],
     'kinet_gemm_headmajor_split': [P, P, P] + [I] * 7 + [P, P, I, I, I, I, P],
     'kinet_gemm': [P, P, P] + [I] * 7 + [P, P, P, I, I, I, P, I, P],
     'kinet_gemm_ex': [P, P, P, P] + [I] * 7 + [P, P, P, I, I, P, P, F, I, P, P],
@@ -49,8 +49,6 @@ _SIGS = {
     'kinet_ffn_set_debug': [I],
     'kinet_ffn_fused': [P, I, P, P, P, P, P, F, P, I, I, I, I, I, P],
     'kinet_stem_conv_image': [P, P, P, P, P, I, I, I, I, P],
-    'kinet_stem_pool_image': [P, P, P, P, P, I, I, I, I, P],
-    'kinet_pool_conv1x1_pair': [P, P, P, P, P, P, I, I, I, I, P],
     'kinet_bottleneck_pack': [P, P, P, P, P, I, I, I, I, P],
     'kinet_bottleneck_pair': [P, I, P, P, P, P, P, P, I, I, I, I, I, P],
     'kinet_layernorm': [P] * 5 + [I, I, F, I, I, P],

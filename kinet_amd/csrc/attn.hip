@@ -118,6 +118,7 @@ __global__ __launch_bounds__(256) void mha_mfma_kernel(const T* __restrict__ Q, 
         }
         Mma<T>::run(o0, va, pb);
         Mma<T>::run(o1, vb, pb);
+        mfma_window_pad<2>();   // the next iteration's rescale reads o0 / o1 across the back edge
     }
     if (!qok) return;
     const float inv = l > 0.f ? 1.f / l : 0.f;

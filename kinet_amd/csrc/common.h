@@ -85,6 +85,20 @@ template <typename T> __device__ __forceinline__ float to_acc(T v, float*) { ret
 
 // compute units of the current device (read once; 256 on MI355X) -- launchers size their
 // grids in rounds of one workgroup per CU
+// N explicit wait states pinned between two scheduling barriers.  ROCm 7.2's hazard recognizer
+// searches an MFMA result window backwards with ONE visited set shared by all predecessor
+// paths, so a window that reaches its reader through a control-flow merge or a loop back edge
+// is padded for whichever path it walks first, not the shortest one (a 3-block reproducer and
+// the scan of this library: tools/mfma_hazard_check.py).  Placed after the
+// last MFMA a loop iteration issues, it covers the back edge.
+template <int N>
+__device__ __forceinline__ void mfma_window_pad() {
+    static_assert(N >= 1 && N <= 16, "s_nop takes 1..16 wait states");
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop %0" ::"i"(N - 1));
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 inline int cu_count() {
     static int n = 0;
     if (n == 0) {

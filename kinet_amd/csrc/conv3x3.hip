@@ -204,142 +204,6 @@ __global__ __launch_bounds__(C3_WAVES * 64, 1) void conv3x3_c64_kernel(const Gem
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// 128 -> 128 channels (ResNet stage-2 conv2, 3x3 / stride 1): the same scheme with K = 1152.
-// 8 waves, wave w owning output channels [16 w, +16) x all 1152 K as 36 A fragments (144
-// VGPRs); tiles of 4 x 32 output pixels whose 6 x 34 halo (256 B per pixel: 52 KiB) is staged by
-// LDS-DMA into a double buffer one tile ahead; every wave reads all 8 pixel sub-tiles' B
-// fragments (16-byte chunks XOR-swizzled by pixel & 15) -- one MFMA per fragment read, as 32
-// channels per wave would need 288 weight registers.
-constexpr int C8_TH = 4, C8_TW = 32;
-constexpr int C8_HH = C8_TH + 2, C8_HW = C8_TW + 2;          // 6 x 34 halo
-constexpr int C8_HPIX = C8_HH * C8_HW;                       // 204 pixels
-constexpr int C8_WAVES = 8;
-constexpr int C8_DMA = 7;                                    // 8 waves x 7 x 4 pixels = 224 >= 204
-constexpr int C8_HBYTES = C8_WAVES * C8_DMA * 4 * 256;       // 56 KiB per halo buffer
-constexpr int C8_OBYTES = C8_TH * C8_TW * 256;               // 32 KiB output staging
-constexpr int C8_KS = 36;                                    // 9 taps x 4 K steps of 32
-static_assert(C8_WAVES * C8_DMA * 4 >= C8_HPIX, "halo fits the DMA slots");
-
-template <typename T>
-__global__ __launch_bounds__(C8_WAVES * 64, 1) void conv3x3_c128_kernel(const GemmArgs p, const int ntiles,
-                                                                       const int ntw, const int tiles_per_img) {
-    __shared__ __attribute__((aligned(16))) char lds[2 * C8_HBYTES + C8_OBYTES + 1024];
-    char* const obuf = lds + 2 * C8_HBYTES;
-    float* const par = reinterpret_cast<float*>(obuf + C8_OBYTES);   // BN scale [128], bias [128]
-    constexpr unsigned OOB = 0x80000000u;
-    const int P = gridDim.x, bx = blockIdx.x;
-    const int cnt = bx < ntiles ? (ntiles - 1 - bx) / P + 1 : 0;
-    if (cnt == 0) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int H = p.Hin, W = p.Win;
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, p.c_bytes, 0x00020000);
-    if (tid < 128) {
-        par[tid] = p.scale ? p.scale[tid] : 1.f;
-        par[128 + tid] = p.bias ? p.bias[tid] : 0.f;
-    }
-    auto tile_origin = [&](int t, int& b, int& oh0, int& ow0) {
-        b = t / tiles_per_img;
-        const int r = t - b * tiles_per_img;
-        const int th = r / ntw;
-        oh0 = th * C8_TH;
-        ow0 = (r - th * ntw) * C8_TW;
-    };
-    // DMA instruction j of this wave: halo pixels [(wave*C8_DMA + j)*4, +4), lane -> pixel +
-    // (lane >> 4), slot (lane & 15) holding logical chunk (lane & 15) ^ (pixel & 15)
-    auto issue_halo = [&](int t, int buf) {
-        int b, oh0, ow0;
-        tile_origin(t, b, oh0, ow0);
-        char* dst = lds + buf * C8_HBYTES;
-#pragma unroll
-        for (int j = 0; j < C8_DMA; ++j) {
-            const int hp = (wave * C8_DMA + j) * 4 + (lane >> 4);
-            const int hr = hp / C8_HW;
-            const int ih = oh0 - 1 + hr, iw = ow0 - 1 + (hp - hr * C8_HW);
-            const bool ok = hp < C8_HPIX && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-            const unsigned ch = (unsigned)(((lane & 15) ^ (hp & 15)) * 16);
-            const unsigned off = ok ? ((unsigned)((b * H + ih) * W + iw) * 256u + ch) : OOB;
-            dma16(rx, dst + (wave * C8_DMA + j) * 1024, off);
-        }
-    };
-    u32x4 wf[C8_KS];
-#pragma unroll
-    for (int s2 = 0; s2 < C8_KS; ++s2) {
-        const unsigned oc = (unsigned)(16 * wave + (lane & 15));
-        wf[s2] = __builtin_amdgcn_raw_buffer_load_b128(rw, (oc * 1152u + (unsigned)(32 * s2 + 8 * (lane >> 4))) * 2u, 0, 0);
-    }
-    const int g4 = lane >> 4;
-    issue_halo(bx, 0);
-    for (int i = 0; i < cnt; ++i) {
-        // tile i's halo landed (younger: the 4 output stores of tile i-1)
-        if (i == 0) c3_wait_vmcnt<0>();
-        else c3_wait_vmcnt<4>();
-        c3_lds_barrier();
-        if (i + 1 < cnt) issue_halo(bx + (i + 1) * P, (i + 1) & 1);
-        const char* hb = lds + (i & 1) * C8_HBYTES;
-        f32x4 acc[8];
-#pragma unroll
-        for (int st = 0; st < 8; ++st) acc[st] = f32x4{0.f, 0.f, 0.f, 0.f};
-        int hq = (lane & 15);
-        asm volatile("" : "+v"(hq));
-        auto read_x = [&](int s2, int st) -> u32x4 {
-            const int tap = s2 >> 2, kh = tap / 3, kw = tap - kh * 3;
-            const int cc = (s2 & 3) * 4 + g4;
-            const int hp = hq + (st >> 1) * C8_HW + (st & 1) * 16 + kh * C8_HW + kw;
-            return *reinterpret_cast<const u32x4*>(hb + hp * 256 + ((cc ^ (hp & 15)) << 4));
-        };
-#pragma unroll
-        for (int s2 = 0; s2 < C8_KS; ++s2) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                u32x4 xb[4];
-#pragma unroll
-                for (int st = 0; st < 4; ++st) xb[st] = read_x(s2, 4 * h + st);
-#pragma unroll
-                for (int st = 0; st < 4; ++st) Mma<T>::run(acc[4 * h + st], wf[s2], xb[st]);
-                // half a K step at a time (else the 288 swizzled fragment addresses are formed
-                // up front and spill)
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        // ---- epilogue: BN + ReLU, park [pixel][128 ch] (chunks swizzled by pixel & 15) ----
-        const int oc0 = 16 * wave + 4 * g4;
-        const f32x4 s4 = *reinterpret_cast<const f32x4*>(par + oc0);
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + 128 + oc0);
-#pragma unroll
-        for (int st = 0; st < 8; ++st) {
-            const int px = (st >> 1) * C8_TW + (st & 1) * 16 + (lane & 15);
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float x = acc[st][r] * s4[r] + b4[r];
-                v[r] = p.relu ? fmaxf(x, 0.f) : x;
-            }
-            uint2 w2;
-            w2.x = (uint32_t)__builtin_bit_cast(uint16_t, Cvt<T>::from(v[0])) | ((uint32_t)__builtin_bit_cast(uint16_t, Cvt<T>::from(v[1])) << 16);
-            w2.y = (uint32_t)__builtin_bit_cast(uint16_t, Cvt<T>::from(v[2])) | ((uint32_t)__builtin_bit_cast(uint16_t, Cvt<T>::from(v[3])) << 16);
-            const int c = oc0 >> 3;
-            *reinterpret_cast<uint2*>(obuf + px * 256 + ((c ^ (px & 15)) << 4) + (oc0 & 4) * 2) = w2;
-        }
-        c3_lds_barrier();
-        int b, oh0, ow0;
-        tile_origin(bx + i * P, b, oh0, ow0);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int q = tid + k * C8_WAVES * 64;   // 16-byte chunk of the 128 x 256 B tile
-            const int px = q >> 4, c = q & 15;
-            const int oh = oh0 + px / C8_TW, ow = ow0 + (px & (C8_TW - 1));
-            const u32x4 v = *reinterpret_cast<const u32x4*>(obuf + px * 256 + ((c ^ (px & 15)) << 4));
-            const bool ok = oh < H && ow < W;
-            const unsigned off = ok ? ((unsigned)((b * H + oh) * W + ow) * (unsigned)p.ldc + (unsigned)(c * 8)) * 2u : OOB;
-            __builtin_amdgcn_raw_buffer_store_b128(v, ry, off, 0, 0);
-        }
-    }
-}
-
 }  // namespace
 
 // Entry from gemm.hip's conv dispatcher: the 3x3 / stride 1 / pad 1, 64 -> 64 channel conv
@@ -370,38 +234,6 @@ bool launch_conv3x3_c64(const GemmArgs& a, int dtype, hipStream_t stream) {
                            nth * ntw);
     else
         hipLaunchKernelGGL((conv3x3_c64_kernel<f16_t>), dim3(grid), dim3(C3_WAVES * 64), 0, stream, g, (int)nt, ntw,
-                           nth * ntw);
-    return true;
-}
-
-// 3x3 / stride 1 / pad 1, 128 -> 128 channels without residual (ResNet stage-2 conv2); false
-// leaves it to the implicit GEMM
-bool launch_conv3x3_c128(const GemmArgs& a, int dtype, hipStream_t stream) {
-    if (dtype != KINET_BF16 && dtype != KINET_F16) return false;
-    if (a.Cin != 128 || a.N != 128 || a.K != 1152 || a.KW != 3 || a.stride != 1 || a.stride_w != 1 || a.pad != 1 ||
-        a.pad_w != 1 || a.Hout != a.Hin || a.Wout != a.Win)
-        return false;
-    if (a.R != nullptr || a.ln_g != nullptr || a.row_mask != nullptr || a.A2 != nullptr || a.kchunk != 0 ||
-        a.hm_rows != 0 || a.m_begin != 0)
-        return false;
-    if (a.ldc < 128 || a.ldc % 8 != 0 || (((uintptr_t)a.C) & 15) != 0) return false;
-    const long long hw = (long long)a.Hout * a.Wout;
-    if (a.M % hw != 0) return false;
-    const int batch = (int)(a.M / hw);
-    const long long cb = ((long long)(a.M - 1) * a.ldc + 128) * 2;
-    if (cb >= (1LL << 31) || (long long)a.M * 256 >= (1LL << 31)) return false;
-    GemmArgs g = a;
-    g.c_bytes = (int)cb;
-    const int nth = (a.Hout + C8_TH - 1) / C8_TH, ntw = (a.Wout + C8_TW - 1) / C8_TW;
-    const long long nt = (long long)batch * nth * ntw;
-    if (nt >= (1LL << 31)) return false;
-    const int cus = cu_count();
-    const int grid = (int)(nt < cus ? nt : cus);
-    if (dtype == KINET_BF16)
-        hipLaunchKernelGGL((conv3x3_c128_kernel<bf16_t>), dim3(grid), dim3(C8_WAVES * 64), 0, stream, g, (int)nt, ntw,
-                           nth * ntw);
-    else
-        hipLaunchKernelGGL((conv3x3_c128_kernel<f16_t>), dim3(grid), dim3(C8_WAVES * 64), 0, stream, g, (int)nt, ntw,
                            nth * ntw);
     return true;
 }

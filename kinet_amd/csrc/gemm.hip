@@ -264,18 +264,20 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
     // to a branch + vmcnt(0) per load, cdna_hip_programming.md §5 item 4(c)).
     constexpr unsigned OOB = 0x80000000u;
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
+    const int a2_bytes = (p.A2 && p.a2_rows) ? ((p.a2_rows - 1) * p.lda + p.K) * (int)sizeof(T) : p.a_bytes;
     const __amdgpu_buffer_rsrc_t ra2 =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(p.A2 ? p.A2 : p.A), (short)0, p.a_bytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(p.A2 ? p.A2 : p.A), (short)0, a2_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
     const bool has_a2 = p.A2 != nullptr;
 
-    unsigned xbase[XR];
+    unsigned xbase[XR], x2sub[XR];   // x2sub: elements back from row m to A2 row m % a2_rows
     int xih[XR], xiw[XR];
     bool xok[XR];
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
         const int m = m0 + sr + 32 * i;
         xok[i] = m < M;
+        x2sub[i] = (!CONV && p.a2_rows) ? (unsigned)(m - m % p.a2_rows) * (unsigned)p.lda : 0u;
         if (CONV) {
             const int hw = p.Hout * p.Wout;
             const int img = m / hw;
@@ -353,7 +355,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
             }
             const unsigned boff = (off * (unsigned)sizeof(T)) | bad;
             xs[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, boff, 0, 0);
-            if (!CONV && has_a2) xs[i] = Mma<T>::add(xs[i], __builtin_amdgcn_raw_buffer_load_b128(ra2, boff, 0, 0));
+            if (!CONV && has_a2)
+                xs[i] = Mma<T>::add(xs[i], __builtin_amdgcn_raw_buffer_load_b128(
+                                               ra2, ((off - x2sub[i]) * (unsigned)sizeof(T)) | bad, 0, 0));
         }
 #pragma unroll
         for (int i = 0; i < WR; ++i) {
@@ -427,6 +431,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs p, const in
         compute(kt & 1);
         store_tile((kt + 1) & 1, xn, wn);
         __syncthreads();
+        // the next step's loads / fragment reads may reuse registers of this step's last MFMAs
+        // (their windows cross the loop back edge)
+        mfma_window_pad<4>();
     };
     load_tile(kmap(0), xs0, ws0);
     load_tile(kmap(1), xs1, ws1);
@@ -622,13 +629,6 @@ int dispatch(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t s) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;
     }
-    // opt-in only: the direct 128-channel kernel measured slower than the implicit GEMM (186-193 vs
-    // 118-134 us at batch 16, profiles/r04v_time.log: one MFMA per LDS fragment read, all 8 waves
-    // reading every fragment -- LDS-bound)
-    if (CONV && (kinet_gemm_flags & 4096) && out_dtype == in_dtype && launch_conv3x3_c128(a, in_dtype, s)) {
-        KINET_LAUNCH_CHECK();
-        return KINET_OK;
-    }
     if (CONV && !(kinet_gemm_flags & 32) && out_dtype == in_dtype && launch_stem_conv(a, in_dtype, s)) {
         KINET_LAUNCH_CHECK();
         return KINET_OK;
@@ -758,7 +758,7 @@ extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M
                                     int rows_per_batch, int head_dim, kinet_stream_t stream);
 extern "C" int kinet_gemm_headmajor_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K,
                                        int lda, int ldb, int in_dtype, int out_dtype, const float* bias,
-                                       const uint8_t* row_mask, int rows_per_batch, int head_dim,
+                                       const uint8_t* row_mask, int rows_per_batch, int head_dim, int a2_rows,
                                        kinet_stream_t stream);
 
 extern "C" int kinet_gemm_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K, int lda,
@@ -794,13 +794,15 @@ extern "C" int kinet_gemm_headmajor(const void* A, const void* B, void* C, int M
                                     int in_dtype, int out_dtype, const float* bias, const uint8_t* row_mask,
                                     int rows_per_batch, int head_dim, kinet_stream_t stream) {
     return kinet_gemm_headmajor_ex(A, nullptr, B, C, M, N, K, lda, ldb, in_dtype, out_dtype, bias, row_mask,
-                                   rows_per_batch, head_dim, stream);
+                                   rows_per_batch, head_dim, 0, stream);
 }
 
 extern "C" int kinet_gemm_headmajor_ex(const void* A, const void* A2, const void* B, void* C, int M, int N, int K,
                                        int lda, int ldb, int in_dtype, int out_dtype, const float* bias,
-                                       const uint8_t* row_mask, int rows_per_batch, int head_dim,
+                                       const uint8_t* row_mask, int rows_per_batch, int head_dim, int a2_rows,
                                        kinet_stream_t stream) {
+    KINET_CHECK_ARG(a2_rows == 0 || (A2 != nullptr && a2_rows >= 32 && M % a2_rows == 0),
+                    "gemm_headmajor: a2_rows must be 0 or >= 32 dividing M (got %d)", a2_rows);
     KINET_CHECK_ARG(out_dtype == in_dtype || (in_dtype == KINET_BF16 && out_dtype == KINET_F16),
                     "gemm_headmajor: out_dtype must equal in_dtype (or f16 from bf16)");
     KINET_CHECK_ARG(M >= 0 && N > 0 && K > 0, "gemm_headmajor: invalid sizes");
@@ -810,7 +812,7 @@ extern "C" int kinet_gemm_headmajor_ex(const void* A, const void* A2, const void
     KINET_CHECK_ARG(aligned16(A) && aligned16(B) && (A2 == nullptr || aligned16(A2)),
                     "gemm_headmajor: A, A2 and B must be 16-byte aligned");
     GemmArgs a{};
-    a.A = A; a.A2 = A2; a.B = B; a.C = C; a.bias = bias; a.row_mask = row_mask;
+    a.A = A; a.A2 = A2; a.B = B; a.C = C; a.bias = bias; a.row_mask = row_mask; a.a2_rows = a2_rows;
     a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = N;
     a.hm_rows = rows_per_batch; a.hm_d = head_dim; a.hm_batch = M / rows_per_batch;
     const long long es = (long long)dtype_size(in_dtype);

@@ -13,6 +13,9 @@ namespace kinet {
 struct GemmArgs {
     const void* A;
     const void* A2;        // optional: A + A2 elementwise (same layout as A)
+    // A2 with a2_rows rows (0: M rows): row m adds A2 row m % a2_rows -- a per-frame operand shared
+    // by every frame of the batch (the position embedding of unpadded equal-size frames)
+    int a2_rows;
     const void* B;
     void* C;
     const void* R;
@@ -59,7 +62,6 @@ bool launch_stem_conv(const GemmArgs& a, int dtype, hipStream_t stream);
 // conv3x3.hip: the direct 3x3 stride-1 64 -> 64 channel convolution (ResNet layer-1 conv2),
 // weights resident in VGPRs, input halo tiles in LDS; false = not that geometry
 bool launch_conv3x3_c64(const GemmArgs& a, int dtype, hipStream_t stream);
-bool launch_conv3x3_c128(const GemmArgs& a, int dtype, hipStream_t stream);
 extern thread_local int rw_min_m;
 extern thread_local int kinet_gemm_flags;   // gemm.hip (diagnostic selection flags; 128 = the read-time-split KINET_F32_X3 TN kernel)
 

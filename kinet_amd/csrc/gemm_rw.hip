@@ -166,19 +166,14 @@ __device__ __forceinline__ void unpack8(const u32x4& u, float* v, bool f16) {
 // max / sum over the 4 lanes lane ^ {0, 16, 32, 48} (the 4 levels of one row): gfx950's row-swap
 // permutes (v_permlane16_swap / v_permlane32_swap) return {own, partner} in some order, so one
 // op per step combines them -- no LDS round trip as __shfl_xor's ds_bpermute takes
-template <bool MAX, bool SHFL = false>
+template <bool MAX>
 __device__ __forceinline__ float level_reduce(float x) {
-    if constexpr (SHFL) {   // diagnostic (DIAG 4): the same reduction through ds_bpermute, no row swaps
-        x = MAX ? fmaxf(x, __shfl_xor(x, 16)) : x + __shfl_xor(x, 16);
-        return MAX ? fmaxf(x, __shfl_xor(x, 32)) : x + __shfl_xor(x, 32);
-    }
     const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     x = MAX ? fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1])) : __uint_as_float(a[0]) + __uint_as_float(a[1]);
     const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return MAX ? fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1])) : __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-template <bool SHFL = false>
 __device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_lds, bool qmasked, int rl, int l,
                                              const float (&v)[12], uint32_t* out) {
     // level constants (lane-dependent level: selects, not an indexed kernel-argument load)
@@ -186,14 +181,14 @@ __device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_
     const int Wl = l == 0 ? p.prep_W[0] : l == 1 ? p.prep_W[1] : l == 2 ? p.prep_W[2] : p.prep_W[3];
     const float Hf = (float)Hl, Wf = (float)Wl;
     const float fs = (float)(1 << p.prep_fb);
-    const float mx = level_reduce<true, SHFL>(fmaxf(fmaxf(v[8], v[9]), fmaxf(v[10], v[11])));
+    const float mx = level_reduce<true>(fmaxf(fmaxf(v[8], v[9]), fmaxf(v[10], v[11])));
     float e[4], es = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         e[q] = __expf(v[8 + q] - mx);
         es += e[q];
     }
-    es = level_reduce<false, SHFL>(es);
+    es = level_reduce<false>(es);
     const float ra = qmasked ? 0.f : __builtin_amdgcn_rcpf(es);
     float rx, ry, sx, sy;   // reference point and the offset scale of each axis
     if (p.prep_refd == 2) {
@@ -234,7 +229,7 @@ __device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_
 // pack_image_kwfold_kernel): K = KH*Cin, logical chunk q of the row = 8 channels of tap
 // kh = q / (Cin/8) read from input row oh*stride - pad + kh (zeros outside the image and past K)
 template <typename T, typename TO, int KC, int NT, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2, bool CR,
-          bool PREP = false, int OCC = 2, int DIAG = 0, int NW = 4>
+          bool PREP = false, int OCC = 2, int NW = 4>
 __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p, const int n_mtiles) {
     using C_ = RwCfg<KC, NT, BMR, NS, HAS_R, LN, HAS_A2, PREP, NW>;
     constexpr int NTHR = C_::NTHR;
@@ -284,8 +279,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
     }
 
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
+    const int a2_bytes = (HAS_A2 && p.a2_rows) ? ((p.a2_rows - 1) * p.lda + p.K) * 2 : p.a_bytes;
     const __amdgpu_buffer_rsrc_t ra2 =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(HAS_A2 ? p.A2 : p.A), (short)0, p.a_bytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(HAS_A2 ? p.A2 : p.A), (short)0, a2_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rr =
         __builtin_amdgcn_make_buffer_rsrc((void*)(HAS_R ? p.R : p.A), (short)0, HAS_R ? p.r_bytes : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rm =
@@ -334,6 +330,16 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
         const int img0 = CR ? m0 / hw : 0;
         const int oh0 = CR ? (m0 - img0 * hw) / p.Wout : 0;
         const int ow0 = CR ? m0 - img0 * hw - oh0 * p.Wout : 0;
+        // A2 of a2_rows rows (row m reads row m % a2_rows): the tile's rows sit in period q0 up
+        // to tile row a2_bnd, in q0 + 1 after it (host: a2_rows >= BMR, so at most one wrap)
+        unsigned a2_sub = 0u, a2_sub1 = 0u;
+        int a2_bnd = 1 << 30;
+        if (HAS_A2 && p.a2_rows) {
+            const int q0 = m0 / p.a2_rows;
+            a2_sub = (unsigned)(q0 * p.a2_rows) * (unsigned)p.lda * 2u;
+            a2_sub1 = a2_sub + (unsigned)p.a2_rows * (unsigned)p.lda * 2u;
+            a2_bnd = (q0 + 1) * p.a2_rows - m0;
+        }
 #pragma unroll
         for (int j = 0; j < C_::A_OPS; ++j) {
             unsigned off = m0 + a_row[j] < M ? abase + a_lo[j] : OOB;
@@ -350,7 +356,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
                 off = ok ? ((unsigned)((img * p.Hin + ih) * p.Win + ow * p.stride_w) * (unsigned)p.Cin + a_lo[j]) * 2u : OOB;
             }
             dma16(ra, st + (j * NTHR + wave * 64) * 16, off);
-            if (HAS_A2) dma16(ra2, st + C_::A_SPAN + (j * NTHR + wave * 64) * 16, off);
+            if (HAS_A2)
+                dma16(ra2, st + C_::A_SPAN + (j * NTHR + wave * 64) * 16,
+                      off == OOB ? OOB : off - (a_row[j] >= a2_bnd ? a2_sub1 : a2_sub));
         }
         const unsigned rbase = (unsigned)m0 * (unsigned)p.ldr * 2u;
 #pragma unroll
@@ -511,16 +519,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
                 for (int a = 0; a < NT; ++a) Mma<T>::run(acc[a][t], wf[a][c], xf);
             }
 
-        if constexpr (DIAG == 1) {   // diagnostic: 32 idle wait states between the MFMAs and the epilogue
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-        } else if constexpr (DIAG == 2) {   // diagnostic: every wave's memory traffic retired first
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            __syncthreads();
-        } else if constexpr (DIAG == 3) {   // diagnostic: MFMAs and epilogue kept apart, no idle states
-            __builtin_amdgcn_sched_barrier(0);
-        }
         // ---- epilogue (registers) ----
         float v[TMR][NC];
         if constexpr (PREP) {
@@ -528,7 +526,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
             for (int t = 0; t < TMR; ++t) {
 #pragma unroll
                 for (int j = 0; j < NC; ++j) v[t][j] = acc[j >> 2][t][j & 3] + par[GW + cl0 + j];
-                prep_records<DIAG == 4>(p, st + C_::REF_OFF, st[C_::MASK_OFF + t * 16 + (lane & 15)] != 0,
+                prep_records(p, st + C_::REF_OFF, st[C_::MASK_OFF + t * 16 + (lane & 15)] != 0,
                                         t * 16 + (lane & 15), lane >> 4, v[t], pend[t]);
             }
             pend_m0 = m0;
@@ -618,7 +616,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
 }
 
 template <typename T, typename TO, int KC, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2 = false, int NT = 4,
-          bool CR = false, bool PREP = false, int OCC = 2, int DIAG = 0, int NW = 4>
+          bool CR = false, bool PREP = false, int OCC = 2, int NW = 4>
 void launch_cfg(const GemmArgs& a, hipStream_t stream) {
     constexpr int GW = NW * NT * 16;
     const int n_mtiles = (a.M + BMR - 1) / BMR;
@@ -631,7 +629,7 @@ void launch_cfg(const GemmArgs& a, hipStream_t stream) {
     int P = slots / ng >= 8 ? slots / ng / 8 * 8 : slots / ng;
     if (P > n_mtiles) P = n_mtiles;
     dim3 grid(P, ng), block(NW * 64);
-    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR, PREP, OCC, DIAG, NW>), grid, block, 0,
+    hipLaunchKernelGGL((gemm_rw_kernel<T, TO, KC, NT, BMR, NS, HAS_R, LN, HAS_A2, CR, PREP, OCC, NW>), grid, block, 0,
                        stream, a, n_mtiles);
 }
 
@@ -655,7 +653,7 @@ template <typename T, typename TO, bool HAS_R, bool LN, bool HAS_A2, int NW, int
 void launch_288(const GemmArgs& a, hipStream_t stream) {
     constexpr int NS = ring_depth<9, 16, HAS_R, LN, HAS_A2, NT, false, NW, 160 * 1024 / OCC>();
     static_assert(NS >= 2, "LDS budget");
-    launch_cfg<T, TO, 9, 16, NS, HAS_R, LN, HAS_A2, NT, false, false, OCC, 0, NW>(a, stream);
+    launch_cfg<T, TO, 9, 16, NS, HAS_R, LN, HAS_A2, NT, false, false, OCC, NW>(a, stream);
 }
 
 template <typename T, typename TO, int KC, bool HAS_R, bool LN, bool HAS_A2, int NT = 4>
@@ -705,9 +703,8 @@ void launch_t(const GemmArgs& a, hipStream_t stream) {
             return;
         }
         // LayerNorm rows: 9 waves x 32 columns (one 288-column group; flag 4194304: the 6-wave x
-        // 48-column groups, A/B and tests); N <= 288 without LayerNorm: 9-wave groups under flag
-        // 2097152 (A/B), else 4-wave 192-column groups
-        const bool w9 = a.N <= 288 && (kinet_gemm_flags & 2097152);
+        // 48-column groups, A/B and tests); without LayerNorm 4-wave 192-column groups (one 9-wave
+        // group measured within noise, round 5: profiles/r05s_split_nine_waves.log)
         if (r && ln) {
             if (kinet_gemm_flags & 4194304) launch_288<T, TO, true, true, false, 6>(a, stream);
             else launch_288<T, TO, true, true, false, 9, 2>(a, stream);
@@ -715,11 +712,9 @@ void launch_t(const GemmArgs& a, hipStream_t stream) {
             if (kinet_gemm_flags & 4194304) launch_288<T, TO, false, true, false, 6>(a, stream);
             else launch_288<T, TO, false, true, false, 9, 2>(a, stream);
         } else if (r) {
-            if (w9) launch_288<T, TO, true, false, false, 9, 2>(a, stream);
-            else launch_288<T, TO, true, false, false, 4>(a, stream);
+            launch_288<T, TO, true, false, false, 4>(a, stream);
         } else {
-            if (w9) launch_288<T, TO, false, false, false, 9, 2>(a, stream);
-            else launch_288<T, TO, false, false, false, 4>(a, stream);
+            launch_288<T, TO, false, false, false, 4>(a, stream);
         }
         return;
     }
@@ -831,7 +826,9 @@ extern "C" int kinet_msda_sample_records(const void* A, const void* A2, const vo
                                          int num_heads, int K, int lda, int in_dtype, const float* ref_points,
                                          int ref_dim, const uint8_t* query_attn_mask, const int64_t* spatial_shapes_host,
                                          int num_levels, int num_point, int frac_bits, void* records,
-                                         kinet_stream_t stream) {
+                                         int a2_rows, kinet_stream_t stream) {
+    KINET_CHECK_ARG(a2_rows == 0 || (A2 != nullptr && a2_rows >= 32 && M % a2_rows == 0),
+                    "msda records: a2_rows must be 0 or >= 32 dividing M (got %d)", a2_rows);
     KINET_CHECK_ARG(M >= 0 && num_heads > 0 && num_heads % 4 == 0, "msda records: heads must be a multiple of 4 (got %d)",
                     num_heads);
     KINET_CHECK_ARG(num_levels == 4 && num_point == 4, "msda records: 4 levels x 4 points (got %d, %d)", num_levels,
@@ -857,7 +854,7 @@ extern "C" int kinet_msda_sample_records(const void* A, const void* A2, const vo
     const long long cb = (long long)num_heads * M * 96, rb = (long long)M * 16 * ref_dim;
     KINET_CHECK_ARG(ab < (1LL << 31) && cb < (1LL << 31) && rb < (1LL << 31), "msda records: operands larger than 2 GiB");
     GemmArgs a{};
-    a.A = A; a.A2 = A2; a.B = W; a.C = records; a.bias = bias; a.row_mask = query_attn_mask;
+    a.A = A; a.A2 = A2; a.B = W; a.C = records; a.bias = bias; a.row_mask = query_attn_mask; a.a2_rows = a2_rows;
     a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = K; a.ldc = N;
     a.a_bytes = (int)ab; a.b_bytes = (int)bb; a.c_bytes = (int)cb;
     a.prep_ref = ref_points; a.prep_refd = ref_dim; a.prep_fb = frac_bits;
@@ -866,38 +863,20 @@ extern "C" int kinet_msda_sample_records(const void* A, const void* A2, const vo
         a.prep_W[l] = (int)spatial_shapes_host[2 * l + 1];
     }
     hipStream_t s = (hipStream_t)stream;
-    constexpr int NS2 = ring_depth<8, 16, false, false, true, 3, true>();
     constexpr int NS1 = ring_depth<8, 16, false, false, false, 3, true>();
     // three workgroups per CU (159 VGPRs, a 2-slot ring: 39 KiB of LDS each) when the tile adds
     // A2: alone the call is ~4 % slower than two workgroups with a 4-slot ring (228 vs 220 us),
     // but under the bench's three batches in flight the whole step is 0.9 % faster (1311 / 1316
     // vs 1304 / 1299 frames/s, profiles/r04z_occ_ab.log) -- the smaller LDS footprint leaves room
-    // for the other streams' workgroups.  Four per CU (128 VGPRs) spills and loses 7 %.  Flag
-    // 8192: the two-workgroup ring.
-    // diagnostic (round 5): the 32-row records tile that differed from the 16-row tile in round 4
-    // (flag 16384; + 32768: idle wait states before the epilogue; + 65536: traffic drained first;
-    // + 262144: MFMAs and epilogue kept apart by a scheduling barrier only; + 524288: the level
-    // reductions through ds_bpermute instead of v_permlane16/32_swap)
-    if ((kinet_gemm_flags & 16384) && A2 && in_dtype == KINET_BF16) {
-        if (kinet_gemm_flags & 32768) launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2, 1>(a, s);
-        else if (kinet_gemm_flags & 65536) launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2, 2>(a, s);
-        else if (kinet_gemm_flags & 262144) launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2, 3>(a, s);
-        else if (kinet_gemm_flags & 524288) launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2, 4>(a, s);
-        else launch_cfg<bf16_t, f16_t, 8, 32, 2, false, false, true, 3, false, true, 2>(a, s);
-        KINET_LAUNCH_CHECK();
-        return KINET_OK;
-    }
-    if (!(kinet_gemm_flags & 8192) && A2) {
-        if (in_dtype == KINET_BF16) launch_cfg<bf16_t, f16_t, 8, 16, 2, false, false, true, 3, false, true, 3>(a, s);
-        else launch_cfg<f16_t, f16_t, 8, 16, 2, false, false, true, 3, false, true, 3>(a, s);
-        KINET_LAUNCH_CHECK();
-        return KINET_OK;
-    }
+    // for the other streams' workgroups.  Four per CU (128 VGPRs) spills and loses 7 %.  The
+    // 32-row tile (two MFMA row tiles per wave) is not used here: its epilogue, interleaved by the
+    // compiler with the second tile's MFMA chain, differed from the 16-row tile in a few hundred
+    // record words from run to run (round 4-5)
     if (in_dtype == KINET_BF16) {
-        if (A2) launch_cfg<bf16_t, f16_t, 8, 16, NS2, false, false, true, 3, false, true>(a, s);
+        if (A2) launch_cfg<bf16_t, f16_t, 8, 16, 2, false, false, true, 3, false, true, 3>(a, s);
         else launch_cfg<bf16_t, f16_t, 8, 16, NS1, false, false, false, 3, false, true>(a, s);
     } else {
-        if (A2) launch_cfg<f16_t, f16_t, 8, 16, NS2, false, false, true, 3, false, true>(a, s);
+        if (A2) launch_cfg<f16_t, f16_t, 8, 16, 2, false, false, true, 3, false, true, 3>(a, s);
         else launch_cfg<f16_t, f16_t, 8, 16, NS1, false, false, false, 3, false, true>(a, s);
     }
     KINET_LAUNCH_CHECK();

@@ -908,7 +908,7 @@ __device__ __forceinline__ int hash_slot(int* keys, int* plist, int* npass, int 
     return -1;
 }
 
-template <typename T, typename TL, int VEC, int NJ, int SP = 2, bool CS = false>
+template <typename T, typename TL, int VEC, int NJ, int SP = 2>
 __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
     const T* __restrict__ value, const int64_t* __restrict__ shapes, const TL* __restrict__ loc,
     const TL* __restrict__ attw, const T* __restrict__ gout, float* __restrict__ gvalue,
@@ -923,15 +923,14 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
     int* keys = reinterpret_cast<int*>(smem + sizeof(LevelInfo));
     int* head = keys + NS;
     int* plist = head + NS;
-    int* npass = plist + NS;   // [0] slots used by the pass; CS: [1..] wave totals of the scan
-    int2* cinfo = reinterpret_cast<int2*>(npass + (CS ? 12 : 4));
-    int* next = reinterpret_cast<int*>(cinfo + 4 * NSMP);   // CS: (slot << 16) | rank, -1 = not listed
+    int* npass = plist + NS;   // [0] slots used by the pass
+    int2* cinfo = reinterpret_cast<int2*>(npass + 4);
+    int* next = reinterpret_cast<int*>(cinfo + 4 * NSMP);
     float* G = reinterpret_cast<float*>(next + 4 * NSMP);
     HTap* taps = reinterpret_cast<HTap*>(G + QP * D);
-    int* srt = reinterpret_cast<int*>(taps + NSMP);          // CS: corner ids sorted by slot
     const int b = blockIdx.y, m = blockIdx.z;
     load_levels(li, shapes, L, S);
-    for (int i = threadIdx.x; i < NS; i += nt) { keys[i] = -1; head[i] = CS ? 0 : -1; }
+    for (int i = threadIdx.x; i < NS; i += nt) { keys[i] = -1; head[i] = -1; }
     if (threadIdx.x == 0) {
         *npass = 0;
         // blocked (encoder calls, queries = pixels in raster order): chunk = one 8 x BH block
@@ -980,10 +979,6 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
             HTap t;
 #pragma unroll
             for (int k = 0; k < 4; ++k) t.off[k] = -1;
-            if constexpr (CS) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) next[4 * s + k] = -1;
-            }
             t.lh = t.lw = t.a = 0.f;
             t.flags = 0;
             if (q >= 0) {
@@ -1015,8 +1010,7 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
                             } else {
                                 const int cid = 4 * s + k;
                                 cinfo[cid] = make_int2(__float_as_int(wt[k] * t.a), qi * D);
-                                if constexpr (CS) next[cid] = (slot << 16) | atomicAdd(head + slot, 1);
-                                else next[cid] = atomicExch(head + slot, cid);
+                                next[cid] = atomicExch(head + slot, cid);
                             }
                         }
                 }
@@ -1024,40 +1018,6 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
             taps[s] = t;
         }
         __syncthreads();
-        if constexpr (CS) {
-            // counting sort of the pass's listed corners by slot: exclusive scan of the slot
-            // counts in plist order (in place: head[slot] becomes the slot's first position),
-            // then every listed corner id lands at its slot's position + its insertion rank
-            const int ns = *npass;
-            const int per = (ns + nt - 1) / nt;
-            const int b0 = min(ns, (int)threadIdx.x * per), b1 = min(ns, b0 + per);
-            int tsum = 0;
-            for (int j = b0; j < b1; ++j) tsum += head[plist[j]];
-            int incl = tsum;
-            const int wl = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int u = __shfl_up(incl, o);
-                if (wl >= o) incl += u;
-            }
-            if (wl == 63) npass[1 + wv] = incl;
-            __syncthreads();
-            int run = incl - tsum;
-            for (int w = 0; w < wv; ++w) run += npass[1 + w];
-            for (int j = b0; j < b1; ++j) {
-                const int sl = plist[j];
-                const int c = head[sl];
-                head[sl] = run;
-                run += c;
-            }
-            __syncthreads();
-            for (int cid = threadIdx.x; cid < 4 * NSMP; cid += nt) {
-                const int v = next[cid];
-                if (v >= 0) srt[head[v >> 16] + (v & 0xffff)] = cid;
-            }
-            __syncthreads();
-        }
-
         // phase 2: 16 lanes per query -- value corners for the location / weight gradients
         // (lanes < NA hold VEC contiguous channels); overflowed corners added directly
         for (int qi = threadIdx.x >> 4; qi < QP; qi += nt >> 4) {
@@ -1156,46 +1116,21 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
         // phase 3 (reads only what phase 1 wrote, so no barrier before it): lane = (slot,
         // channel), consecutive lanes on consecutive channels of the pass's rows
         const int n = (dbg & 4) ? 0 : *npass;
-        if constexpr (CS) {
-            // the slot's corners are contiguous in srt: their loads do not chain
-            int total = 0;
-            for (int w = 0; w < (nt >> 6); ++w) total += npass[1 + w];
-            // (a 4-channel-per-lane variant measured 2.2x slower: its 4 strided atomics per
-            // lane touch 4x the cache lines per instruction)
-            for (int i = threadIdx.x; i < n * D; i += nt) {
-                const int si = i / D, c = i - si * D;
-                const int slot = plist[si];
-                const int e0 = head[slot], e1 = si + 1 < n ? head[plist[si + 1]] : total;
-                float acc = 0.f;
-                int e = e0;
-                for (; e + 1 < e1; e += 2) {
-                    const int2 c0 = cinfo[srt[e]], c1 = cinfo[srt[e + 1]];
-                    acc += __int_as_float(c0.x) * G[c0.y + c];
-                    acc += __int_as_float(c1.x) * G[c1.y + c];
-                }
-                if (e < e1) {
-                    const int2 c0 = cinfo[srt[e]];
-                    acc += __int_as_float(c0.x) * G[c0.y + c];
-                }
-                if (!(dbg & 2)) atomicAdd(gimg + (long)keys[slot] * MD + c, acc);
+        for (int i = threadIdx.x; i < n * D; i += nt) {
+            const int si = i / D, c = i - si * D;
+            const int slot = plist[si];
+            float acc = 0.f;
+            for (int cid = head[slot]; cid >= 0; cid = next[cid]) {
+                const int2 ci = cinfo[cid];
+                acc += __int_as_float(ci.x) * G[ci.y + c];
             }
-        } else {
-            for (int i = threadIdx.x; i < n * D; i += nt) {
-                const int si = i / D, c = i - si * D;
-                const int slot = plist[si];
-                float acc = 0.f;
-                for (int cid = head[slot]; cid >= 0; cid = next[cid]) {
-                    const int2 ci = cinfo[cid];
-                    acc += __int_as_float(ci.x) * G[ci.y + c];
-                }
-                if (!(dbg & 2)) atomicAdd(gimg + (long)keys[slot] * MD + c, acc);
-            }
+            if (!(dbg & 2)) atomicAdd(gimg + (long)keys[slot] * MD + c, acc);
         }
         __syncthreads();
         for (int i = threadIdx.x; i < n; i += nt) {
             const int slot = plist[i];
             keys[slot] = -1;
-            head[slot] = CS ? 0 : -1;
+            head[slot] = -1;
         }
         if (threadIdx.x == 0) *npass = 0;
         __syncthreads();
@@ -1321,10 +1256,8 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
         const int QP = tn.flush_at > 0 ? tn.flush_at : threads / 16;   // queries per pass
         const int log2ns = tn.log2ns ? tn.log2ns : 10;
         const size_t nsmp = (size_t)QP * LP;
-        const bool cs = tn.mode == 4;   // counting-sorted corner lists (A/B)
-        const size_t lds = sizeof(LevelInfo) + ((size_t)3 << log2ns) * sizeof(int) + (cs ? 12 : 4) * sizeof(int) +
-                           nsmp * 4 * (sizeof(int2) + sizeof(int)) + (size_t)QP * D * sizeof(float) + nsmp * sizeof(HTap) +
-                           (cs ? nsmp * 4 * sizeof(int) : 0);
+        const size_t lds = sizeof(LevelInfo) + ((size_t)3 << log2ns) * sizeof(int) + 4 * sizeof(int) +
+                           nsmp * 4 * (sizeof(int2) + sizeof(int)) + (size_t)QP * D * sizeof(float) + nsmp * sizeof(HTap);
         KINET_CHECK_ARG(threads % 64 == 0 && threads <= 512 && QP >= 1 && lds <= 160 * 1024,
                         "msda backward: pass of %d queries x %d samples does not fit LDS", QP, LP);
         // query chunk per workgroup: as long as the grid still fills the chip 4 times over
@@ -1341,12 +1274,7 @@ int launch_bwd(const void* value, const int64_t* shapes, const void* loc, const 
         const int nq = blocked ? (S + QP - 1) / QP : (Lq + qc - 1) / qc;
         dim3 grid(blocked ? nq + nq / 8 + 2 * L : nq, N, M);
 #define KH(VEC, NJ)                                                                                             \
-    if (cs)                                                                                                     \
-        hipLaunchKernelGGL((msda_bwd_list_kernel<T, TL, VEC, NJ, 2, true>), grid, dim3(threads), lds, stream,   \
-                           (const T*)value, shapes, (const TL*)loc, (const TL*)attw, (const T*)gout,            \
-                           (float*)acc_buf, (TL*)gloc, (TL*)gattw, S, M, D, L, Lq, P, qc, QP, c.lpq, log2ns,    \
-                           blocked, bwd_dbg);                                                                   \
-    else if (tn.mode == 3)                                                                                      \
+    if (tn.mode == 3)                                                                                           \
         hipLaunchKernelGGL((msda_bwd_list_kernel<T, TL, VEC, NJ, 4>), grid, dim3(threads), lds, stream,         \
                            (const T*)value, shapes, (const TL*)loc, (const TL*)attw, (const T*)gout,            \
                            (float*)acc_buf, (TL*)gloc, (TL*)gattw, S, M, D, L, Lq, P, qc, QP, c.lpq, log2ns,    \

@@ -358,216 +358,6 @@ __global__ __launch_bounds__(256, 2) void stem_img_kernel(const StemImgArgs p, c
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Stem + max-pool (torchvision conv1 + bn1 + relu + maxpool 3x3/2 pad 1) in one launch, from the
-// f32 image (kinet_stem_pool_image): the 64-channel conv output (546 MB at batch 16) is never
-// written; only the pooled map (137 MB) is.  A workgroup owns 2 pooled rows x 32 pooled columns:
-// their windows cover conv rows 4t-1 .. 4t+3 and conv columns 64u-1 .. 64u+63, computed here
-// as 5 rows x 80 columns (5 MFMA pixel tiles; 1.56x the conv's MFMA work, the price of not
-// exchanging halos between workgroups).  Wave w owns output channels [16w, 16w+16) of all 25
-// (row, pixel-tile) tiles, its 6 weight fragments in registers; the folded input rows (15) are
-// built in LDS from the image as in stem_img_kernel; the conv tile is parked in LDS (BN + ReLU,
-// positions outside the conv output zeroed -- post-ReLU values are >= 0, so a zero stands in for
-// the pool's -inf padding) and pooled from there.
-constexpr int SP_ROWS = 5, SP_PXT = 5, SP_PX = SP_PXT * 16;   // conv rows / pixels per tile
-constexpr int SP_IN = 2 * (SP_ROWS - 1) + SK_KH;              // 15 folded input rows
-constexpr int SP_RAWC = 168;                                  // >= 2*(SP_PX-1) + 7
-constexpr int SP_PAIRS = SP_IN * 3;                           // 45 row-planes
-constexpr int SP_PPW = (SP_PAIRS + 3) / 4;                    // 12 per wave
-constexpr int SP_FOLD = SP_IN * SP_PX * 48;                   // 57600 B
-constexpr int SP_PARK = SP_ROWS * SP_PX * SK_CO * 2;          // 51200 B
-static_assert(SP_PARK <= SP_FOLD, "parked conv tile fits the folded rows");
-
-template <typename T>
-__global__ __launch_bounds__(256, 2) void stem_pool_kernel(const StemImgArgs p, const int tiles_x, const int tiles_y,
-                                                           const int ntiles) {
-    __shared__ __attribute__((aligned(16))) char lds[SP_FOLD];
-    __shared__ __attribute__((aligned(16))) uint16_t raw[SP_PAIRS * SP_RAWC];
-    __shared__ float par[2][SK_CO];
-    constexpr unsigned OOB = 0x80000000u;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (tid < SK_CO) {
-        par[0][tid] = p.scale ? p.scale[tid] : 1.f;
-        par[1][tid] = p.bias ? p.bias[tid] : 0.f;
-    }
-    const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void*)p.img, (short)0, p.img_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, (short)0, p.w_bytes, 0x00020000);
-    // p.Ho / p.Wo: the conv output; the pooled map is ((Ho-1)/2+1, (Wo-1)/2+1)
-    const int Hp = (p.Ho - 1) / 2 + 1, Wp = (p.Wo - 1) / 2 + 1;
-    struct Tile { int n, ph0, pw0; };
-    auto decode = [&](int t) {
-        const int bx = t % tiles_x, rest = t / tiles_x;
-        return Tile{rest / tiles_y, (rest % tiles_y) * 2, bx * 32};
-    };
-    // this wave's weights: output channels 16 wave + (lane & 15), the 6 K-steps
-    u32x4 wf[SK_KS];
-#pragma unroll
-    for (int s2 = 0; s2 < SK_KS; ++s2) {
-        const int k = 32 * s2 + 8 * (lane >> 4);
-        const unsigned off = k < SK_NCH * 8 ? ((unsigned)((wave * 16 + (lane & 15)) * (SK_KH * SK_CG) + k)) * 2u : OOB;
-        wf[s2] = __builtin_amdgcn_raw_buffer_load_b128(rw, off, 0, 0);
-    }
-    float xin[SP_PPW][3];
-    auto load_in = [&](const Tile& tl) {
-        const int ih0 = 4 * tl.ph0 - 5, iw0 = 4 * tl.pw0 - 5;   // conv row 2ph0-1 -> input row 2(2ph0-1)-3
-#pragma unroll
-        for (int i = 0; i < SP_PPW; ++i) {
-            const int pr = i * 4 + wave;
-            const int r = pr / 3, c = pr - 3 * r;
-            const int ih = ih0 + r;
-            const bool rok = pr < SP_PAIRS && (unsigned)ih < (unsigned)p.H;
-            const unsigned rowb = (unsigned)(((tl.n * 3 + c) * p.H + ih) * p.W_);
-#pragma unroll
-            for (int k3 = 0; k3 < 3; ++k3) {
-                const int k = lane + 64 * k3, iw = iw0 + k;
-                const bool ok = rok && k < SP_RAWC && (unsigned)iw < (unsigned)p.W_;
-                xin[i][k3] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ri, ok ? (rowb + (unsigned)iw) * 4u : OOB, 0, 0));
-            }
-        }
-    };
-    int t = blockIdx.x;
-    Tile cur = decode(t);
-    load_in(cur);
-    T* __restrict__ Y = (T*)p.Y;
-
-    for (; t < ntiles; t += gridDim.x) {
-#pragma unroll
-        for (int i = 0; i < SP_PPW; ++i) {
-            const int pr = i * 4 + wave;
-            if (pr < SP_PAIRS) {
-#pragma unroll
-                for (int k3 = 0; k3 < 3; ++k3) {
-                    const int k = lane + 64 * k3;
-                    if (k < SP_RAWC) raw[pr * SP_RAWC + k] = __builtin_bit_cast(uint16_t, Cvt<T>::from(xin[i][k3]));
-                }
-            }
-        }
-        __syncthreads();
-        for (int rp = tid; rp < SP_IN * SP_PX; rp += 256) {
-            const int r = rp / SP_PX, px = rp - r * SP_PX;
-            const uint16_t* src = raw + r * 3 * SP_RAWC + 2 * px;
-            u32x4* dst = reinterpret_cast<u32x4*>(lds + rp * 48);
-#pragma unroll
-            for (int part = 0; part < 3; ++part) {
-                uint32_t w[4];
-#pragma unroll
-                for (int e2 = 0; e2 < 4; ++e2) {
-                    uint32_t h2[2];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int j = part * 8 + 2 * e2 + h, kw = j / 3, c = j - 3 * kw;
-                        h2[h] = j < SK_KH * 3 ? (uint32_t)src[c * SP_RAWC + kw] : 0u;
-                    }
-                    w[e2] = h2[0] | (h2[1] << 16);
-                }
-                dst[part] = u32x4{w[0], w[1], w[2], w[3]};
-            }
-        }
-        __syncthreads();
-        const int tn = t + gridDim.x;
-        const Tile nxt = decode(tn < ntiles ? tn : t);
-
-        // conv: acc[r][q] = channels 16 wave + 4 (lane >> 4) + i of pixel 16 q + (lane & 15) of row r
-        f32x4 acc[SP_ROWS][SP_PXT];
-#pragma unroll
-        for (int r = 0; r < SP_ROWS; ++r)
-#pragma unroll
-            for (int q = 0; q < SP_PXT; ++q) acc[r][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < SK_KS; ++s2) {
-            const int ci = 4 * s2 + (lane >> 4);
-            const int kh = ci / 3, part = ci - 3 * kh;
-            const bool valid = ci < SK_NCH;
-#pragma unroll
-            for (int r = 0; r < SP_ROWS; ++r) {
-                const char* rowp = lds + (2 * r + (valid ? kh : 0)) * (SP_PX * 48) + part * 16;
-#pragma unroll
-                for (int q = 0; q < SP_PXT; ++q) {
-                    u32x4 b = *reinterpret_cast<const u32x4*>(rowp + (q * 16 + (lane & 15)) * 48);
-                    if (!valid) b = u32x4{0u, 0u, 0u, 0u};
-                    Mma<T>::run(acc[r][q], wf[s2], b);
-                }
-            }
-            // fragment reads at most a few MFMAs ahead (all 25 hoisted: 100 more VGPRs)
-#pragma unroll
-            for (int u = 0; u < SP_ROWS * SP_PXT; ++u) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            }
-        }
-        __syncthreads();   // folded rows consumed: the LDS takes the conv tile
-
-        // BN + ReLU; positions outside the conv output -> 0; park [row][pixel][64 ch], 16-byte
-        // chunks XOR-swizzled by (pixel & 7)
-        {
-            const int ch0 = wave * 16 + 4 * (lane >> 4);
-            const f32x4 sc = *reinterpret_cast<const f32x4*>(&par[0][ch0]);
-            const f32x4 bi = *reinterpret_cast<const f32x4*>(&par[1][ch0]);
-            const int oh0 = 2 * cur.ph0 - 1, ow0 = 2 * cur.pw0 - 1;
-#pragma unroll
-            for (int r = 0; r < SP_ROWS; ++r) {
-                const bool rin = (unsigned)(oh0 + r) < (unsigned)p.Ho;
-#pragma unroll
-                for (int q = 0; q < SP_PXT; ++q) {
-                    const int px = q * 16 + (lane & 15);
-                    const bool in = rin && (unsigned)(ow0 + px) < (unsigned)p.Wo;
-                    float v[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) v[i] = in ? fmaxf(acc[r][q][i] * sc[i] + bi[i], 0.f) : 0.f;
-                    uint32_t w[2];
-#pragma unroll
-                    for (int i = 0; i < 2; ++i)
-                        w[i] = (uint32_t)__builtin_bit_cast(uint16_t, Cvt<T>::from(v[2 * i])) |
-                               ((uint32_t)__builtin_bit_cast(uint16_t, Cvt<T>::from(v[2 * i + 1])) << 16);
-                    const int chunk = (ch0 >> 3) ^ (px & 7);
-                    uint32_t* dst = reinterpret_cast<uint32_t*>(lds + (r * SP_PX + px) * (SK_CO * 2) + chunk * 16 + (ch0 & 4) * 2);
-                    dst[0] = w[0];
-                    dst[1] = w[1];
-                }
-            }
-        }
-        // the next tile's image rows load under the pooling (issued once the accumulators are
-        // parked: their 36 registers would not fit beside them)
-        if (tn < ntiles) load_in(nxt);
-        __syncthreads();
-        // pool: 2 rows x 32 columns x 8 chunks of 8 channels; pooled (j, pw) = max over conv rows
-        // 2j .. 2j+2 and tile pixels 2 pw .. 2 pw + 2
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int idx = i * 256 + tid;
-            const int j = idx >> 8, rem = idx & 255;
-            const int pw = rem >> 3, c16 = rem & 7;
-            float m[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) m[e] = 0.f;
-#pragma unroll
-            for (int dr = 0; dr < 3; ++dr)
-#pragma unroll
-                for (int dc = 0; dc < 3; ++dc) {
-                    const int r = 2 * j + dr, px = 2 * pw + dc;
-                    const u32x4 v = *reinterpret_cast<const u32x4*>(lds + (r * SP_PX + px) * (SK_CO * 2) + ((c16 ^ (px & 7)) * 16));
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        m[2 * e] = fmaxf(m[2 * e], to_f32(__builtin_bit_cast(T, (uint16_t)(v[e] & 0xffffu))));
-                        m[2 * e + 1] = fmaxf(m[2 * e + 1], to_f32(__builtin_bit_cast(T, (uint16_t)(v[e] >> 16))));
-                    }
-                }
-            const int ph = cur.ph0 + j, pwg = cur.pw0 + pw;
-            if (ph < Hp && pwg < Wp) {
-                u32x4 o;
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    o[e] = (uint32_t)__builtin_bit_cast(uint16_t, Cvt<T>::from(m[2 * e])) |
-                           ((uint32_t)__builtin_bit_cast(uint16_t, Cvt<T>::from(m[2 * e + 1])) << 16);
-                *reinterpret_cast<u32x4*>(Y + ((long)(cur.n * Hp + ph) * Wp + pwg) * SK_CO + c16 * 8) = o;
-            }
-        }
-        __syncthreads();
-        cur = nxt;
-    }
-}
-
 }  // namespace
 
 // Entry from gemm.hip's conv dispatcher (false = not the stem geometry): the 7 x 1 conv with
@@ -624,36 +414,6 @@ extern "C" int kinet_stem_conv_image(const float* img, const void* w_packed, con
         hipLaunchKernelGGL((stem_img_kernel<bf16_t>), dim3(grid), dim3(256), 0, s, a, tiles_x, tiles_y, (int)nt);
     else
         hipLaunchKernelGGL((stem_img_kernel<f16_t>), dim3(grid), dim3(256), 0, s, a, tiles_x, tiles_y, (int)nt);
-    KINET_LAUNCH_CHECK();
-    return KINET_OK;
-}
-
-// torchvision conv1 + bn1 + relu + maxpool (3x3 / 2, pad 1) from the f32 NCHW image in one
-// launch -- include/kinet_gemm.h
-extern "C" int kinet_stem_pool_image(const float* img, const void* w_packed, const float* scale, const float* bias,
-                                     void* Y, int N, int H, int W, int dtype, kinet_stream_t stream) {
-    KINET_CHECK_ARG(N >= 0 && H > 0 && W > 0, "stem_pool_image: bad geometry");
-    KINET_CHECK_ARG(dtype == KINET_BF16 || dtype == KINET_F16, "stem_pool_image: dtype must be bf16 or f16");
-    KINET_CHECK_ARG(img && w_packed && Y, "stem_pool_image: NULL argument");
-    KINET_CHECK_ARG((((uintptr_t)Y) & 15u) == 0 && (((uintptr_t)w_packed) & 15u) == 0, "stem_pool_image: Y and weights must be 16-byte aligned");
-    if (N == 0) return KINET_OK;
-    const long long ib = (long long)N * 3 * H * W * 4;
-    KINET_CHECK_ARG(ib < (1LL << 31), "stem_pool_image: image batch larger than 2 GiB (split the call)");
-    StemImgArgs a{};
-    a.img = img; a.W = w_packed; a.scale = scale; a.bias = bias; a.Y = Y;
-    a.N = N; a.H = H; a.W_ = W; a.Ho = (H - 1) / 2 + 1; a.Wo = (W - 1) / 2 + 1; a.ldy = SK_CO;
-    a.img_bytes = (int)ib;
-    a.w_bytes = SK_CO * SK_KH * SK_CG * 2;
-    const int Hp = (a.Ho - 1) / 2 + 1, Wp = (a.Wo - 1) / 2 + 1;
-    const int tiles_x = (Wp + 31) / 32, tiles_y = (Hp + 1) / 2;
-    const long long nt = (long long)tiles_x * tiles_y * N;
-    KINET_CHECK_ARG(nt < (1LL << 31), "stem_pool_image: too many tiles");
-    const int grid = nt < 512 ? (int)nt : 512;
-    hipStream_t s = (hipStream_t)stream;
-    if (dtype == KINET_BF16)
-        hipLaunchKernelGGL((stem_pool_kernel<bf16_t>), dim3(grid), dim3(256), 0, s, a, tiles_x, tiles_y, (int)nt);
-    else
-        hipLaunchKernelGGL((stem_pool_kernel<f16_t>), dim3(grid), dim3(256), 0, s, a, tiles_x, tiles_y, (int)nt);
     KINET_LAUNCH_CHECK();
     return KINET_OK;
 }

@@ -137,6 +137,8 @@ def linear(x, weight, bias=None, relu=False, residual=None, row_mask=None, out_d
     N.require_gpu(x)
     K = x.shape[-1]
     lead = x.shape[:-1]
+    if x_add is not None and x_add.dim() == x.dim() and x_add.shape != x.shape:
+        x_add = x_add.expand(x.shape)   # a frame-shared operand (forward_flat's unpadded pos)
     x2 = x.reshape(-1, K)
     kp = (-K) % 8
     if kp:
@@ -410,48 +412,6 @@ def stem_conv_image(img, w_packed, scale, bias, dtype):
     return y
 
 
-def stem_pool_image(img, w_packed, scale, bias, dtype):
-    """ResNet stem + max-pool in one launch from the f32 NCHW image (kinet_stem_pool_image):
-    (B, 3, H, W) -> (B, Hp, Wp, 64) NHWC, Hp = ((H-1)//2)//2 + 1, the conv map never stored."""
-    img = img.float().contiguous()
-    N.require_gpu(img)
-    B, C, H, W = img.shape
-    if C != 3:
-        raise RuntimeError('stem_pool_image expects 3-channel images')
-    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
-    Hp, Wp = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
-    y = torch.empty((B, Hp, Wp, 64), dtype=dtype, device=img.device)
-    work = {'family': 'conv', 'flops': 2.0 * B * Ho * Wo * 64 * 147, 'shape': ('stem_pool', B, H, W),
-            'bytes': B * 3 * H * W * 4 + B * Hp * Wp * 64 * y.element_size()}
-    N.call('kinet_stem_pool_image', N.ptr(img), N.ptr(w_packed), N.ptr(f32(scale)), N.ptr(f32(bias)), N.ptr(y),
-           B, H, W, N.dtype_code(dtype), N.stream(img.device), work=work)
-    return y
-
-
-def pool_conv1x1_pair(x, w1, s1, b1, wds, sds, bds):
-    """maxpool 3x3/2 of the stem output x (B, Ho, Wo, 64) NHWC, then layer1[0].conv1 (w1 (64, 64,
-    1, 1), folded bn1 s1/b1, ReLU) and layer1[0].downsample (wds (256, 64, 1, 1), folded BN) in one
-    launch (kinet_pool_conv1x1_pair) -> (t1 (B, Hp, Wp, 64), identity (B, Hp, Wp, 256))."""
-    N.require_gpu(x)
-    B, Ho, Wo, C = x.shape
-    if C != 64 or not x.is_contiguous():
-        raise RuntimeError('pool_conv1x1_pair: x must be a contiguous (B, Ho, Wo, 64) tensor')
-    Hp, Wp = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
-    wcat = cached_multi([w1, wds], ('pool_pair_w', x.dtype),
-                        lambda a, b: torch.cat([a.detach().reshape(64, 64), b.detach().reshape(256, 64)]).to(x.dtype).contiguous())
-    sc = cached_multi([s1, sds], ('pool_pair_s',), lambda a, b: torch.cat([f32(a), f32(b)]).contiguous())
-    bi = cached_multi([b1, bds], ('pool_pair_b',), lambda a, b: torch.cat([f32(a), f32(b)]).contiguous())
-    t1 = torch.empty((B, Hp, Wp, 64), dtype=x.dtype, device=x.device)
-    idn = torch.empty((B, Hp, Wp, 256), dtype=x.dtype, device=x.device)
-    M = B * Hp * Wp
-    e = x.element_size()
-    work = {'family': 'conv', 'flops': 2.0 * M * 320 * 64, 'shape': ('pool_pair', M),
-            'bytes': (B * Ho * Wo * 64 + M * 320) * e}
-    N.call('kinet_pool_conv1x1_pair', N.ptr(x), N.ptr(wcat), N.ptr(sc), N.ptr(bi), N.ptr(t1), N.ptr(idn), B, Ho, Wo,
-           N.dtype_code(x.dtype), N.stream(x.device), work=work)
-    return t1, idn
-
-
 def bottleneck_pack(w3, w1, s3, s1, dtype):
     """kinet_bottleneck_pack of conv3 (F, D, 1, 1) and the next block's conv1 (DB, F, 1, 1) with
     their FrozenBN scales folded in, cached per parameter version."""
@@ -705,54 +665,19 @@ def encoder_tile_order(shapes, device, qt=16):
     return o
 
 
-# column panels per strip of the encoder's tile order (strip_panel_order); 1 = row sweeps
-ENC_PANELS = [1]
-_panel_orders = {}
-
-
-def strip_panel_order(order, shapes, nstrip, panels, qt=16):
-    """The encoder tile order `order` (encoder_tile_order: tiles sorted by normalised row)
-    re-sorted WITHIN each strip of the strip kernel's plan -- the contiguous slices
-    [s*n/nstrip, (s+1)*n/nstrip) of the order, one per workgroup of a head map -- by
-    (column panel, row): a strip walks `panels` vertical panels one after another instead of
-    sweeping whole rows.  Every strip keeps the same set of tiles (so the same staged LDS rows,
-    msda_enc.hip strip_rows) and any order gives the same per-query results; what changes is the
-    reuse distance of the texture-gathered levels' rows in L2 (a row of level 0 is reused by the
-    tiles a few rows away, 1/panels of a row sweep later).  Cached per (order, nstrip, panels)."""
-    if panels <= 1 or nstrip < 1 or order is None:
-        return order
-    key = (tuple(tuple(int(v) for v in s) for s in shapes), order.data_ptr(), int(nstrip), int(panels))
-    o = _panel_orders.get(key)
-    if o is None:
-        import numpy as np
-        base = order.cpu().numpy().astype(np.int64)
-        hw = np.array([h * w for h, w in key[0]], dtype=np.int64)
-        starts = np.concatenate([[0], np.cumsum(hw)[:-1]])
-        q = base * qt
-        lvl = np.searchsorted(starts, q, side='right') - 1
-        H = np.array([h for h, _ in key[0]], dtype=np.float64)[lvl]
-        W = np.array([w for _, w in key[0]], dtype=np.int64)[lvl]
-        r = q - starts[lvl]
-        y = (r // W + 0.5) / H
-        x = (r % W + 0.5) / W
-        pan = np.minimum((x * panels).astype(np.int64), panels - 1)
-        n = base.size
-        out = np.empty_like(base)
-        for st in range(nstrip):
-            t0, t1 = st * n // nstrip, (st + 1) * n // nstrip
-            idx = np.lexsort((np.arange(t1 - t0), y[t0:t1], pan[t0:t1]))
-            out[t0:t1] = base[t0:t1][idx]
-        o = torch.as_tensor(out.astype(np.int32), device=order.device)
-        _panel_orders[key] = (o, order)   # keep the base alive: its data_ptr is part of the key
-    else:
-        o = o[0]
-    return o
-
-
 _host_shapes = {}
 _enc_plans = {}
 # template-argument spelling of the element types in rocprofv3 kernel names
 _KT = {torch.bfloat16: 'kinet::bf16_t', torch.float16: 'kinet::f16_t', torch.float32: 'float', torch.float64: 'double'}
+
+
+def msda_encoder_set_strips(strips):
+    """Strips per head map for the encoder sampler on the calling thread (0 = the plan's own
+    choice; kinet_msda_encoder_set_strips, A/B tooling).  The cached plans are dropped, so
+    msda_encoder_plan reports what the next launch runs.  Returns the previous value."""
+    old = N.lib().kinet_msda_encoder_set_strips(int(strips))
+    _enc_plans.clear()
+    return old
 
 
 def msda_encoder_plan(shapes, batch, n_heads, Lq, channels=32):
@@ -811,8 +736,6 @@ def msda_encoder_split(value, shapes, offlog_hm, reference_points, n_heads, quer
     offlog_hm = offlog_hm.contiguous()
     nsamp = B * Lq * M_ * 16
     plan = msda_encoder_plan(key, B, M_, Lq, 36)
-    if plan and query_tile_order is not None:
-        query_tile_order = strip_panel_order(query_tile_order, key, plan[1], ENC_PANELS[0])
     kname = 'msda_enc_kernel<%s, %d, %d, %s, false, true, 12>' % (_KT[od], plan[0] if plan else -1, ref.shape[-1],
                                                                   'true' if qm is not None else 'false')
     N.call('kinet_msda_encoder_forward_split', N.ptr(main), main.stride(1), main.stride(0), N.ptr(tail),
@@ -838,6 +761,29 @@ def msda_encoder_supported(value, shapes, Lq, n_heads, n_levels, n_points, batch
     return value.data_ptr() % 16 == 0 and value.stride(1) % 8 == 0 and value.stride(0) % 8 == 0
 
 
+def _load_add_operand(x2, x_add, B, Lq, K):
+    """(x2, a2, a2_rows) for a GEMM over x2 = x.reshape(B*Lq, K) rows with x_add added at load:
+    an x_add of ONE frame (1, Lq, K) for a batch of B > 1 frames stays one frame in memory and
+    every frame's rows read it (a2_rows = Lq: the unpadded batch's shared position embedding,
+    deformable_transformer.py forward_flat) -- else x_add has x's rows and layout."""
+    if x_add is None:
+        return x2, None, 0
+    if x_add.shape[0] == 1 and B > 1 and Lq >= 32:
+        if x2.stride(-1) != 1 or x2.stride(0) != K or x2.data_ptr() % 16:
+            x2 = x2.contiguous()
+        a2 = x_add.reshape(Lq, K)
+        if a2.stride() != x2.stride() or a2.data_ptr() % 16:
+            a2 = a2.contiguous()
+        return x2, a2, Lq
+    if x_add.shape[0] != B:
+        x_add = x_add.expand(B, Lq, K)
+    a2 = x_add.reshape(B * Lq, K)
+    if x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16 or a2.stride() != x2.stride() or \
+            a2.data_ptr() % 16:
+        x2, a2 = x2.contiguous(), a2.contiguous()
+    return x2, a2, 0
+
+
 def offsets_proj_headmajor(x, weight, bias, heads, x_add=None, out_dtype=torch.float16):
     """The MSDA offsets + logits projection (x [+ x_add]) @ W^T + b stored head-major
     (heads, B, Lq, Nout/heads): W's rows must already be grouped per head
@@ -845,21 +791,20 @@ def offsets_proj_headmajor(x, weight, bias, heads, x_add=None, out_dtype=torch.f
     N.require_gpu(x)
     B, Lq, K = x.shape
     x2 = x.reshape(B * Lq, K)
-    a2 = x_add.reshape(B * Lq, K) if x_add is not None else None
-    if x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16 or \
-            (a2 is not None and (a2.stride() != x2.stride() or a2.data_ptr() % 16)):
+    if x_add is None and (x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16):
         x2 = x2.contiguous()
-        a2 = a2.contiguous() if a2 is not None else None
+    x2, a2, a2_rows = _load_add_operand(x2, x_add, B, Lq, K)
     w = weight_as(weight, x.dtype)
     Nout = w.shape[0]
     rec = Nout // heads
     out = torch.empty((heads, B, Lq, rec), dtype=out_dtype, device=x.device)
     e = x.element_size()
     N.call('kinet_gemm_headmajor_ex', N.ptr(x2), N.ptr(a2), N.ptr(w), N.ptr(out), B * Lq, Nout, K, x2.stride(0), K,
-           N.dtype_code(x.dtype), N.dtype_code(out_dtype), N.ptr(f32(bias)), None, Lq, rec, N.stream(x.device),
+           N.dtype_code(x.dtype), N.dtype_code(out_dtype), N.ptr(f32(bias)), None, Lq, rec, a2_rows,
+           N.stream(x.device),
            work={'family': 'gemm', 'flops': 2.0 * B * Lq * Nout * K, 'shape': (B * Lq, Nout, K),
                  'role': 'msda_prep',
-                 'bytes': (B * Lq * K * (2 if a2 is not None else 1) + Nout * K) * e + B * Lq * Nout * 2})
+                 'bytes': (B * Lq * K + (0 if a2 is None else a2.shape[0] * K) + Nout * K) * e + B * Lq * Nout * 2})
     return out
 
 
@@ -884,8 +829,6 @@ def msda_encoder(value, shapes, offlog_hm, reference_points, n_heads, query_attn
     offlog_hm = offlog_hm.contiguous()
     nsamp = B * Lq * M_ * 16
     plan = msda_encoder_plan(key, B, M_, Lq)
-    if plan and query_tile_order is not None:
-        query_tile_order = strip_panel_order(query_tile_order, key, plan[1], ENC_PANELS[0])
     # the instantiation kinet_msda_encoder_forward launches (as rocprofv3 names it)
     kname = 'msda_enc_kernel<%s, %d, %d, %s>' % (_KT[od], plan[0] if plan else -1, ref.shape[-1],
                                                    'true' if qm is not None else 'false')
@@ -927,11 +870,9 @@ def msda_sample_records(x, weight, bias, heads, reference_points, shapes_host, x
     N.require_gpu(x)
     B, Lq, K_ = x.shape
     x2 = x.reshape(B * Lq, K_)
-    a2 = x_add.reshape(B * Lq, K_) if x_add is not None else None
-    if x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16 or \
-            (a2 is not None and (a2.stride() != x2.stride() or a2.data_ptr() % 16)):
+    if x_add is None and (x2.stride(-1) != 1 or (x2.stride(0) % 8) or x2.data_ptr() % 16):
         x2 = x2.contiguous()
-        a2 = a2.contiguous() if a2 is not None else None
+    x2, a2, a2_rows = _load_add_operand(x2, x_add, B, Lq, K_)
     w = weight_as(weight, x.dtype)
     key = tuple(tuple(int(v) for v in s) for s in shapes_host)
     hs = _host_shapes.get(key)
@@ -944,11 +885,11 @@ def msda_sample_records(x, weight, bias, heads, reference_points, shapes_host, x
     e = x.element_size()
     N.call('kinet_msda_sample_records', N.ptr(x2), N.ptr(a2), N.ptr(w), N.ptr(f32(bias)), B * Lq, heads, K_,
            x2.stride(0), N.dtype_code(x.dtype), N.ptr(ref), ref.shape[-1], N.ptr(qm), N.ptr(hs), 4, 4, fb, N.ptr(rec),
-           N.stream(x.device),
+           a2_rows, N.stream(x.device),
            work={'family': 'gemm', 'flops': 2.0 * B * Lq * heads * 48 * K_, 'shape': (B * Lq, heads * 48, K_),
                  'role': 'msda_prep',
-                 'bytes': (B * Lq * K_ * (2 if a2 is not None else 1) + heads * 48 * K_) * e + ref.numel() * 4
-                 + rec.numel() * 4})
+                 'bytes': (B * Lq * K_ + (0 if a2 is None else a2.shape[0] * K_) + heads * 48 * K_) * e
+                 + ref.numel() * 4 + rec.numel() * 4})
     return rec, fb
 
 
@@ -970,8 +911,6 @@ def msda_encoder_records(value, shapes, records, frac_bits, out_dtype=None, quer
     records = records.contiguous()
     nsamp = B * Lq * M_ * 16
     plan = msda_encoder_plan(key, B, M_, Lq)
-    if plan and query_tile_order is not None:
-        query_tile_order = strip_panel_order(query_tile_order, key, plan[1], ENC_PANELS[0])
     kname = 'msda_enc_kernel<%s, %d, 2, false, true>' % (_KT[od], plan[0] if plan else -1)
     N.call('kinet_msda_encoder_forward_records', N.ptr(value), value.stride(1), value.stride(0), N.ptr(hs),
            N.ptr(records), int(frac_bits), N.ptr(out), B, S, M_, D, 4, Lq, 4, N.dtype_code(od),

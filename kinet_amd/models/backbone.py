@@ -61,11 +61,6 @@ FUSE_PAIR_WIDTHS = (64,)
 # 16-bit stem straight from the f32 image (kinet_stem_conv_image); False: pack_image_kwfold +
 # the folded conv (A/B: bench.py --stem-image 0)
 STEM_FROM_IMAGE = True
-# ... and the max-pool fused into it (kinet_stem_pool_image; A/B: bench.py --stem-pool 0)
-STEM_POOL = False
-# max-pool + layer1[0].conv1 + layer1[0].downsample in one launch (kinet_pool_conv1x1_pair):
-# measured 1.4 % slower than the three kernels in the bench, off by default
-POOL_PAIR = False
 
 
 def conv_bn(x, conv, bn, relu, residual=None, cin_pad=None):
@@ -116,23 +111,19 @@ def _pair_ok(dtype, blk, nxt):
             and K.bottleneck_pair_supported(dtype, blk.conv3.weight, nxt.conv1.weight))
 
 
-def forward_layer_nhwc(layer, x, t1=None, next_block=None, identity0=None):
+def forward_layer_nhwc(layer, x, t1=None, next_block=None):
     """One ResNet stage over NHWC x -> (stage output, next_block's conv1 output or None).
     With FUSE_BOTTLENECK_PAIRS the chain conv3 (+ residual + ReLU) of block i -> conv1 of block
     i+1 runs as one kinet_bottleneck_pair launch: the block output is written once (the next
     block's residual) and not re-read by the next conv1.  `next_block` (the next stage's first
     block) extends the chain across the stage boundary where the pair kernel covers it (stage 1
     -> 2: its conv1 is stride 1); `t1` = this stage's first conv1 output when the previous stage
-    computed it, `identity0` its first block's downsample output (then x is not read).  Same
-    math as Bottleneck.forward_nhwc per block (torchvision, backbone.py:102)."""
+    computed it.  Same math as Bottleneck.forward_nhwc per block (torchvision, backbone.py:102)."""
     blocks = list(layer)
     b0 = blocks[0]
     if t1 is None:
         t1 = conv_bn(x, b0.conv1, b0.bn1, True)
-    if identity0 is not None:
-        identity = identity0
-    else:
-        identity = x if b0.downsample is None else conv_bn(x, b0.downsample[0], b0.downsample[1], False)
+    identity = x if b0.downsample is None else conv_bn(x, b0.downsample[0], b0.downsample[1], False)
     t_next = None
     for i, blk in enumerate(blocks):
         t2 = conv_bn(t1, blk.conv2, blk.bn2, True)
@@ -221,27 +212,14 @@ class ResNetBody(nn.Module):
         kh, kw = c1.kernel_size
         cg = (3 * kw + 7) // 8 * 8
         scale, bias = self.bn1.folded()
-        if STEM_FROM_IMAGE and STEM_POOL and dtype in (torch.bfloat16, torch.float16):
-            # conv1 + bn1 + relu + maxpool in one launch from the f32 image (conv map never stored)
-            x = K.stem_pool_image(img_nchw, K.pack_stem_weight(c1.weight, dtype, cg), scale, bias, dtype)
+        if STEM_FROM_IMAGE and dtype in (torch.bfloat16, torch.float16):
+            # the folded rows built in LDS from the f32 image (no packed copy of the image)
+            x = K.stem_conv_image(img_nchw, K.pack_stem_weight(c1.weight, dtype, cg), scale, bias, dtype)
         else:
-            if STEM_FROM_IMAGE and dtype in (torch.bfloat16, torch.float16):
-                # the folded rows built in LDS from the f32 image (no packed copy of the image)
-                x = K.stem_conv_image(img_nchw, K.pack_stem_weight(c1.weight, dtype, cg), scale, bias, dtype)
-            else:
-                x = K.pack_image_kwfold(img_nchw, dtype, kw, c1.stride[1], c1.padding[1], cg)
-                x = K.conv2d_nhwc(x, K.pack_stem_weight(c1.weight, dtype, cg), (c1.stride[0], 1),
-                                  (c1.padding[0], 0), scale=scale, bias=bias, relu=True)
-            b0 = self.layer1[0]
-            if (POOL_PAIR and dtype in (torch.bfloat16, torch.float16) and b0.downsample is not None
-                    and tuple(b0.conv1.weight.shape) == (64, 64, 1, 1)
-                    and tuple(b0.downsample[0].weight.shape) == (256, 64, 1, 1) and b0.downsample[0].stride == (1, 1)):
-                # maxpool + layer1[0].conv1 + layer1[0].downsample in one launch (pooled map not stored)
-                s1, bb1 = b0.bn1.folded()
-                sd, bd = b0.downsample[1].folded()
-                t1, idn = K.pool_conv1x1_pair(x, b0.conv1.weight, s1, bb1, b0.downsample[0].weight, sd, bd)
-                return forward_layer_nhwc(self.layer1, None, t1, next_block, identity0=idn)
-            x = K.maxpool_3x3s2(x)
+            x = K.pack_image_kwfold(img_nchw, dtype, kw, c1.stride[1], c1.padding[1], cg)
+            x = K.conv2d_nhwc(x, K.pack_stem_weight(c1.weight, dtype, cg), (c1.stride[0], 1),
+                              (c1.padding[0], 0), scale=scale, bias=bias, relu=True)
+        x = K.maxpool_3x3s2(x)
         return forward_layer_nhwc(self.layer1, x, None, next_block)
 
     def forward(self, x):
@@ -349,18 +327,28 @@ class Joiner(nn.Sequential):
     def _pos(self, x):
         """The position embedding of level x (a function of its padding mask only).  When the mask
         is fully determined by the image sizes (NestedTensor.sizes), the embedding is cached per
-        (sizes, level shape, dtype, device): the training path's op-for-op forward otherwise
-        recomputes 2 x 4 levels x frames of it per step."""
+        (sizes, batch, level height / width, dtype, device) -- not per channel count, which it does
+        not depend on -- in a small LRU: the training path's op-for-op forward otherwise
+        recomputes 2 x 4 levels x frames of it per step, and multi-scale training cycles through
+        geometries, so the least recently used entry goes first."""
         if x.sizes is None:
             return self[1](x).to(x.tensors.dtype)
-        key = (x.sizes, tuple(x.tensors.shape), x.tensors.dtype, str(x.tensors.device))
-        cache = self.__dict__.setdefault('_pos_cache', {})
+        t = x.tensors
+        key = (x.sizes, t.shape[0], t.shape[-2], t.shape[-1], t.dtype, str(t.device))
+        cache = self.__dict__.get('_pos_cache')
+        if cache is None:
+            from collections import OrderedDict
+            cache = self.__dict__['_pos_cache'] = OrderedDict()
         p = cache.get(key)
         if p is None:
-            if len(cache) >= 16:
-                cache.clear()
-            p = cache[key] = self[1](x).to(x.tensors.dtype)
+            p = cache[key] = self[1](x).to(t.dtype)
+            while len(cache) > self.POS_CACHE_ENTRIES:
+                cache.popitem(last=False)
+        else:
+            cache.move_to_end(key)
         return p
+
+    POS_CACHE_ENTRIES = 8
 
 
 def build_backbone(args):

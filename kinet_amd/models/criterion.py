@@ -172,6 +172,10 @@ class SetCriterion(nn.Module):
         return [[(next(it), next(it)) for _ in per_set] for per_set in host]
 
     deferred_checks = None
+    # opt-in (the training step sets it around its criterion call): collect the GIoU
+    # degenerate-box flags instead of asserting them in loss_boxes; every other caller keeps
+    # the reference's immediate assert (util/box_ops.py:44-45)
+    defer_box_checks = False
 
     def pop_deferred_checks(self):
         """The GIoU degenerate-box flags of the last forward as one device bool (None if none):
@@ -181,7 +185,7 @@ class SetCriterion(nn.Module):
         return torch.stack(c).all() if c else None
 
     def forward(self, outputs, targets):
-        self.deferred_checks = []
+        self.deferred_checks = [] if self.defer_box_checks else None
         outputs_without_aux = {k: v for k, v in outputs.items() if k != 'aux_outputs'}
         aux = list(outputs.get('aux_outputs', []))
         all_indices = self.match([outputs_without_aux] + aux, targets)

@@ -439,16 +439,22 @@ class DeformableTransformer(nn.Module):
                     ref.unsqueeze(0).expand(bs, -1, -1).contiguous())
         return K.cached_multi([query_embed, rp.weight, rp.bias], ('query_inputs', bs, dt), make)
 
+    share_frame_pos = True   # forward_flat: unpadded frames read one shared position embedding (A/B, tests)
+
     def forward_flat(self, src_flatten, lvl_pos_embed_flatten, geo, query_embed=None, targets=None):
         """deformable_transformer.py:159-257 on flattened inputs."""
         assert query_embed is not None
         pad = geo['pad_mask']
+        # no frame padded: every frame's position embedding is the same function of the level
+        # shapes, so the encoder's projections read frame 0's rows for all frames (x_add of one
+        # frame, kernels._load_add_operand) -- the same values, 1/B of the bytes
+        pos_shared = self.share_frame_pos and fast_path(self) and pad is None and src_flatten.shape[0] > 1
         encs = []
         for e in geo['enc']:
             tok = e['tok']
             pm = pad[:, tok] if pad is not None else None
             src = src_flatten[:, tok]
-            pos = lvl_pos_embed_flatten[:, tok]
+            pos = lvl_pos_embed_flatten[:1, tok] if pos_shared else lvl_pos_embed_flatten[:, tok]
             if fast_path(self):
                 src, pos = src.contiguous(), pos.contiguous()
                 pm = pm.contiguous() if pm is not None else None

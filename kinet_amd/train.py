@@ -65,7 +65,14 @@ def reduce_dict(input_dict, average=True):
 def train_step(model, criterion, optimizer, samples, targets, clip_max_norm=0.1):
     """One optimisation step (engine.py:124-149).  Returns (weighted loss, loss_dict)."""
     outputs, targets, *_ = model(samples, targets)
-    loss_dict = criterion(outputs, targets)
+    defer = hasattr(criterion, 'pop_deferred_checks')
+    if defer:
+        criterion.defer_box_checks = True
+    try:
+        loss_dict = criterion(outputs, targets)
+    finally:
+        if defer:
+            criterion.defer_box_checks = False
     losses = weighted_loss(loss_dict, criterion.weight_dict)
     # one host read for the loss-finiteness check (engine.py:131-134) and the criterion's GIoU
     # degenerate-box asserts (util/box_ops.py:44-45, deferred to here)
@@ -117,13 +124,16 @@ def synthetic_mot_batch(batch, height, width, device, generator, num_boxes=(10, 
     return nested_tensor_from_tensor_list(samples), targets
 
 
-def setup_ddp(model, device):
-    """train.py:84-91: DistributedDataParallel over the RCCL process group (env:// rendezvous)."""
+def setup_ddp(model, device, find_unused_parameters=True):
+    """train.py:84-91: DistributedDataParallel over the RCCL process group (env:// rendezvous).
+    find_unused_parameters=True is the reference's setting (train.py:89-91); every parameter of
+    this model receives a gradient in the two-pass step, so False skips DDP's extra traversal of
+    the autograd graph per step without changing the result (bench.py --ddp-find-unused 0)."""
     if not (dist.is_available() and dist.is_initialized()):
         return model
     local = int(os.environ.get('LOCAL_RANK', '0'))
     return torch.nn.parallel.DistributedDataParallel(model, device_ids=[local] if device.type == 'cuda' else None,
-                                                     find_unused_parameters=True)
+                                                     find_unused_parameters=find_unused_parameters)
 
 
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -166,7 +176,7 @@ def train_rooflines(trace):
 
 
 def benchmark_train(steps=10, warmup=2, batch=2, height=800, width=1333, prev_dtype=torch.bfloat16, device=None,
-                    dropout=None, matmul_precision='high'):
+                    dropout=None, matmul_precision='high', find_unused_parameters=True):
     """Config-4 training throughput (BASELINE.json configs[3], cfgs/train_mot17.yaml: `mot17
     deformable multi_frame tracking`, d=288, 500 queries, two-pass track-query training,
     focal + L1 + GIoU with aux losses, AdamW, clip 0.1) on synthetic (current, prev) frame
@@ -180,12 +190,14 @@ def benchmark_train(steps=10, warmup=2, batch=2, height=800, width=1333, prev_dt
     prev_prec = torch.get_float32_matmul_precision()
     torch.set_float32_matmul_precision(matmul_precision)
     try:
-        return _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dropout, matmul_precision)
+        return _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dropout, matmul_precision,
+                                find_unused_parameters)
     finally:
         torch.set_float32_matmul_precision(prev_prec)
 
 
-def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dropout, matmul_precision):
+def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dropout, matmul_precision,
+                     find_unused_parameters=True):
     import statistics
     import time
     from kinet_amd.models import build_model
@@ -199,7 +211,7 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
     model, criterion, _ = build_model(args)
     model = model.to(dev).train()
     model.set_compute_dtype(prev_dtype)
-    ddp = setup_ddp(model, dev)
+    ddp = setup_ddp(model, dev, find_unused_parameters)
     opt = build_optimizer(ddp, args)
     g = torch.Generator().manual_seed(1000 + rank)
     samples, targets = synthetic_mot_batch(batch, height, width, dev, g)
@@ -266,6 +278,7 @@ def _benchmark_train(steps, warmup, batch, height, width, prev_dtype, device, dr
     pg = 'none (single process)'
     if world >= 1 and dist.is_available() and dist.is_initialized():
         pg = f'ddp{world}: DistributedDataParallel over a {world}-rank {dist.get_backend()} process group'
+        pg += ', find_unused_parameters=%s' % find_unused_parameters
         if dist.get_backend() == 'nccl':
             pg += ' (RCCL all-reduce)'
     return {'metric': 'train frames/sec (config 4: mot17 deformable multi_frame tracking, 3x%dx%d pairs)'

@@ -7,11 +7,14 @@ frames are regenerated here from CPU generator seeds, so only outputs are commit
       - HIP fp32 vs reference: pred_logits / pred_boxes / hs_embed / aux / memory within
         1e-3 abs (the BASELINE north_star gate).
       - HIP bf16 (the mode bench.py times) vs HIP fp32, per-tensor max-abs bounds BF16_TOL.
+      - HIP bf16 vs the REFERENCE's outputs directly (closing the chain timed kernels ->
+        reference): within BF16_TOL + 1e-3 per tensor (the fp32 gate plus the 16-bit bound).
   * config 5 (cfgs/train_full_res.yaml: ResNet-101, d=288, 500 queries, separate
     per-frame encoders, 8-level decoder, tracking step with prev_features + K track
     queries): at 96x128 and at 1080x1920.
       - HIP fp32 vs reference within 1e-3 abs, both frames of the step.
-      - HIP fp16 (the config's compute dtype) vs HIP fp32, per-tensor bounds F16_TOL.
+      - HIP fp16 (the config's compute dtype) vs HIP fp32, per-tensor bounds F16_TOL, and vs
+        the reference's outputs within F16_TOL + 1e-3.
 """
 import os
 
@@ -107,6 +110,28 @@ def test_config2_full_bf16_vs_fp32(config2_full):
     assert torch.isfinite(got['pred_boxes']).all() and (got['pred_boxes'] >= 0).all() and (got['pred_boxes'] <= 1).all()
 
 
+def _vs_reference(out, d, prefix=''):
+    """max / mean |HIP - reference| per tensor against the fixture."""
+    r = {}
+    for k in ('pred_logits', 'pred_boxes', 'hs_embed'):
+        diff = np.abs(out[k].float().cpu().numpy() - d[k + prefix])
+        r[k] = (float(diff.max()), float(diff.mean()))
+    return r
+
+
+def test_config2_full_bf16_vs_reference(config2_full):
+    """The timed bf16 path (records sampler, bf16 GEMM / conv kernels, 1/256-px sampling
+    locations) against the reference model's own fp32 outputs at 800x1333: per-tensor max |diff|
+    within BF16_TOL + TOL (the bf16-vs-HIP-fp32 bound plus the fp32 gate)."""
+    d, model, img = config2_full
+    got = _fwd(model, [img], torch.bfloat16)[0]
+    r = _vs_reference(got, d)
+    print('[fullsize] config2 800x1333 bf16 vs reference: ' +
+          ' '.join(f'{k}=max {a:.4g} mean {m:.3g}' for k, (a, m) in r.items()))
+    for k, tol in BF16_TOL.items():
+        assert r[k][0] < tol + TOL, (k, r[k], tol + TOL)
+
+
 # ---------------------------------------------------------------------------------- config 5
 def _config5_model(golden_dir):
     model = _build(golden_dir, 'config5.keys.txt', 81, 'train_deformable', 'train_multi_frame', 'train_tracking',
@@ -148,3 +173,18 @@ def test_config5_full_fp16_vs_fp32(golden_dir, config5_model):
     _report('config5 1080x1920 fp16 vs HIP fp32', diffs)
     for k, tol in F16_TOL.items():
         assert diffs[k] < tol, (k, diffs[k], tol)
+
+
+def test_config5_full_fp16_vs_reference(golden_dir, config5_model):
+    """config 5's timed fp16 path against the reference model's fp32 outputs at 1080x1920
+    (both frames of the tracking step): within F16_TOL + TOL per tensor."""
+    d = dict(np.load(os.path.join(golden_dir, 'config5_full.npz')))
+    f0, f1 = _frame(5001, 1080, 1920).cuda(), _frame(5002, 1080, 1920).cuda()
+    top = torch.from_numpy(d['top_idx']).cuda()
+    out0, out1 = _config5_step(config5_model, f0, f1, top, torch.float16)
+    for tag, out, prefix in (('frame 0', out0, '0'), ('frame 1', out1, '')):
+        r = _vs_reference(out, d, prefix)
+        print(f'[fullsize] config5 1080x1920 fp16 vs reference, {tag}: ' +
+              ' '.join(f'{k}=max {a:.4g} mean {m:.3g}' for k, (a, m) in r.items()))
+        for k, tol in F16_TOL.items():
+            assert r[k][0] < tol + TOL, (tag, k, r[k], tol + TOL)

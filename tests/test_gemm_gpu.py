@@ -526,37 +526,6 @@ def test_rw288_ln_wave_variants(K, gemm_flags, M, N, mode, dtype):
     assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
 
 
-@pytest.mark.parametrize('case', ['plain', 'res_mask', 'f32', 'hm36', 'split'])
-def test_rw288_nine_wave_groups_bit_identical(K, gemm_flags, case):
-    """N <= 288 without LayerNorm on one 9-wave x 32-column group (flag 2097152) vs the 4-wave x
-    48-column groups: every output element is the same K-ordered MFMA chain -- bit for bit,
-    row-major, head-major (d = 36) and split-plane stores alike."""
-    dtype = torch.float16
-    if case in ('hm36', 'split'):
-        g = torch.Generator().manual_seed(31)
-        x = torch.randn(2, 4700, 288, generator=g).to(dtype).cuda()
-        w = (torch.randn(288, 288, generator=g) / 17).to(dtype).cuda()
-        b = torch.randn(288, generator=g).cuda()
-        mask = (torch.rand(2, 4700, generator=g) < 0.2).cuda()
-        if case == 'split':
-            ws, bs = K.split_value_weights(w, b, 8)
-            def run():
-                sv = K.value_proj_headmajor_split(x, ws, bs, 8, row_mask=mask)
-                return torch.cat([sv.main.reshape(-1), sv.tail.reshape(-1)])
-        else:
-            run = lambda: K.value_proj_headmajor(x, w, b, 36, row_mask=mask)
-    else:
-        M, N = {'plain': (8197, 288), 'res_mask': (12000, 280), 'f32': (4099, 200)}[case]
-        x, w, b, kw, _ = _rw_case(M, N, 288, case, 33, dtype)
-        run = lambda: K.linear(x.cuda(), w.cuda(), b.cuda(), **kw)
-    gemm_flags(0)
-    y4 = run().clone()
-    gemm_flags(2097152)
-    y9 = run().clone()
-    torch.cuda.synchronize()
-    assert torch.equal(y4, y9), (y4.float() - y9.float()).abs().max().item()
-
-
 @pytest.mark.parametrize('hd', [36, 48, 'split'])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
 def test_rw288_headmajor(K, hd, dtype):
@@ -991,85 +960,3 @@ def test_stem_conv_image_equals_folded_path(K, B, H, W, dtype):
     if H * W < 10 ** 6:
         ref = F.relu(F.conv2d(img, w, stride=2, padding=3) * scale[None, :, None, None] + bias[None, :, None, None])
         assert _rel(y1.permute(0, 3, 1, 2), ref) < 2e-2
-
-
-@pytest.mark.parametrize('B,H,W', [(2, 50, 66), (1, 37, 41), (2, 800, 1333), (1, 1080, 1920), (1, 9, 7), (1, 3, 130)])
-@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
-def test_stem_pool_image_equals_separate(K, B, H, W, dtype):
-    """kinet_stem_pool_image (conv1 + BN + ReLU + maxpool 3x3/2 in one launch; the conv map is
-    recomputed on tile halos and never stored) is bit-identical to kinet_stem_conv_image +
-    kinet_maxpool2d_3x3s2, incl. ragged pooled tiles and images smaller than one tile."""
-    g = torch.Generator().manual_seed(H * W + B + 7)
-    img = torch.randn(B, 3, H, W, generator=g)
-    w = torch.randn(64, 3, 7, 7, generator=g) * 0.1
-    scale = torch.rand(64, generator=g) + 0.5
-    bias = torch.randn(64, generator=g) * 0.1
-    wp = K.pack_stem_weight(w.cuda(), dtype, 24)
-    sep = K.maxpool_3x3s2(K.stem_conv_image(img.cuda(), wp, scale.cuda(), bias.cuda(), dtype))
-    fused = K.stem_pool_image(img.cuda(), wp, scale.cuda(), bias.cuda(), dtype)
-    torch.cuda.synchronize()
-    assert fused.shape == sep.shape
-    assert torch.equal(fused, sep)
-
-
-@pytest.mark.parametrize('B,Ho,Wo', [(2, 400, 667), (1, 37, 53), (2, 5, 3), (1, 540, 960)])
-@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
-def test_pool_conv1x1_pair_vs_separate(K, B, Ho, Wo, dtype):
-    """kinet_pool_conv1x1_pair (maxpool 3x3/2 + layer1[0].conv1 + bn1 + ReLU and the 64 -> 256
-    downsample + BN in one launch) against maxpool_3x3s2 followed by the two convs: the pooled
-    map is the same (max is exact), the 1x1 convs agree to one output rounding; and against
-    torch fp32 on the rounded pooled map."""
-    g = torch.Generator().manual_seed(Ho * Wo + B)
-    x = torch.relu(torch.randn(B, Ho, Wo, 64, generator=g)).to(dtype).cuda()
-    w1 = (torch.randn(64, 64, 1, 1, generator=g) * 0.15).cuda()
-    wd = (torch.randn(256, 64, 1, 1, generator=g) * 0.15).cuda()
-    s1, b1 = (torch.rand(64, generator=g) + 0.5).cuda(), (torch.randn(64, generator=g) * 0.1).cuda()
-    sd, bd = (torch.rand(256, generator=g) + 0.5).cuda(), (torch.randn(256, generator=g) * 0.1).cuda()
-    t1, idn = K.pool_conv1x1_pair(x, w1, s1, b1, wd, sd, bd)
-    xp = K.maxpool_3x3s2(x)
-    t1r = K.conv2d_nhwc(xp, K.pack_conv_weight(w1, dtype), 1, 0, scale=s1, bias=b1, relu=True)
-    idr = K.conv2d_nhwc(xp, K.pack_conv_weight(wd, dtype), 1, 0, scale=sd, bias=bd)
-    torch.cuda.synchronize()
-    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
-    for got, ref in ((t1, t1r), (idn, idr)):
-        assert got.shape == ref.shape
-        d = (got.float() - ref.float()).abs()
-        assert (d <= 2 * ulp * ref.float().abs() + 1e-3).all(), d.max().item()
-    xf = xp.float().reshape(-1, 64)
-    f1 = torch.relu(xf @ (w1.reshape(64, 64).to(dtype).float()).T * s1 + b1)
-    fd = xf @ (wd.reshape(256, 64).to(dtype).float()).T * sd + bd
-    for got, ref in ((t1, f1), (idn, fd)):
-        d = (got.float().reshape(ref.shape) - ref).abs()
-        assert (d <= 2 * ulp * ref.abs() + 1e-3).all(), d.max().item()
-
-
-@pytest.mark.parametrize('B,H,W', [(16, 100, 167), (2, 37, 53), (1, 3, 5), (3, 9, 70)])
-@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
-def test_direct_conv3x3_c128_vs_fp32(K, B, H, W, dtype):
-    """The direct 3x3 / stride 1 / pad 1, 128 -> 128 conv (csrc/conv3x3.hip conv3x3_c128_kernel,
-    opt-in through kinet_gemm_set_flags 4096: weights resident in VGPRs, 4 x 32 tiles with LDS
-    halos) and the default implicit GEMM, both against torch fp32 F.conv2d + folded BN + ReLU at
-    the config-2 stage-2 size and ragged sizes, and against each other."""
-    from kinet_amd import _native
-    g = torch.Generator().manual_seed(H * W + B + 128)
-    x = torch.relu(torch.randn(B, 128, H, W, generator=g)).to(dtype)
-    w = (torch.randn(128, 128, 3, 3, generator=g) * (2.0 / 1152) ** 0.5).to(dtype)
-    scale = torch.rand(128, generator=g) + 0.5
-    bias = torch.randn(128, generator=g) * 0.1
-    xn = x.permute(0, 2, 3, 1).contiguous().cuda()
-    wp = K.pack_conv_weight(w.cuda(), dtype)
-    y = K.conv2d_nhwc(xn, wp, 1, 1, scale=scale.cuda(), bias=bias.cuda(), relu=True)
-    old = _native.lib().kinet_gemm_set_flags(4096)
-    try:
-        y_gemm = K.conv2d_nhwc(xn, wp, 1, 1, scale=scale.cuda(), bias=bias.cuda(), relu=True)
-    finally:
-        _native.lib().kinet_gemm_set_flags(old)
-    torch.cuda.synchronize()
-    ref = F.relu(F.conv2d(x.float().cuda(), w.float().cuda(), padding=1) * scale.cuda()[None, :, None, None]
-                 + bias.cuda()[None, :, None, None])
-    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
-    for out in (y, y_gemm):
-        err = (out.permute(0, 3, 1, 2).float() - ref).abs()
-        assert (err <= 2 * ulp * ref.abs() + 1e-3).all(), err.max().item()
-    d = (y.float() - y_gemm.float()).abs()
-    assert (d <= 2 * ulp * y_gemm.float().abs() + 1e-3).all(), d.max().item()

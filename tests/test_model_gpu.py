@@ -124,6 +124,38 @@ def test_config2_bf16_deterministic(config2):
         model.set_compute_dtype(torch.float32)
 
 
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_shared_frame_pos_bit_identical(config2, dtype):
+    """Unpadded equal-size frames: the encoder projections read ONE frame's position embedding
+    for the whole batch (DeformableTransformer.share_frame_pos) -- the same bits as the per-frame
+    embedding buffer, in the timed bf16 path and the fp32 parity path; also the frames' own
+    outputs equal those of each frame run alone."""
+    from kinet_amd.models.deformable_transformer import DeformableTransformer
+    d, model = config2
+    g = torch.Generator().manual_seed(77)
+    imgs = [torch.randn(3, 160, 224, generator=g).cuda() for _ in range(3)]
+    model.set_compute_dtype(dtype)
+    try:
+        outs = {}
+        for share in (True, False):
+            DeformableTransformer.share_frame_pos = share
+            with torch.no_grad():
+                o = model(imgs)[0]
+            torch.cuda.synchronize()
+            outs[share] = {k: o[k].clone() for k in ('pred_logits', 'pred_boxes', 'hs_embed')}
+        for k in outs[True]:
+            assert torch.equal(outs[True][k], outs[False][k]), k
+        with torch.no_grad():
+            one = model(imgs[1:2])[0]
+        torch.cuda.synchronize()
+        tol = 1e-5 if dtype == torch.float32 else 2e-2
+        for k in ('pred_logits', 'pred_boxes'):
+            assert (one[k][0] - outs[True][k][1]).abs().max().item() <= tol, k
+    finally:
+        DeformableTransformer.share_frame_pos = True
+        model.set_compute_dtype(torch.float32)
+
+
 def test_tracking_multiframe_parity(golden_dir):
     d = dict(np.load(os.path.join(golden_dir, 'detr_tracking_mf_small.npz')))
     model = _build(golden_dir, 'detr_tracking_mf_small.keys.txt', 31, 'train_deformable', 'train_multi_frame',

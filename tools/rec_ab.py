@@ -3,7 +3,7 @@ logits projection GEMM -> f16 head-major offsets + logits -> kinet_msda_encoder_
 the sampling-records pipeline (kinet_msda_sample_records -> kinet_msda_encoder_forward_records).
 Times each kernel alone (HIP events, interleaved repeats) and prints the max output difference.
 
-usage: python tools/rec_ab.py [--batch 16] [--iters 30] [--reps 3] [--rec-flags 0,8192,2097152]
+usage: python tools/rec_ab.py [--batch 16] [--iters 30] [--reps 3] [--rec-flags 0]
 (--rec-flags: time the records GEMM alone under each kinet_gemm_set_flags value, interleaved)
 """
 import argparse
