@@ -106,6 +106,9 @@ def parse():
     ap.add_argument('--share-pos', type=int, default=1,
                     help='1: unpadded frames read one shared position embedding in the encoder projections '
                          '(DeformableTransformer.share_frame_pos); 0: per-frame rows (A/B)')
+    ap.add_argument('--enc-strips', type=int, default=0,
+                    help='strips per head map of the encoder sampler (kernels.msda_encoder_set_strips; 0 = the '
+                         "plan's own choice; A/B)")
     ap.add_argument('--stem-image', type=int, default=1,
                     help='1: the stem conv reads the f32 image directly (kinet_stem_conv_image); '
                          '0: pack_image_kwfold + the folded conv (A/B)')
@@ -786,6 +789,8 @@ def main():
         _native.lib().kinet_ffn_set_debug(a.ffn_knob)
     from kinet_amd import kernels as K
     K.MSDA_RECORDS[0] = bool(a.msda_records)
+    if a.enc_strips:
+        K.msda_encoder_set_strips(a.enc_strips)
     from kinet_amd.models import backbone as BB
     BB.FUSE_BOTTLENECK_PAIRS = bool(a.bneck_pairs)
     from kinet_amd.models.deformable_transformer import DeformableTransformer

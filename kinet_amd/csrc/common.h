@@ -83,8 +83,6 @@ template <> struct Acc<double> { typedef double type; };
 __device__ __forceinline__ double to_acc(double v, double*) { return v; }
 template <typename T> __device__ __forceinline__ float to_acc(T v, float*) { return to_f32(v); }
 
-// compute units of the current device (read once; 256 on MI355X) -- launchers size their
-// grids in rounds of one workgroup per CU
 // N explicit wait states pinned between two scheduling barriers.  ROCm 7.2's hazard recognizer
 // searches an MFMA result window backwards with ONE visited set shared by all predecessor
 // paths, so a window that reaches its reader through a control-flow merge or a loop back edge
@@ -99,6 +97,8 @@ __device__ __forceinline__ void mfma_window_pad() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// compute units of the current device (read once; 256 on MI355X) -- launchers size their
+// grids in rounds of one workgroup per CU
 inline int cu_count() {
     static int n = 0;
     if (n == 0) {

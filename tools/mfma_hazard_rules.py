@@ -8,6 +8,7 @@ checks the code against the same rules the compiler pads by (and reports where h
 code or a scheduling decision leaves a pair short).
 
     python tools/mfma_hazard_rules.py            # prints the table (JSON with --json)
+    python tools/mfma_hazard_rules.py --cfg-repro  # the recognizer's gap across a CFG merge
 
 Producer / consumer classes (registers: D = MFMA destination, A/B/C = MFMA sources):
   raw_valu      D -> VALU read                 waw_valu   D -> VALU write
@@ -123,10 +124,59 @@ def probe():
     return table
 
 
+CFG_REPRO = """---
+name: merge
+tracksRegLiveness: false
+machineFunctionInfo:
+  isEntryFunction: true
+body: |
+  bb.0:
+    successors: %bb.1, %bb.2
+    $vgpr0_vgpr1_vgpr2_vgpr3 = V_MFMA_F32_16X16X32_F16_vgprcd_e64 $vgpr40_vgpr41_vgpr42_vgpr43, $vgpr48_vgpr49_vgpr50_vgpr51, $vgpr64_vgpr65_vgpr66_vgpr67, 0, 0, 0, implicit $mode, implicit $exec
+    S_CBRANCH_VCCZ %bb.2, implicit $vcc
+  bb.1:
+    successors: %bb.3
+    $vgpr126 = V_MOV_B32_e32 $vgpr125, implicit $exec
+    $vgpr127 = V_MOV_B32_e32 $vgpr125, implicit $exec
+    $vgpr128 = V_MOV_B32_e32 $vgpr125, implicit $exec
+    $vgpr129 = V_MOV_B32_e32 $vgpr125, implicit $exec
+    $vgpr130 = V_MOV_B32_e32 $vgpr125, implicit $exec
+    S_BRANCH %bb.3
+  bb.2:
+    successors: %bb.3
+    $vgpr120 = V_RCP_IFLAG_F32_e32 $vgpr121, implicit $mode, implicit $exec
+  bb.3:
+    S_WAITCNT 0
+    $vgpr100 = V_ADD_F32_e32 $vgpr0, $vgpr101, implicit $mode, implicit $exec
+    S_ENDPGM 0
+...
+"""
+
+
+def cfg_repro():
+    """An MFMA, a branch, and its result read after the merge: 8 wait states via bb.1 (5 moves +
+    branch + wait), 3 via bb.2 (1 instruction).  The recognizer pads 8 - (the distance along the
+    first predecessor it searches) and never re-searches bb.0 through bb.2."""
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, 'r.mir')
+        with open(src, 'w') as f:
+            f.write(CFG_REPRO)
+        r = subprocess.run([LLC, '-mtriple=amdgcn-amd-amdhsa', '-mcpu=gfx950', '-run-pass=post-RA-hazard-rec', src,
+                            '-o', '-'], capture_output=True, text=True)
+    body = r.stdout.split('body:', 1)[1]
+    nops = re.findall(r'S_NOP (\d+)', body)
+    print(body.strip())
+    print('s_nop inserted:', nops or 'none', '-- the path through bb.2 has 3 wait states, 8 are required')
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--json', action='store_true')
+    ap.add_argument('--cfg-repro', action='store_true')
     a = ap.parse_args()
+    if a.cfg_repro:
+        cfg_repro()
+        return
     t = probe()
     if a.json:
         print(json.dumps(t, indent=1, sort_keys=True))
