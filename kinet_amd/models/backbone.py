@@ -54,10 +54,14 @@ class FrozenBatchNorm2d(nn.Module):
 
 # Block i's conv3 and block i+1's conv1 as one launch (kinet_bottleneck_pair) for the stages
 # whose bottleneck width is in FUSE_PAIR_WIDTHS; False runs every conv on its own (A/B:
-# tools/bneck_ab.py).  Layer 1 (64) only: at 128 / 256 the persistent pair kernel's row tiles
-# leave a partial last round at batch 16 and the two-launch path is faster (profiles/r04h_bneck_ab.log)
+# tools/bneck_ab.py, bench.py --pair-widths).  Round 4 kept stages 2-3 (128 / 256) as two launches:
+# at batch 16 the pair kernel's 256-row tiles left a half-empty last round
+# (profiles/r04h_bneck_ab.log).  At the round-6 bench batches (24 / 12 / 4 frames, three batches in
+# flight) the pairs win at every width: config 2 1344 / 1357 -> 1386 / 1382 frames/s, config 3
+# 616 / 613 -> 619 / 624, config 5 274 / 276 -> 282 / 282 (A B A B on one box,
+# profiles/r06c_ab_summary.txt, r06d_ab_summary.txt)
 FUSE_BOTTLENECK_PAIRS = True
-FUSE_PAIR_WIDTHS = (64,)
+FUSE_PAIR_WIDTHS = (64, 128, 256)
 # 16-bit stem straight from the f32 image (kinet_stem_conv_image); False: pack_image_kwfold +
 # the folded conv (A/B: bench.py --stem-image 0)
 STEM_FROM_IMAGE = True
