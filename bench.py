@@ -48,8 +48,10 @@ PMC_MFMA = os.path.join(HERE, 'profiles', 'pmc_mfma.json')
 WORKLOADS = {
     # batch per in-flight slot: the interleaved --batch sweeps of round 5 (profiles/r05zz_batch_sweep.txt)
     # -- config 2: 16 -> 1314-1321, 24 -> 1352-1358, 28 -> 1353-1355, 32 -> 1299-1302 frames/s;
-    # config 3: 8 -> 610-613, 12 -> 627-630, 16 -> 616; config 5: 4, 6, 8 within 1 %
-    'config2': dict(cfgs=('train_deformable',), over={}, h=800, w=1333, batch=24, streams=3, dtype='bf16',
+    # config 3: 8 -> 610-613, 12 -> 627-630, 16 -> 616; config 5: 4, 6, 8 within 1 %.  Round 6, with
+    # the bottleneck pairs at every width (profiles/r06e_batch_sweep.txt): config 2 24 -> 1366 / 1372,
+    # 28 -> 1378 / 1380, 32 -> 1338 / 1333; 24 with 4 batches in flight 1352 / 1352
+    'config2': dict(cfgs=('train_deformable',), over={}, h=800, w=1333, batch=28, streams=3, dtype='bf16',
                     K=0, desc='config2 cfgs/train_deformable.yaml: R-50 Deformable-DETR inference forward, '
                               'd=256, 4 levels, 6/6 layers, 300 queries, box refine'),
     'config3': dict(cfgs=('train_deformable', 'train_multi_frame', 'train_tracking'), over=dict(dataset='mot'),
