@@ -523,6 +523,8 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
         eager = []
         for k in range(nst):   # the eager outputs of every slot, kept to check the replays against
             o = step(k)
+            # step k ran on strs[k]: wait for it before copying its outputs on this stream
+            torch.cuda.synchronize()
             eager.append((o[0]['pred_logits'].clone(), o[0]['pred_boxes'].clone()))
         torch.cuda.synchronize()
         try:
@@ -547,7 +549,9 @@ def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype
             if same:
                 graphed, graph_check = True, 'replays bit-identical to eager (every slot)'
             else:
-                print(f'[bench] {name}: graph replay differs from eager, timing eager', file=sys.stderr)
+                diffs = [float((gouts[k][0]['pred_logits'].float() - eager[k][0].float()).abs().max()) for k in range(nst)]
+                print(f'[bench] {name}: graph replay differs from eager (max |dlogits| per slot {diffs}), timing eager',
+                      file=sys.stderr)
                 graph_check = 'replay differed from eager: timed eager'
                 del graphs, gouts
                 step = eager_step
