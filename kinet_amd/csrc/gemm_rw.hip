@@ -174,11 +174,10 @@ __device__ __forceinline__ float level_reduce(float x) {
     return MAX ? fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1])) : __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-__device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_lds, bool qmasked, int rl, int l,
+// r: the (query, level) reference point (x, y[, w, h]), qmasked: the query's mask byte, both read
+// from the tile's LDS stage by the caller
+__device__ __forceinline__ void prep_records(const GemmArgs& p, const float4 r, bool qmasked, int Hl, int Wl,
                                              const float (&v)[12], uint32_t* out) {
-    // level constants (lane-dependent level: selects, not an indexed kernel-argument load)
-    const int Hl = l == 0 ? p.prep_H[0] : l == 1 ? p.prep_H[1] : l == 2 ? p.prep_H[2] : p.prep_H[3];
-    const int Wl = l == 0 ? p.prep_W[0] : l == 1 ? p.prep_W[1] : l == 2 ? p.prep_W[2] : p.prep_W[3];
     const float Hf = (float)Hl, Wf = (float)Wl;
     const float fs = (float)(1 << p.prep_fb);
     const float mx = level_reduce<true>(fmaxf(fmaxf(v[8], v[9]), fmaxf(v[10], v[11])));
@@ -192,13 +191,11 @@ __device__ __forceinline__ void prep_records(const GemmArgs& p, const char* ref_
     const float ra = qmasked ? 0.f : __builtin_amdgcn_rcpf(es);
     float rx, ry, sx, sy;   // reference point and the offset scale of each axis
     if (p.prep_refd == 2) {
-        const float2 r = *reinterpret_cast<const float2*>(ref_lds + (rl * 4 + l) * 8);
         rx = r.x;
         ry = r.y;
         sx = __builtin_amdgcn_rcpf(Hf);   // :77-79 (offsets / spatial_shapes, (H, W) on (x, y))
         sy = __builtin_amdgcn_rcpf(Wf);
     } else {
-        const float4 r = *reinterpret_cast<const float4*>(ref_lds + (rl * 4 + l) * 16);
         rx = r.x;
         ry = r.y;
         sx = 0.125f * r.z;   // :80-82 (/ n_points * wh * 0.5, n_points = 4)
@@ -386,6 +383,18 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
         if (s < cnt) issue(s);
 
     const int cl0 = wave * NC * 4 + (lane >> 4) * NC;   // this lane's first column in the group
+    // PREP: this lane's level (lane >> 4, fixed for the launch) and its shape, selected once and
+    // pinned in VGPRs.  Selected inside the loop, the compiler turned the select chain into an
+    // indexed load from the kernel-argument segment, and that load's s_waitcnt vmcnt(0) before
+    // the epilogue also waited for the DMA of the next row tile: the ring's prefetch was exposed
+    // once per tile
+    int lvl_H = 0, lvl_W = 0;
+    if constexpr (PREP) {
+        const int l = lane >> 4;
+        lvl_H = l == 0 ? p.prep_H[0] : l == 1 ? p.prep_H[1] : l == 2 ? p.prep_H[2] : p.prep_H[3];
+        lvl_W = l == 0 ? p.prep_W[0] : l == 1 ? p.prep_W[1] : l == 2 ? p.prep_W[2] : p.prep_W[3];
+        asm volatile("" : "+v"(lvl_H), "+v"(lvl_W));
+    }
     uint32_t pend[TMR][PW] = {};
     int pend_m0 = 0;
     // packed outputs of one row tile: ALWAYS S buffer stores per lane (offsets past the
@@ -497,6 +506,20 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
             }
         }
         lds_barrier();
+        // PREP: the tile's mask bytes and reference points read BEFORE the next tile's DMA is
+        // issued: an LDS read after it gets an s_waitcnt vmcnt(0) from the compiler (it cannot
+        // prove the DMA's stage disjoint), which would wait for that DMA before the epilogue
+        float4 pref[PREP ? TMR : 1];
+        bool pmask[PREP ? TMR : 1];
+        if constexpr (PREP) {
+            const char* sc = stages + (i % NS) * C_::STAGE;
+#pragma unroll
+            for (int t = 0; t < TMR; ++t) {
+                const int rl = t * 16 + (lane & 15), l = lane >> 4;
+                pmask[t] = sc[C_::MASK_OFF + rl] != 0;
+                pref[t] = *reinterpret_cast<const float4*>(sc + C_::REF_OFF + (rl * 4 + l) * (p.prep_refd == 2 ? 8 : 16));
+            }
+        }
         store_pending(i > 0);
         if (i + NS - 1 < cnt) issue(i + NS - 1);
 
@@ -506,7 +529,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
 #pragma unroll
         for (int a = 0; a < NT; ++a)
 #pragma unroll
-            for (int t = 0; t < TMR; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int t = 0; t < TMR; ++t) {
+                // PREP: the accumulators start at the bias (one LDS read per 4 columns instead of
+                // an add per column after the K loop)
+                if constexpr (PREP) acc[a][t] = *reinterpret_cast<const f32x4*>(par + GW + cl0 + a * 4);
+                else acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
 #pragma unroll
         for (int c = 0; c < KC; ++c)
 #pragma unroll
@@ -525,9 +553,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
 #pragma unroll
             for (int t = 0; t < TMR; ++t) {
 #pragma unroll
-                for (int j = 0; j < NC; ++j) v[t][j] = acc[j >> 2][t][j & 3] + par[GW + cl0 + j];
-                prep_records(p, st + C_::REF_OFF, st[C_::MASK_OFF + t * 16 + (lane & 15)] != 0,
-                                        t * 16 + (lane & 15), lane >> 4, v[t], pend[t]);
+                for (int j = 0; j < NC; ++j) v[t][j] = acc[j >> 2][t][j & 3];
+                prep_records(p, pref[t], pmask[t], lvl_H, lvl_W, v[t], pend[t]);
             }
             pend_m0 = m0;
             continue;
@@ -868,7 +895,11 @@ extern "C" int kinet_msda_sample_records(const void* A, const void* A2, const vo
     // A2: alone the call is ~4 % slower than two workgroups with a 4-slot ring (228 vs 220 us),
     // but under the bench's three batches in flight the whole step is 0.9 % faster (1311 / 1316
     // vs 1304 / 1299 frames/s, profiles/r04z_occ_ab.log) -- the smaller LDS footprint leaves room
-    // for the other streams' workgroups.  Four per CU (128 VGPRs) spills and loses 7 %.  The
+    // for the other streams' workgroups.  Four per CU (128 VGPRs) spills and loses 7 %.  Round 6,
+    // with the per-tile DMA drain gone (the level shape hoisted, the tile's mask / reference
+    // points read before the next DMA), two workgroups with a 4- or 3-slot ring gave the same
+    // records time (275 vs 273 us) and a slower bench step (1404-1406 / 1414 vs 1416-1423 frames/s,
+    // profiles/r06i_records_ring_ab.txt)  The
     // 32-row tile (two MFMA row tiles per wave) is not used here: its epilogue, interleaved by the
     // compiler with the second tile's MFMA chain, differed from the 16-row tile in a few hundred
     // record words from run to run (round 4-5)
