@@ -24,9 +24,12 @@ def main():
     ap.add_argument('--top', type=int, default=40)
     ap.add_argument('--gemm-flags', type=int, default=0, help='kinet_gemm_set_flags value (A/B runs)')
     ap.add_argument('--filter', default='', help='only rows whose shape contains this text')
+    ap.add_argument('--ffn-knob', type=int, default=0, help='kinet_ffn_set_debug value (A/B runs)')
     a = ap.parse_args()
     if a.gemm_flags:
         _native.lib().kinet_gemm_set_flags(a.gemm_flags)
+    if a.ffn_knob:
+        _native.lib().kinet_ffn_set_debug(a.ffn_knob)
     wl = bench.WORKLOADS[a.workload]
     a.batch = a.batch or wl['batch']
     dev = torch.device('cuda', 0)
