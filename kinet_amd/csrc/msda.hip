@@ -1116,15 +1116,21 @@ __global__ __launch_bounds__(512) void msda_bwd_list_kernel(
         // phase 3 (reads only what phase 1 wrote, so no barrier before it): lane = (slot,
         // channel), consecutive lanes on consecutive channels of the pass's rows
         const int n = (dbg & 4) ? 0 : *npass;
-        for (int i = threadIdx.x; i < n * D; i += nt) {
-            const int si = i / D, c = i - si * D;
-            const int slot = plist[si];
-            float acc = 0.f;
-            for (int cid = head[slot]; cid >= 0; cid = next[cid]) {
-                const int2 ci = cinfo[cid];
-                acc += __int_as_float(ci.x) * G[ci.y + c];
+        {
+            // thread = (slot group, channel), fixed for the pass: one division per thread instead of
+            // one per (slot, channel) item (D is a run-time value): 1.05-1.10 -> 1.03 ms at the
+            // config-4 encoder call (tools/msda_bwd_probe.py --ab, profiles/r06t_bwd_phase3.txt)
+            // (D <= 64 <= nt on this path: launch_bwd takes it for nj <= 4 and 64-thread multiples)
+            const int c = threadIdx.x % D, sg = threadIdx.x / D, nsg = nt / D;
+            for (int si = sg; sg < nsg && si < n; si += nsg) {
+                const int slot = plist[si];
+                float acc = 0.f;
+                for (int cid = head[slot]; cid >= 0; cid = next[cid]) {
+                    const int2 ci = cinfo[cid];
+                    acc += __int_as_float(ci.x) * G[ci.y + c];
+                }
+                if (!(dbg & 2)) atomicAdd(gimg + (long)keys[slot] * MD + c, acc);
             }
-            if (!(dbg & 2)) atomicAdd(gimg + (long)keys[slot] * MD + c, acc);
         }
         __syncthreads();
         for (int i = threadIdx.x; i < n; i += nt) {
