@@ -465,7 +465,17 @@ def train_leg(a, dev, world):
 def run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype_name, steps, warmup):
     """Time `steps` forwards of workload `name` (WORKLOADS) after `warmup`, then trace 3 more on
     one stream.  Returns (elapsed seconds (max over ranks), trace families, MSDA launches,
-    GEMM/conv roofline split, decoder touched bytes)."""
+    GEMM/conv roofline split, decoder touched bytes).  With one batch in flight the library's
+    launch-fill policy is "solo" (kinet_set_solo_launch: partial-round shapes on smaller tiles)."""
+    from kinet_amd import _native
+    old = _native.lib().kinet_set_solo_launch(1 if max(1, streams) == 1 else 0)
+    try:
+        return _run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype_name, steps, warmup)
+    finally:
+        _native.lib().kinet_set_solo_launch(old)
+
+
+def _run_workload(a, name, dev, world, rank, batch, streams, height, width, dtype_name, steps, warmup):
     from kinet_amd import _native
     from kinet_amd.models import nested_tensor_from_tensor_list
     wl = WORKLOADS[name]

@@ -130,6 +130,16 @@ int kinet_stem_conv_image(const float* img, const void* w_packed, const float* s
  * NOT reach the backward kernels launched through autograd (only forward / direct calls). */
 int kinet_gemm_set_flags(int flags);
 
+/* Launch-fill policy (no reference counterpart), process-wide.  1 = "solo": the caller keeps one
+ * batch in flight, so no other stream's work fills CUs a launch leaves idle -- shapes whose
+ * default tiles cover under 60 % of one round of workgroups per CU (config 5's stage-3 3x3
+ * convolutions and D = 256 bottleneck pairs, M = 32,640 rows) switch to tiles half as tall that
+ * fill the chip: config 5 on one stream 239 -> 257 frames/s.  0 (default) = throughput mode:
+ * with several batches in flight the other streams fill those CUs and the taller tiles' better
+ * per-CU efficiency wins (config 5 on 3 streams 294 vs 290 frames/s).  Same outputs bit for bit
+ * either way.  Returns the previous policy. */
+int kinet_set_solo_launch(int on);
+
 #ifdef __cplusplus
 }
 #endif

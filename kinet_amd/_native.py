@@ -35,6 +35,7 @@ _SIGS = {
     'kinet_msda_encoder_forward_records': [P, I64, I64, P, P, I, P] + [I] * 8 + [P, P],
     'kinet_msda_fused_forward': [P, I64, I64, I64, P, P, I, P, I, P, P, P, P] + [I] * 10 + [P, P],
     'kinet_gemm_set_flags': [I],
+    'kinet_set_solo_launch': [I],
     'kinet_gemm_force_tile': [I, I],
     'kinet_gemm_headmajor': [P, P, P] + [I] * 7 + [P, P, I, I, P],
     'kinet_gemm_headmajor_ex': [P, P, P, P] + [I] * 7 + [P, P, I, I, I, P],

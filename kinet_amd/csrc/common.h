@@ -97,6 +97,10 @@ __device__ __forceinline__ void mfma_window_pad() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// launch-fill policy (kinet_set_solo_launch, defined in gemm.hip): 1 = one batch in flight, so
+// launches size their tiles to fill the chip on their own; 0 = throughput mode (default)
+extern int kinet_solo_launch;
+
 // compute units of the current device (read once; 256 on MI355X) -- launchers size their
 // grids in rounds of one workgroup per CU
 inline int cu_count() {

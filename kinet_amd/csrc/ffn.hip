@@ -44,7 +44,8 @@ struct FfnArgs {
     int dbg;   // diagnostic knobs (kinet_ffn_set_debug): 1 = no weight DMA after the prologue
                // (timing only, results are garbage); 2 = the 4-wave x 32-row tile at D = 256;
                // 8 = the 8-wave x 16-row tile (default: 8 waves x 32 rows, ffn_fused_rt2_kernel);
-               // 16 = kinet_bottleneck_pair at D = 64 on the LDS-ring kernel (bneck_pair_kernel)
+               // 16 = kinet_bottleneck_pair at D = 64 on the LDS-ring kernel (bneck_pair_kernel);
+               // 128 / 256 = kinet_bottleneck_pair at D = 128 / 256 on 1- / 2-row-tile waves
 };
 
 thread_local int ffn_debug = 0;   // test-only knob (kinet_ffn_set_debug), per calling thread
@@ -940,8 +941,30 @@ int launch_pair(const PairArgs& a, int D, int DB, hipStream_t s) {
                 hipLaunchKernelGGL((bneck64_kernel<T, 64, 8>), dim3(nb < 512 ? nb : 512), dim3(512), 0, s, a, nt);
             }
             break;
-        case 128: launch_pair_cfg<T, 128, 2, 8, 1>(a, s); break;
-        case 256: launch_pair_cfg<T, 256, 2, 8, 1>(a, s); break;
+        case 128:
+        case 256: {
+            // one or two 16-row tiles per wave (128- or 256-row workgroup tiles; the same sums per
+            // element either way): the 2-tile tile reads each weight fragment once for two MFMAs,
+            // but with one batch in flight (kinet_set_solo_launch), when its tiles fill their rounds
+            // of one workgroup per CU 1.5x worse than the 1-tile grid, the 1-tile grid wins --
+            // config 5's stage-3 pairs (M = 32,640: 128 vs 255 tiles on 256 CUs) 84.7 -> 62.9 us
+            // alone (profiles/r06aa_config5_shapes.txt); on 3 streams the other batches fill the
+            // idle CUs (neutral, profiles/r06ab_solo_launch_ab.txt).
+            // ffn_debug 128 / 256 force the 1- / 2-tile grid (tests, A/B)
+            const int cus = cu_count();
+            const long t2 = (a.M + 255) / 256, t1 = (a.M + 127) / 128;
+            const double e2 = (double)t2 / (double)(((t2 + cus - 1) / cus) * cus);
+            const double e1 = (double)t1 / (double)(((t1 + cus - 1) / cus) * cus);
+            const bool one = (ffn_debug & 128) || (!(ffn_debug & 256) && kinet_solo_launch && e1 > 1.5 * e2);
+            if (D == 128) {
+                if (one) launch_pair_cfg<T, 128, 1, 8, 1>(a, s);
+                else launch_pair_cfg<T, 128, 2, 8, 1>(a, s);
+            } else {
+                if (one) launch_pair_cfg<T, 256, 1, 8, 1>(a, s);
+                else launch_pair_cfg<T, 256, 2, 8, 1>(a, s);
+            }
+            break;
+        }
         default: return KINET_ERR_ARG;
     }
     return KINET_OK;

@@ -46,6 +46,7 @@ namespace {
 // test / A-B selection knobs (kinet_gemm_set_flags, kinet_gemm_force_tile): per calling thread,
 // never read by default paths except as "0 = automatic"
 thread_local int kinet_gemm_flags = 0;   // declared in gemm_common.h (read by grad.hip too)
+int kinet_solo_launch = 0;                 // declared in common.h (kinet_set_solo_launch)
 namespace {
 // diagnostic tile override for gemm_kernel (kinet_gemm_force_tile; 0 = heuristic)
 thread_local int force_bm = 0, force_bn = 0;
@@ -600,7 +601,17 @@ int launch(const GemmArgs& a, hipStream_t stream) {
             if (mfull > mt_all) mfull = mt_all;
             // less than one round but at least half of one: a single partial round of 8-wave
             // tiles still beats the 4-wave grid (layer-4 3x3 at batch 16: 119 vs 128 us)
-            if (mfull == 0 && mt_all * nN8 >= 128) mfull = mt_all;
+            if (mfull == 0 && mt_all * nN8 >= 128) {
+                // ... unless one batch is in flight (kinet_set_solo_launch), it fills less than 60 %
+                // of the CUs and 128 x 256 tiles (twice as many, same 8-wave main loop, same sums)
+                // fill them better: config 5's stage-3 3x3 convs (M = 32,640, N = 256: 128 vs 255
+                // tiles) 74.8 -> 48.5 us alone (profiles/r06aa_config5_shapes.txt), but -1 % on 3
+                // streams, whose other batches fill the idle CUs (profiles/r06ab_solo_launch_ab.txt)
+                const long t128 = (long)((a.M + 127) / 128) * nN8;
+                if (kinet_solo_launch && mt_all * nN8 * 10 < 256L * 6 && t128 <= 256)
+                    return run(a, 128, 256, (a.M + 127) / 128);
+                mfull = mt_all;
+            }
             // a remainder of more than a quarter round: the partly filled last round of 8-wave
             // tiles beats the 4-wave tail (layer-3 3x3 at batch 24: 394 m-tiles = 256 + 138,
             // 140 vs 151 us, profiles/r05f2_conv24.log); flag 8388608 keeps the split (A/B)
@@ -885,6 +896,12 @@ extern "C" int kinet_gemm_force_tile(int bm, int bn) {
     force_bm = bm;
     force_bn = bn;
     return KINET_OK;
+}
+
+extern "C" int kinet_set_solo_launch(int on) {
+    const int old = kinet_solo_launch;
+    kinet_solo_launch = on ? 1 : 0;
+    return old;
 }
 
 extern "C" int kinet_gemm_set_flags(int flags) {

@@ -70,6 +70,14 @@ def cached_multi(tensors, tag, make):
     return v
 
 
+def set_solo_launch(on):
+    """Launch-fill policy of the library (include/kinet_gemm.h kinet_set_solo_launch): True when
+    the caller keeps ONE batch in flight (latency mode: partial-round shapes run smaller tiles
+    that fill the chip alone), False (default) when several streams overlap.  Outputs are the
+    same bit for bit either way.  Returns the previous policy."""
+    return bool(N.lib().kinet_set_solo_launch(1 if on else 0))
+
+
 def param_rows(p, start, end):
     """A stable (cached) row-slice view of a parameter, so its dtype cast is cached too."""
     return cached(p, ('rows', start, end), lambda t: t.detach()[start:end])

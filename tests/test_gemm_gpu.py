@@ -677,6 +677,7 @@ def test_ffn_fused_no_norm_and_errors(K):
     (16, 50, 84, 256, 256, 3, 1, 1),    # 263 tiles of 256x256: one full round + a 4-wave remainder launch
     (8, 50, 84, 256, 256, 3, 1, 1),     # 132 tiles: one partial round of 8-wave tiles
     (16, 25, 42, 512, 512, 3, 1, 1),    # layer-4 3x3 (N = 2 tile columns)
+    (4, 68, 120, 256, 256, 3, 1, 1),    # config-5 stage 3: 128 tiles of 256x256 -> 255 of 128x256
 ])
 def test_conv_full_rounds_split_vs_fp32(K, B, H, W, Cin, Cout, k, s, p):
     """Multi-tap convs split into whole rounds of 8-wave 256x256 tiles + the remainder rows on
@@ -906,6 +907,56 @@ def test_bottleneck_pair64_kernels_bit_identical(K, M):
         _native.lib().kinet_ffn_set_debug(old)
     torch.cuda.synchronize()
     assert torch.equal(y0, y1) and torch.equal(t0, t1)
+
+
+@pytest.mark.parametrize('D,M', [(128, 5), (128, 32640), (256, 5), (256, 1000), (256, 32640), (256, 117600)])
+def test_bottleneck_pair_row_tiles_bit_identical(K, D, M):
+    """At D = 128 / 256 the pair runs one or two 16-row tiles per wave (chosen by how well the
+    tiles fill rounds of one workgroup per CU; kinet_ffn_set_debug 128 / 256 force either): the
+    same sums per element, so bit-identical y and t; the automatic choice runs under
+    kinet_set_solo_launch 1 (the only mode that picks the 1-tile grid by itself)."""
+    from kinet_amd import _native
+    g = torch.Generator().manual_seed(M + D)
+    F_ = 4 * D
+    x = torch.relu(torch.randn(M, 1, 1, D, generator=g)).bfloat16().cuda()
+    res = torch.randn(M, 1, 1, F_, generator=g).bfloat16().cuda()
+    w3 = (torch.randn(F_, D, 1, 1, generator=g) * (2.0 / D) ** 0.5).cuda()
+    w1 = (torch.randn(D, F_, 1, 1, generator=g) * (2.0 / F_) ** 0.5).cuda()
+    s3, b3 = (torch.rand(F_, generator=g) + 0.5).cuda(), (torch.randn(F_, generator=g) * 0.1).cuda()
+    s1, b1 = (torch.rand(D, generator=g) + 0.5).cuda(), (torch.randn(D, generator=g) * 0.1).cuda()
+    packed = K.bottleneck_pack(w3, w1, s3, s1, torch.bfloat16)
+    outs = []
+    for knob, solo in ((0, 0), (0, 1), (128, 0), (256, 0)):
+        old, old_solo = _native.lib().kinet_ffn_set_debug(knob), _native.lib().kinet_set_solo_launch(solo)
+        try:
+            outs.append(K.bottleneck_pair(x, res, packed, b3, b1))
+        finally:
+            _native.lib().kinet_ffn_set_debug(old)
+            _native.lib().kinet_set_solo_launch(old_solo)
+    torch.cuda.synchronize()
+    for y, t in outs[1:]:
+        assert torch.equal(outs[0][0], y) and torch.equal(outs[0][1], t)
+
+
+@pytest.mark.parametrize('B,H,W', [(4, 68, 120), (8, 50, 84)])
+def test_conv_partial_round_tiles_bit_identical(K, B, H, W):
+    """With one batch in flight (kinet_set_solo_launch 1) a multi-tap conv whose 256x256 tiles
+    would fill under 60 % of one round runs 128x256 tiles instead (csrc/gemm.hip): the same K
+    order per element, so bit-identical outputs to the default 256x256 round."""
+    from kinet_amd import _native
+    g = torch.Generator().manual_seed(B * H * W)
+    x = torch.randn(B, H, W, 256, generator=g).bfloat16().cuda()
+    w = (torch.randn(256, 256, 3, 3, generator=g) * (2.0 / 2304) ** 0.5).bfloat16().cuda()
+    scale, bias = (torch.rand(256, generator=g) + 0.5).cuda(), (torch.randn(256, generator=g) * 0.1).cuda()
+    wp = K.pack_conv_weight(w, torch.bfloat16)
+    y0 = K.conv2d_nhwc(x, wp, 1, 1, scale=scale, bias=bias, relu=True)
+    old = _native.lib().kinet_set_solo_launch(1)
+    try:
+        y1 = K.conv2d_nhwc(x, wp, 1, 1, scale=scale, bias=bias, relu=True)
+    finally:
+        _native.lib().kinet_set_solo_launch(old)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
 
 
 @pytest.mark.parametrize('B,H,W,N', [(16, 200, 334, 512), (2, 67, 81, 256), (1, 64, 64, 512)])
