@@ -489,42 +489,59 @@ __global__ __launch_bounds__(512) void ffn_fused_rt2_kernel(const FfnArgs p, con
                     h1[rt] = bb1;
                 }
             }
+            // Fragments are read ahead of their MFMAs: phase A's two k-steps ahead, phase B's four
+            // fragments ahead, the first four issued during phase A's last two k-steps (so the
+            // ReLU / rounding between the phases overlaps their latency).  The scheduling barriers
+            // keep the compiler from sinking the reads back next to their uses, where each pair of
+            // MFMAs waited for its own LDS round trip: 593-599 -> 566-569 us per batch-28 encoder
+            // FFN, bit-identical (profiles/r06af_ffn_prefetch_ab.txt; 3 or 6 ahead: the same time)
+            auto frag = [&](int f) { return *reinterpret_cast<const u32x4*>(wb + lane * 16 + f * 1024); };
+            constexpr int PDA = 2, PDB = 4;
+            static_assert(KS >= PDA && NT >= PDB, "prefetch depths");
+            u32x4 fa[KS][2], fw[NT];
+#pragma unroll
+            for (int i = 0; i < PDA; ++i) {
+                fa[i][0] = frag(i);
+                fa[i][1] = frag(KS + i);
+            }
             // phase A: H^T chunk (32 hidden x 32 rows) = W1c x^T + b1
-            u32x4 fa0 = *reinterpret_cast<const u32x4*>(wb + lane * 16);
-            u32x4 fa1 = *reinterpret_cast<const u32x4*>(wb + lane * 16 + KS * 1024);
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                u32x4 na0 = fa0, na1 = fa1;
-                if (ks + 1 < KS) {
-                    na0 = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (ks + 1) * 1024);
-                    na1 = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (KS + ks + 1) * 1024);
+                if (ks + PDA < KS) {
+                    fa[ks + PDA][0] = frag(ks + PDA);
+                    fa[ks + PDA][1] = frag(KS + ks + PDA);
+                } else {   // phase B's first PDB reads, spread over phase A's last PDA k-steps
+                    const int t = ks + PDA - KS;
+#pragma unroll
+                    for (int j = t * PDB / PDA; j < (t + 1) * PDB / PDA; ++j) fw[j] = frag(2 * KS + j);
                 }
 #pragma unroll
                 for (int rt = 0; rt < RT; ++rt) {
-                    Mma<T>::run(h0[rt], fa0, xr[rt][ks]);
-                    Mma<T>::run(h1[rt], fa1, xr[rt][ks]);
+                    Mma<T>::run(h0[rt], fa[ks][0], xr[rt][ks]);
+                    Mma<T>::run(h1[rt], fa[ks][1], xr[rt][ks]);
                 }
-                fa0 = na0;
-                fa1 = na1;
+                __builtin_amdgcn_sched_barrier(0);
             }
-            // ReLU + round: the B operand of phase B (hidden order as kinet_ffn_pack permuted W2)
+            // ReLU + round: the B operand of phase B (hidden order as kinet_ffn_pack permuted W2).
+            // ReLU as a signed-integer max on the bit pattern (one VALU op; fmaxf on an MFMA
+            // result costs a canonicalising max first): the same value for every finite input
+            auto relu = [](float v) { return __builtin_bit_cast(float, max(__builtin_bit_cast(int, v), 0)); };
             u32x4 hb[RT];
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
-                hb[rt][0] = pack2<T>(fmaxf(h0[rt][0], 0.f), fmaxf(h0[rt][1], 0.f));
-                hb[rt][1] = pack2<T>(fmaxf(h0[rt][2], 0.f), fmaxf(h0[rt][3], 0.f));
-                hb[rt][2] = pack2<T>(fmaxf(h1[rt][0], 0.f), fmaxf(h1[rt][1], 0.f));
-                hb[rt][3] = pack2<T>(fmaxf(h1[rt][2], 0.f), fmaxf(h1[rt][3], 0.f));
+                hb[rt][0] = pack2<T>(relu(h0[rt][0]), relu(h0[rt][1]));
+                hb[rt][1] = pack2<T>(relu(h0[rt][2]), relu(h0[rt][3]));
+                hb[rt][2] = pack2<T>(relu(h1[rt][0]), relu(h1[rt][1]));
+                hb[rt][3] = pack2<T>(relu(h1[rt][2]), relu(h1[rt][3]));
             }
+            __builtin_amdgcn_sched_barrier(0);
             // phase B: out^T += W2c H^T, each W2 fragment feeding both row tiles
-            u32x4 fw = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (2 * KS) * 1024);
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
-                u32x4 nw = fw;
-                if (nt + 1 < NT) nw = *reinterpret_cast<const u32x4*>(wb + lane * 16 + (2 * KS + nt + 1) * 1024);
+                if (nt + PDB < NT) fw[nt + PDB] = frag(2 * KS + nt + PDB);
 #pragma unroll
-                for (int rt = 0; rt < RT; ++rt) Mma<T>::run(acc[rt][nt], fw, hb[rt]);
-                fw = nw;
+                for (int rt = 0; rt < RT; ++rt) Mma<T>::run(acc[rt][nt], fw[nt], hb[rt]);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
         // ---- tile epilogue (as ffn_fused_kernel): + b2 + residual x, LayerNorm, 16-byte stores ----
