@@ -173,24 +173,39 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN == 4 ? 2 : 1) void gemm_d
 #pragma unroll
         for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // The K-step's two 32-deep halves: the second half's fragments are read while the first
+    // half's MFMAs run -- its TN weight fragments right at the start, its TM activation fragments
+    // one by one as the first half retires each activation fragment (row-fragment-outer MFMA
+    // order) -- so only the K-step's first reads wait out an LDS round trip.  Scheduling barriers
+    // keep the compiler from sinking the reads back next to their uses.  Same MFMAs per
+    // accumulator in the same order (bit-identical).  256x256 tiles: within noise (two waves
+    // per SIMD already cover it); 256x128 / 128x256: 4-8 % faster (profiles/r06ai_gemm_dma_prefetch_ab.txt)
     auto compute = [&](int slot) {
         const char* xl = lds + slot * STAGE;
         const char* wl = xl + BM * ROWB;
+        auto xfrag = [&](int kk, int t) {
+            return Mma<T>::frag(*reinterpret_cast<const u32x4*>(xl + swz(wm * WTM + t * 16 + (lane & 15), kk * 4 + (lane >> 4))));
+        };
+        auto wfrag = [&](int kk, int t) {
+            return Mma<T>::frag(*reinterpret_cast<const u32x4*>(wl + swz(wn * WTN + t * 16 + (lane & 15), kk * 4 + (lane >> 4))));
+        };
+        typename Mma<T>::Frag bfr[2][TM], afr[2][TN];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int ch = kk * 4 + (lane >> 4);
-            typename Mma<T>::Frag bfr[TM], afr[TN];
+        for (int t = 0; t < TN; ++t) afr[0][t] = wfrag(0, t);
 #pragma unroll
-            for (int t = 0; t < TM; ++t)
-                bfr[t] = Mma<T>::frag(*reinterpret_cast<const u32x4*>(xl + swz(wm * WTM + t * 16 + (lane & 15), ch)));
+        for (int t = 0; t < TM; ++t) bfr[0][t] = xfrag(0, t);
 #pragma unroll
-            for (int t = 0; t < TN; ++t)
-                afr[t] = Mma<T>::frag(*reinterpret_cast<const u32x4*>(wl + swz(wn * WTN + t * 16 + (lane & 15), ch)));
+        for (int t = 0; t < TN; ++t) afr[1][t] = wfrag(1, t);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int a = 0; a < TN; ++a)
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-                for (int b = 0; b < TM; ++b) Mma<T>::run(acc[a][b], afr[a], bfr[b]);
-        }
+            for (int b = 0; b < TM; ++b) {
+#pragma unroll
+                for (int a = 0; a < TN; ++a) Mma<T>::run(acc[a][b], afr[kk][a], bfr[kk][b]);
+                if (kk == 0) bfr[1][b] = xfrag(1, b);
+                __builtin_amdgcn_sched_barrier(0);
+            }
     };
 
     stage(0);
