@@ -726,7 +726,11 @@ void launch_t(const GemmArgs& a, hipStream_t stream) {
     if (a.K == 288) {
         const bool r = a.R != nullptr, ln = a.ln_g != nullptr;
         if (a.A2 != nullptr) {
-            launch_288<T, TO, false, false, true, 4>(a, stream);
+            // x + pos rows (the d = 288 offsets / logits and value projections): one 8-wave group of
+            // up to 384 columns per row tile, so each tile's x + pos rows are read once -- as the
+            // records GEMM (kinet_msda_sample_records); flag 268435456: the 4-wave 192-column groups
+            if (a.N > 192 && a.N <= 384 && !(kinet_gemm_flags & 268435456)) launch_288<T, TO, false, false, true, 8, 3, 1>(a, stream);
+            else launch_288<T, TO, false, false, true, 4>(a, stream);
             return;
         }
         // LayerNorm rows: 9 waves x 32 columns (one 288-column group; flag 4194304: the 6-wave x
@@ -891,18 +895,26 @@ extern "C" int kinet_msda_sample_records(const void* A, const void* A2, const vo
     }
     hipStream_t s = (hipStream_t)stream;
     constexpr int NS1 = ring_depth<8, 16, false, false, false, 3, true>();
-    // three workgroups per CU (159 VGPRs, a 2-slot ring: 39 KiB of LDS each) when the tile adds
-    // A2: alone the call is ~4 % slower than two workgroups with a 4-slot ring (228 vs 220 us),
-    // but under the bench's three batches in flight the whole step is 0.9 % faster (1311 / 1316
-    // vs 1304 / 1299 frames/s, profiles/r04z_occ_ab.log) -- the smaller LDS footprint leaves room
-    // for the other streams' workgroups.  Four per CU (128 VGPRs) spills and loses 7 %.  Round 6,
-    // with the per-tile DMA drain gone (the level shape hoisted, the tile's mask / reference
-    // points read before the next DMA), two workgroups with a 4- or 3-slot ring gave the same
-    // records time (275 vs 273 us) and a slower bench step (1404-1406 / 1414 vs 1416-1423 frames/s,
-    // profiles/r06i_records_ring_ab.txt)  The
-    // 32-row tile (two MFMA row tiles per wave) is not used here: its epilogue, interleaved by the
-    // compiler with the second tile's MFMA chain, differed from the 16-row tile in a few hundred
-    // record words from run to run (round 4-5)
+    // With the position embedding added on load (A2, the encoder): ONE 8-wave 384-column group per
+    // 16-row tile, one workgroup per CU (166 VGPRs, a 4-slot ring): each row tile's x + pos rows
+    // are read once.  The two 4-wave 192-column groups before it (three workgroups per CU, a
+    // 2-slot ring) were meant to share each row tile through the XCD's L2 (same XCD by linear id),
+    // but PMC showed 1.11 GB fetched per batch-28 call against ~0.35 GB of operands: 270 -> 238 us
+    // per call, encoder call 0.72-0.74 -> 0.69-0.70 ms, bench 1416 / 1429 -> 1441 / 1446 frames/s
+    // interleaved, records bit-identical (profiles/r06am_records_8wave_ab.txt; two 8-wave groups per
+    // CU: 245 us, 1435 / 1445).  Flag 268435456 keeps the 4-wave groups (A/B, tests).  Round 4's
+    // notes on the 4-wave grid: three per CU beat two with a 4-slot ring under three streams
+    // (profiles/r04z_occ_ab.log), four per CU spilled.  The 32-row tile (two MFMA row tiles per
+    // wave) is not used here: its epilogue, interleaved by the compiler with the second tile's
+    // MFMA chain, differed from the 16-row tile in a few hundred record words from run to run
+    // (round 4-5)
+    if (A2 && !(kinet_gemm_flags & 268435456)) {
+        constexpr int NS8 = ring_depth<8, 16, false, false, true, 3, true, 8, 160 * 1024>();
+        if (in_dtype == KINET_BF16) launch_cfg<bf16_t, f16_t, 8, 16, NS8, false, false, true, 3, false, true, 1, 8>(a, s);
+        else launch_cfg<f16_t, f16_t, 8, 16, NS8, false, false, true, 3, false, true, 1, 8>(a, s);
+        KINET_LAUNCH_CHECK();
+        return KINET_OK;
+    }
     if (in_dtype == KINET_BF16) {
         if (A2) launch_cfg<bf16_t, f16_t, 8, 16, 2, false, false, true, 3, false, true, 3>(a, s);
         else launch_cfg<bf16_t, f16_t, 8, 16, NS1, false, false, false, 3, false, true>(a, s);

@@ -503,6 +503,22 @@ def test_rw288_matches_tiled_kernel(K, gemm_flags, M, N, mode):
     assert (d == 0).float().mean().item() > 0.9
 
 
+@pytest.mark.parametrize('M,N,mode', [(8200, 384, 'add'), (8200, 384, 'add_f32'), (20011, 288, 'add'), (4099, 200, 'add')])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_rw288_add_group_variants_bit_identical(K, gemm_flags, M, N, mode, dtype):
+    """K = 288 with the second operand added on load and 192 < N <= 384: one 8-wave group of up
+    to 384 columns per row tile (default) vs two 4-wave 192-column groups (flag 268435456): the
+    same products in the same K order per column, so bit-identical."""
+    x, w, b, kw, _ = _rw_case(M, N, 288, mode, 5, dtype)
+    args = (x.cuda(), w.cuda(), b.cuda())
+    gemm_flags(0)
+    y8 = K.linear(*args, **kw)
+    gemm_flags(268435456)
+    y4 = K.linear(*args, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(y8, y4)
+
+
 @pytest.mark.parametrize('M,N,mode', [(10001, 288, 'res_ln_mask'), (20011, 288, 'res_ln'), (8197, 280, 'res_ln'),
                                       (9001, 288, 'ln')])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])

@@ -706,6 +706,28 @@ def test_sample_records_vs_oracle(shapes, noise, ref_dim, masked):
     assert dmax <= 2.0 ** -fb * 2 * np.abs(v).max() + 2e-3 and dmean <= 1e-5, (dmax, dmean)
 
 
+@pytest.mark.parametrize('shapes', [((100, 167), (50, 84), (25, 42), (13, 21)), ((25, 40), (15, 20), (8, 10), (4, 5))])
+@pytest.mark.parametrize('ref_dim,masked', [(2, False), (2, True), (4, False)])
+def test_sample_records_group_variants_bit_identical(shapes, ref_dim, masked):
+    """The records GEMM with the position embedding added on load runs one 8-wave 384-column
+    group per row tile (default) or two 4-wave 192-column groups (kinet_gemm_set_flags
+    268435456): the same K order and epilogue per record, so bit-identical records."""
+    from kinet_amd import _native
+    from kinet_amd import kernels as K
+    B, M = 3, 8
+    x, pos, w, bias, ref, qmask, _ = _record_problem(shapes, B, 3.0, 7, ref_dim, masked)
+    args = (x.cuda(), w.cuda(), bias.cuda(), M, ref.cuda(), shapes)
+    kw = dict(x_add=pos.cuda(), query_attn_mask=qmask.cuda() if masked else None)
+    r8, _ = K.msda_sample_records(*args, **kw)
+    old = _native.lib().kinet_gemm_set_flags(268435456)
+    try:
+        r4, _ = K.msda_sample_records(*args, **kw)
+    finally:
+        _native.lib().kinet_gemm_set_flags(old)
+    torch.cuda.synchronize()
+    assert torch.equal(r8, r4)
+
+
 @pytest.mark.parametrize('shapes', [
     ((100, 167), (50, 84), (25, 42), (13, 21)),    # config 2 (800x1333): level 0 gathered, 1-3 staged
     ((60, 70), (40, 50), (45, 50), (10, 13)),      # wide level 2: levels 2-3 staged
