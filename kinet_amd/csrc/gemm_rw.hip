@@ -752,7 +752,13 @@ void launch_t(const GemmArgs& a, hipStream_t stream) {
     if (a.K == 64) launch_k<T, TO, 2>(a, stream);
     else if (a.K == 128) launch_k<T, TO, 4>(a, stream);
     else if (a.K == 256) launch_k<T, TO, 8>(a, stream);
-    else launch_ring<T, TO, 16, false, false, false, 2>(a, stream);   // K == 512
+    else if (a.N > 128 && a.N <= 256 && !(kinet_gemm_flags & 268435456)) {
+        // K == 512, N == 256 (config 2's level-0 input projection, 512 -> 256): one 8-wave
+        // 256-column group per row tile, one workgroup per CU, so each tile's 1 KiB rows are read
+        // once (the two 4-wave 128-column groups fetched 2x the operand, profiles/pmc_traffic.json)
+        constexpr int NS = ring_depth<16, 16, false, false, false, 2, false, 8, 160 * 1024>();
+        launch_cfg<T, TO, 16, 16, NS, false, false, false, 2, false, false, 1, 8>(a, stream);
+    } else launch_ring<T, TO, 16, false, false, false, 2>(a, stream);   // K == 512
 }
 
 bool al16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }

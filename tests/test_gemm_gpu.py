@@ -503,6 +503,24 @@ def test_rw288_matches_tiled_kernel(K, gemm_flags, M, N, mode):
     assert (d == 0).float().mean().item() > 0.9
 
 
+@pytest.mark.parametrize('M,N,mode', [(20011, 256, 'plain'), (8197, 200, 'relu'), (9000, 256, 'f32')])
+def test_rw512_group_variants_bit_identical(K, gemm_flags, M, N, mode):
+    """K = 512 with 128 < N <= 256 (config 2's level-0 input projection): one 8-wave 256-column
+    group per row tile (default) vs two 4-wave 128-column groups (flag 268435456): the same
+    products in the same K order per column, so bit-identical."""
+    x, w, b, kw, ref = _rw_case(M, N, 512, mode, 3, torch.bfloat16)
+    args = (x.cuda(), w.cuda(), b.cuda())
+    gemm_flags(0)
+    y8 = K.linear(*args, **kw)
+    gemm_flags(268435456)
+    y4 = K.linear(*args, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(y8, y4)
+    err = (y8.float().cpu() - ref).abs()
+    tol = (1e-4 * ref.abs() + 2e-3) if 'f32' in mode else (1e-2 * ref.abs() + 2e-2)
+    assert (err <= tol).all(), err.max().item()
+
+
 @pytest.mark.parametrize('M,N,mode', [(8200, 384, 'add'), (8200, 384, 'add_f32'), (20011, 288, 'add'), (4099, 200, 'add')])
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
 def test_rw288_add_group_variants_bit_identical(K, gemm_flags, M, N, mode, dtype):
