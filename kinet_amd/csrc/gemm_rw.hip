@@ -712,8 +712,19 @@ void launch_k(const GemmArgs& a, hipStream_t stream) {
         if (r || ln) return;
         launch_ring<T, TO, KC, false, false, true, NT>(a, stream);
     } else if (r && ln) launch_ring<T, TO, KC, true, true, false, NT>(a, stream);
-    else if (r) launch_ring<T, TO, KC, true, false, false, NT>(a, stream);
-    else if (ln) launch_ring<T, TO, KC, false, true, false, NT>(a, stream);
+    else if (r) {
+        // + residual with N > 256 (the stage-end conv3s, 128 -> 512 and 256 -> 1024): 8-wave
+        // 512-column groups, one workgroup per CU, so each row tile's x rows are fetched by half as
+        // many groups (one instead of two at N = 512); flag 268435456: the 4-wave 256-column groups
+        if constexpr (NT == 4 && KC <= 8) {
+            if (a.N > 256 && !(kinet_gemm_flags & 268435456)) {
+                constexpr int NS8 = ring_depth<KC, 16, true, false, false, 4, false, 8, 160 * 1024>();
+                launch_cfg<T, TO, KC, 16, NS8, true, false, false, 4, false, false, 1, 8>(a, stream);
+                return;
+            }
+        }
+        launch_ring<T, TO, KC, true, false, false, NT>(a, stream);
+    } else if (ln) launch_ring<T, TO, KC, false, true, false, NT>(a, stream);
     else launch_ring<T, TO, KC, false, false, false, NT>(a, stream);
 }
 

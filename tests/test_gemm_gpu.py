@@ -503,6 +503,24 @@ def test_rw288_matches_tiled_kernel(K, gemm_flags, M, N, mode):
     assert (d == 0).float().mean().item() > 0.9
 
 
+@pytest.mark.parametrize('M,N,Kd,mode', [(20011, 512, 128, 'res_relu'), (8197, 1024, 256, 'res_relu'),
+                                         (9000, 512, 64, 'res_mask'), (4099, 400, 128, 'res')])
+def test_rw_res_group_variants_bit_identical(K, gemm_flags, M, N, Kd, mode):
+    """+ residual with N > 256 (the stage-end conv3s): 8-wave 512-column groups (default) vs
+    4-wave 256-column groups (flag 268435456): the same products and epilogue per column, so
+    bit-identical."""
+    x, w, b, kw, ref = _rw_case(M, N, Kd, mode, 11, torch.bfloat16)
+    args = (x.cuda(), w.cuda(), b.cuda())
+    gemm_flags(0)
+    y8 = K.linear(*args, **kw)
+    gemm_flags(268435456)
+    y4 = K.linear(*args, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(y8, y4)
+    err = (y8.float().cpu() - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
+
+
 @pytest.mark.parametrize('M,N,mode', [(20011, 256, 'plain'), (8197, 200, 'relu'), (9000, 256, 'f32')])
 def test_rw512_group_variants_bit_identical(K, gemm_flags, M, N, mode):
     """K = 512 with 128 < N <= 256 (config 2's level-0 input projection): one 8-wave 256-column
