@@ -725,6 +725,8 @@ void launch_k(const GemmArgs& a, hipStream_t stream) {
         }
         launch_ring<T, TO, KC, true, false, false, NT>(a, stream);
     } else if (ln) launch_ring<T, TO, KC, false, true, false, NT>(a, stream);
+    // (plain epilogues keep the 4-wave groups: 8-wave 512-column groups ran config 2's six decoder
+    // value projections (N = 1536) slower, 669 vs 648 us, profiles/r06ar_wide_8wave_ab.txt)
     else launch_ring<T, TO, KC, false, false, false, NT>(a, stream);
 }
 
@@ -755,6 +757,11 @@ void launch_t(const GemmArgs& a, hipStream_t stream) {
             else launch_288<T, TO, false, true, false, 9, 2>(a, stream);
         } else if (r) {
             launch_288<T, TO, true, false, false, 4>(a, stream);
+        } else if (a.N > 384 && !(kinet_gemm_flags & 268435456)) {
+            // N > 384 (the d = 288 decoder's six value projections in one launch, N = 1728): 8-wave
+            // 384-column groups, one workgroup per CU -- half as many groups fetch each row tile:
+            // 1048 -> 948 us in config 3 (profiles/r06ar_wide_8wave_ab.txt)
+            launch_288<T, TO, false, false, false, 8, 3, 1>(a, stream);
         } else {
             launch_288<T, TO, false, false, false, 4>(a, stream);
         }

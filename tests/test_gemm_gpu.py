@@ -503,6 +503,31 @@ def test_rw288_matches_tiled_kernel(K, gemm_flags, M, N, mode):
     assert (d == 0).float().mean().item() > 0.9
 
 
+@pytest.mark.parametrize('M,N,Kd,mode', [(9001, 1728, 288, 'plain'), (4099, 500, 288, 'relu'), (8197, 400, 288, 'relu_mask')])
+def test_rw_wide_group_variants_bit_identical(K, gemm_flags, M, N, Kd, mode):
+    """K = 288 plain epilogues with N > 384 (the d = 288 decoder's six value projections in one
+    launch): 8-wave 384-column groups (default) vs 4-wave groups (flag 268435456), row-major and
+    head-major stores: bit-identical."""
+    x, w, b, kw, ref = _rw_case(M, N, Kd, mode, 12, torch.bfloat16)
+    args = (x.cuda(), w.cuda(), b.cuda())
+    gemm_flags(0)
+    y8 = K.linear(*args, **kw)
+    gemm_flags(268435456)
+    y4 = K.linear(*args, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(y8, y4)
+    err = (y8.float().cpu() - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
+    if mode == 'plain':
+        hd = 36
+        gemm_flags(0)
+        h8 = K.value_proj_headmajor(x.cuda().view(1, M, Kd), w.cuda(), b.cuda(), hd)
+        gemm_flags(268435456)
+        h4 = K.value_proj_headmajor(x.cuda().view(1, M, Kd), w.cuda(), b.cuda(), hd)
+        torch.cuda.synchronize()
+        assert torch.equal(h8, h4)
+
+
 @pytest.mark.parametrize('M,N,Kd,mode', [(20011, 512, 128, 'res_relu'), (8197, 1024, 256, 'res_relu'),
                                          (9000, 512, 64, 'res_mask'), (4099, 400, 128, 'res')])
 def test_rw_res_group_variants_bit_identical(K, gemm_flags, M, N, Kd, mode):
