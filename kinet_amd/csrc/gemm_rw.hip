@@ -760,7 +760,8 @@ void launch_t(const GemmArgs& a, hipStream_t stream) {
         } else if (a.N > 384 && !(kinet_gemm_flags & 268435456)) {
             // N > 384 (the d = 288 decoder's six value projections in one launch, N = 1728): 8-wave
             // 384-column groups, one workgroup per CU -- half as many groups fetch each row tile:
-            // 1048 -> 948 us in config 3 (profiles/r06ar_wide_8wave_ab.txt)
+            // 1048 -> 948 us in config 3 (profiles/r06ar_wide_8wave_ab.txt); at 192 < N <= 384 (the
+            // value projection's split planes) 89 vs 91 us, bench within noise: not taken (r06at)
             launch_288<T, TO, false, false, false, 8, 3, 1>(a, stream);
         } else {
             launch_288<T, TO, false, false, false, 4>(a, stream);
