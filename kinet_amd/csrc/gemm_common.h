@@ -35,6 +35,9 @@ struct GemmArgs {
     // first, C + hm_split*hm_batch*hm_rows, as ((g*hm_batch + b)*hm_rows + s)*hm_d2 + d with
     // n - hm_split = g*hm_d2 + d -- the head_dim-36 MSDA value as a 32-channel plane + a 4-channel plane
     int hm_split, hm_d2;
+    // 1 = the resident-weight kernel's 32-column head-major stores go through its LDS transpose
+    // (gemm_rw.hip; set by launch_rw from kinet_gemm_flags, never by callers)
+    int hm_tr;
     int M, N, K, lda, ldb, ldc, ldr, relu;
     // split-K (gemm_kernel only): blockIdx.y = K slice of kchunk elements, whose f32 partial
     // tile goes to C + blockIdx.y * c_slice (no epilogue; splitk_finalize applies it)

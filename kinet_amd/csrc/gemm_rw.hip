@@ -455,7 +455,41 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
         for (int t = 0; t < TMR; ++t)
             s_lo[t][h] = ((unsigned)(t * 16 + (lane & 15)) * r_s + colpart) * (unsigned)sizeof(TO);
     }
+    // head-major outputs of 32-column heads (the d = 256 value projections): each wave's 16 x 64
+    // output block is 2 heads; transposed through LDS (the pending tile's ring slot, free after the
+    // tile's barrier until the next DMA is issued into it) so each store instruction writes one
+    // head plane's 16 rows x 64 B = 1 KiB contiguous instead of 8-byte pieces 64 B apart
+    constexpr bool HM32_OK = !PREP && !LN && sizeof(TO) == 2 && NC == 16 && WPU == 4 && TMR * 2048 * NW <= C_::STAGE;
+    const bool hm32 = HM32_OK && p.hm_tr && p.hm_rows && p.hm_d == 32 && !p.hm_split && N % 64 == 0;
+    int pend_slot = 0;
     auto store_pending = [&](bool valid) {
+        if constexpr (HM32_OK) {
+            if (hm32) {
+                if (!valid) return;   // nothing pending (and pend_slot may be the slot about to be computed)
+                char* scr = stages + pend_slot * C_::STAGE + wave * (TMR * 2048);
+                const int g = lane >> 4, r = lane & 15;
+#pragma unroll
+                for (int t = 0; t < TMR; ++t) {
+                    char* b = scr + t * 2048 + (g >> 1) * 1024 + r * 64 + (g & 1) * 32;
+                    *reinterpret_cast<u32x4*>(b) = u32x4{pend[t][0], pend[t][1], pend[t][2], pend[t][3]};
+                    *reinterpret_cast<u32x4*>(b + 16) = u32x4{pend[t][4], pend[t][5], pend[t][6], pend[t][7]};
+                }
+                const int hg0 = (ncol0 + wave * 64) >> 5;
+                const bool wok = ncol0 + wave * 64 < N;
+#pragma unroll
+                for (int t = 0; t < TMR; ++t)
+#pragma unroll
+                    for (int hl = 0; hl < 2; ++hl) {
+                        const u32x4 w = *reinterpret_cast<const u32x4*>(scr + t * 2048 + hl * 1024 + lane * 16);
+                        const int row = pend_m0 + t * 16 + (lane >> 2);
+                        const unsigned off = (wok && row < M) ? (((unsigned)(hg0 + hl) * (unsigned)M + (unsigned)row) * 32u +
+                                                                 (unsigned)(lane & 3) * 8u) * 2u
+                                                              : OOB;
+                        __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 0);
+                    }
+                return;
+            }
+        }
         if constexpr (PREP) {
             const unsigned base = (unsigned)pend_m0 * (unsigned)rs * (unsigned)sizeof(TO);
 #pragma unroll
@@ -521,6 +555,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
             }
         }
         store_pending(i > 0);
+        if (hm32) lds_barrier();   // every wave done with its transpose scratch (the slot refilled below)
         if (i + NS - 1 < cnt) issue(i + NS - 1);
 
         const char* st = stages + (i % NS) * C_::STAGE;
@@ -638,8 +673,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_rw_kernel(const GemmArgs p,
             for (int j4 = 0; j4 < NC / 4; ++j4) Pack<TO>::put(&pend[t][j4 * Pack<TO>::WORDS_PER_4], &v[t][j4 * 4]);
         }
         pend_m0 = m0;
+        pend_slot = i % NS;
     }
-    if (cnt > 0) store_pending(true);
+    if (cnt > 0) {
+        if (hm32) lds_barrier();   // the last tile's slot: every wave done reading it
+        store_pending(true);
+    }
 }
 
 template <typename T, typename TO, int KC, int BMR, int NS, bool HAS_R, bool LN, bool HAS_A2 = false, int NT = 4,
@@ -813,6 +852,7 @@ bool launch_rw(const GemmArgs& a, int in_dtype, int out_dtype, hipStream_t strea
     if (cb >= (1LL << 31)) return false;
     GemmArgs ac = a;
     ac.c_bytes = (int)cb;
+    ac.hm_tr = (kinet_gemm_flags & 1073741824) ? 0 : 1;   // flag: 32-column head-major stores without the LDS transpose (A/B)
     if (in_dtype == KINET_BF16) {
         if (out_dtype == KINET_F16) launch_t<bf16_t, f16_t>(ac, stream);
         else if (o16) launch_t<bf16_t, bf16_t>(ac, stream);

@@ -503,6 +503,28 @@ def test_rw288_matches_tiled_kernel(K, gemm_flags, M, N, mode):
     assert (d == 0).float().mean().item() > 0.9
 
 
+@pytest.mark.parametrize('M,N', [(20011, 256), (9001, 1536), (4103, 512), (8200, 256)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_rw_headmajor32_transpose_bit_identical(K, gemm_flags, M, N, dtype):
+    """32-column head-major stores of the resident-weight kernel through its LDS transpose (one
+    1 KiB head-plane piece per store, the default) vs the direct 16-byte unit stores (flag
+    1073741824): the same values at the same places, ragged row counts included; and against fp32."""
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(1, M, 256, generator=g).to(dtype)
+    w = (torch.randn(N, 256, generator=g) / 16).to(dtype)
+    b = torch.randn(N, generator=g)
+    mask = torch.rand(1, M, generator=g) < 0.1
+    gemm_flags(0)
+    y0 = K.value_proj_headmajor(x.cuda(), w.cuda(), b.cuda(), 32, row_mask=mask.cuda())
+    gemm_flags(1073741824)
+    y1 = K.value_proj_headmajor(x.cuda(), w.cuda(), b.cuda(), 32, row_mask=mask.cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    ref = F.linear(x.float(), w.float(), b).masked_fill(mask[..., None], 0).view(1, M, N // 32, 32).permute(2, 0, 1, 3)
+    err = (y0.float().cpu() - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 2e-2).all(), err.max().item()
+
+
 @pytest.mark.parametrize('M,N,Kd,mode', [(9001, 1728, 288, 'plain'), (4099, 500, 288, 'relu'), (8197, 400, 288, 'relu_mask')])
 def test_rw_wide_group_variants_bit_identical(K, gemm_flags, M, N, Kd, mode):
     """K = 288 plain epilogues with N > 384 (the d = 288 decoder's six value projections in one
