@@ -124,8 +124,11 @@ int kinet_stem_conv_image(const float* img, const void* w_packed, const float* s
  * resident-weight streaming kernel; bit 8 (256): keep K = 512 problems off it (the
  * tiled kernel, as before round 3); bit 1024: never the direct 3x3 64 -> 64 channel
  * convolution (the implicit GEMM instead); bit 2048: strided 1x1 convolutions (the stage-2
- * downsample) on the implicit-GEMM kernel instead of the resident-weight conv-row kernel.
- * Returns the previous flags.  Per CALLING THREAD: torch
+ * downsample) on the implicit-GEMM kernel instead of the resident-weight conv-row kernel;
+ * bit 268435456: the resident-weight kernel's 4-wave column groups everywhere (round 6 runs the
+ * x + pos projections, K = 512 / N = 256, residual N > 256 and K = 288 N > 384 launches on
+ * 8-wave groups); bit 1073741824: 32-column head-major stores without the LDS transpose.
+ * All of these select among bit-identical kernels.  Returns the previous flags.  Per CALLING THREAD: torch
  * runs autograd backward for device tensors on its own engine thread, so flags set here do
  * NOT reach the backward kernels launched through autograd (only forward / direct calls). */
 int kinet_gemm_set_flags(int flags);
