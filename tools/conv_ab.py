@@ -3,6 +3,7 @@ heuristic vs forced tiles (kinet_gemm_force_tile) and the LDS-DMA staging of the
 (kinet_gemm_set_flags 16).  HIP-event timing over --iters launches; outputs checked against the
 heuristic's.  python tools/conv_ab.py [--iters 20]"""
 import argparse
+import time
 import os
 import sys
 
@@ -35,9 +36,12 @@ def main():
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         fl = 2.0 * B * Ho * Wo * Cout * k * k * Cin
         ref = None
-        for _ in range(10):   # warm the clocks before the first (heuristic) variant is timed
+        # warm the clocks before the first (heuristic) variant is timed: 10 launches left the first
+        # variant of the first shape ~15 % slow (profiles/r06ak_conv128_tiles.txt); ~0.3 s of work
+        t_end = time.perf_counter() + 0.3
+        while time.perf_counter() < t_end:
             K.conv2d_nhwc(x, wp, s, p)
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
         for name, flags, tile in variants:
             L.kinet_gemm_set_flags(flags)
             L.kinet_gemm_force_tile(*tile)
